@@ -1,0 +1,42 @@
+"""Loaders for the two in-tree native modules.
+
+``native()``  -> host C++ module (built on demand with g++; needed by CPU tests too).
+``hip()``     -> HIP kernel module ``_C``; on a machine with a GPU a missing/broken module is a hard error (no silent
+                 eager fallback), on a CPU-only machine callers get a clear RuntimeError.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_native = None
+_hip = None
+
+
+def native():
+    global _native
+    if _native is None:
+        with _lock:
+            if _native is None:
+                from . import _build
+                if not os.path.exists(_build.native_path()):
+                    _build.build_native(verbose=False)
+                _native = importlib.import_module(__package__ + "._native")
+    return _native
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                from . import _build
+                if not os.path.exists(_build.hip_path()):
+                    if os.environ.get("CFL_NO_JIT_BUILD"):
+                        raise RuntimeError("HIP extension _C is not built (run __graft_entry__.build())")
+                    _build.build_hip(verbose=True)
+                import torch  # noqa: F401  (libtorch must be loaded before _C)
+                _hip = importlib.import_module(__package__ + "._C")
+    return _hip

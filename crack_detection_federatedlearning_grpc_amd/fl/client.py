@@ -1,0 +1,213 @@
+"""FL client driver loop.
+
+Reference: fl_client.py:77-175 (``send_message``). Same verb sequence - READY -> PARAM -> TRAINING -> train ->
+loop { TRAIN_DONE -> RESP_ACY: poll VERSION until NOT_WAIT | RESP_ARY: TRAINING + train | FIN: exit } - with:
+* FIN handled while polling (the reference polls forever);
+* server-side long-poll (``wait_s`` in the VERSION config) instead of blind 20 s sleeps;
+* RPC deadlines + retry with backoff (reference has none, §5.3);
+* optional RCCL data plane: the weighted all-reduce runs between the clients on their GPUs
+  (``parallel/rccl.py``); gRPC carries control only and rank 0 uploads the averaged model for the server's copy.
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+import time
+from typing import Callable, Dict, List, Optional, Protocol
+
+import grpc
+import numpy as np
+
+from ..config import FLConfig
+from . import codec
+from . import proto as P
+from .rpc import TransportServiceStub, channel_options
+
+
+class LocalTrainer(Protocol):
+    n_samples: int
+
+    def set_weights(self, arrays: List[np.ndarray]) -> None: ...
+
+    def get_weights(self) -> List[np.ndarray]: ...
+
+    def train_round(self, current_round: int) -> Dict[str, float]: ...
+
+
+def _one(msg):
+    yield msg
+
+
+class FLClient:
+    def __init__(self, cfg: FLConfig, trainer_factory: Callable[[], LocalTrainer], name: Optional[str] = None,
+                 target: Optional[str] = None, aggregator_factory: Optional[Callable[[Dict], object]] = None):
+        self.cfg = cfg
+        self.trainer_factory = trainer_factory
+        self.name = name or f"client{random.randint(1, 100000)}"     # fl_client.py:26
+        self.target = target or f"{cfg.host}:{cfg.port}"
+        self.aggregator_factory = aggregator_factory
+        self.aggregator = None
+        self.trainer: Optional[LocalTrainer] = None
+        self.history: List[Dict] = []
+        self.info: Dict[str, object] = {}
+        self.final_state = ""
+
+    # -- transport helpers ---------------------------------------------------------------------------
+    def _call(self, stub, req) -> "P.transportResponse":
+        delay = 0.5
+        for attempt in range(self.cfg.rpc_retries + 1):
+            try:
+                last = None
+                for rep in stub.transport(_one(req), timeout=self.cfg.rpc_timeout_s):
+                    last = rep
+                return last
+            except grpc.RpcError as e:
+                code = e.code() if hasattr(e, "code") else None
+                if code not in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED) or \
+                        attempt == self.cfg.rpc_retries:
+                    raise
+                time.sleep(delay)
+                delay = min(delay * 2, 10.0)
+
+    def _ready(self, stub):
+        req = P.transportRequest(ready_req=P.ReadyReq(type="R", cname=self.name, state=P.ON,
+                                                     config={"current_round": P.Scalar(scint32=0)}))
+        return self._call(stub, req).ready_rep.config
+
+    def _params(self, stub) -> bytes:
+        return self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="P"))).update_rep.buffer_chunk
+
+    def _training(self, stub) -> None:
+        self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="T", cname=self.name, state=P.TRAINING)))
+
+    def _train_done(self, stub, cr: int, payload: bytes, n: int):
+        req = P.transportRequest(update_req=P.UpdateReq(type="D", buffer_chunk=payload, state=P.TRAIN_DONE,
+                                                        cname=self.name, current_round=cr, file_len=int(n)))
+        return self._call(stub, req).update_rep
+
+    def _version(self, stub, mv: int, cr: int, wait_s: float):
+        req = P.transportRequest(version_req=P.VersionReq(type="P", config={
+            "model_version": P.Scalar(scint32=mv), "current_round": P.Scalar(scint32=cr),
+            "wait_s": P.Scalar(scfloat=float(wait_s))}))
+        return self._call(stub, req).version_rep
+
+    def send_logs(self, stub, root: Optional[str] = None) -> int:
+        """fl_client.py:34-50 (call site commented out in the reference, :110-118)."""
+        root = root or self.cfg.log_dir
+        sent = 0
+        chunk = self.cfg.log_chunk_mb * 1024 * 1024
+        for dirpath, _, files in os.walk(root):
+            for fn in sorted(files):
+                full = os.path.join(dirpath, fn)
+                title = "./send_logs/" + os.path.relpath(full, os.path.dirname(root.rstrip("/")) or ".")
+
+                def gen():
+                    with open(full, "rb") as f:
+                        while True:
+                            piece = f.read(chunk)
+                            if not piece:
+                                return
+                            yield P.transportRequest(update_req=P.UpdateReq(type="L", buffer_chunk=piece,
+                                                                            title=title, file_len=len(piece)))
+                for _ in stub.transport(gen(), timeout=self.cfg.rpc_timeout_s):
+                    pass
+                sent += 1
+        return sent
+
+    # -- local work ------------------------------------------------------------------------------------
+    def _train(self, cr: int) -> None:
+        if self.cfg.fault_drop_round and cr >= self.cfg.fault_drop_round:
+            print(f"[{self.name}] fault injection: dropping out at round {cr}")
+            raise SystemExit(3)
+        t0 = time.perf_counter()
+        m = self.trainer.train_round(cr)
+        m = dict(m, round=cr, client=self.name, train_s=time.perf_counter() - t0)
+        self.history.append(m)
+        if self.cfg.client_weight_file:   # trainer -> driver hand-off file (client_fit_model.py:238-240)
+            codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
+
+    def _payload(self) -> bytes:
+        arrays = self.trainer.get_weights()
+        n = getattr(self.trainer, "n_samples", 0)
+        if self.aggregator is not None:
+            arrays = self.aggregator.average(arrays, n)          # weighted all-reduce over RCCL
+            if self.aggregator.rank != 0:
+                return b""
+        if self.cfg.fault_corrupt:
+            return b"\x80corrupt" + os.urandom(64)
+        return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype)
+
+    def _apply(self, blob: bytes) -> None:
+        if self.aggregator is not None or not blob:
+            return                      # RCCL mode: local weights already hold the all-reduced average
+        self.trainer.set_weights(codec.decode(blob)[0])
+
+    # -- main loop ------------------------------------------------------------------------------------------
+    def run(self) -> str:
+        with grpc.insecure_channel(self.target, options=channel_options(self.cfg.max_message_mb)) as ch:
+            stub = TransportServiceStub(ch)
+            print(f"### Ready Client ### {self.name}")
+            conf = self._ready(stub)
+            if conf["state"].scstring != "SW":
+                print(f"[{self.name}] registration closed ({conf['state'].scstring}); exiting")
+                self.final_state = conf["state"].scstring
+                return self.final_state
+            cr = conf["current_round"].scint32
+            mtr = conf["max_train_round"].scint32
+            mv = conf["model_version"].scint32
+            self.info = {k: (v.scstring or v.scint32 or v.scfloat) for k, v in conf.items()}
+            if "world_size" in conf and self.aggregator_factory is not None:
+                self.aggregator = self.aggregator_factory(self.info)
+            print("### Request Global Model Parameter ###")
+            self.trainer = self.trainer_factory()
+            self.trainer.set_weights(codec.decode(self._params(stub))[0])
+            self._training(stub)
+            self._train(cr)
+            while cr <= mtr:
+                print(f"### Deliver model state: TRAIN DONE to server ### round {cr}")
+                if self.cfg.fault_delay_s:
+                    time.sleep(self.cfg.fault_delay_s)
+                rep = self._train_done(stub, cr, self._payload(), getattr(self.trainer, "n_samples", 0))
+                st = rep.config["state"].scstring
+                print(f"### Received from state {st} ###")
+                if st == "RESP_ACY":
+                    while True:
+                        vr = self._version(stub, mv, cr, self.cfg.long_poll_s)
+                        if vr.state == P.NOT_WAIT:
+                            cr = vr.config["current_round"].scint32
+                            mv = vr.config["model_version"].scint32
+                            self._apply(vr.buffer_chunk)
+                            self._training(stub)
+                            self._train(cr)
+                            break
+                        if vr.state == P.FIN:
+                            cr = vr.config["current_round"].scint32
+                            mv = vr.config["model_version"].scint32
+                            self.final_state = "FIN"
+                            break
+                        time.sleep(min(self.cfg.poll_period_s, 1.0) if self.cfg.long_poll_s > 0
+                                   else self.cfg.poll_period_s)
+                    if self.final_state == "FIN":
+                        break
+                elif st == "RESP_ARY":
+                    self._training(stub)
+                    cr = rep.config["current_round"].scint32
+                    mv = rep.config["model_version"].scint32
+                    self._apply(rep.buffer_chunk)
+                    self._train(cr)
+                elif st == "FIN":
+                    cr = rep.config["current_round"].scint32
+                    mv = rep.config["model_version"].scint32
+                    self.final_state = "FIN"
+                    break
+                else:
+                    print(f"[{self.name}] unexpected state {st!r}; exiting")
+                    self.final_state = st
+                    break
+            if self.cfg.upload_logs:
+                self.send_logs(stub)
+            print("all training finish")
+            if self.aggregator is not None:
+                self.aggregator.close()
+            return self.final_state or "FIN"

@@ -1,0 +1,240 @@
+"""FL server: gRPC servicer over the locked ``RoundState``.
+
+Reference: fl_server.py. Same single bidi-stream RPC and verbs (dispatcher fl_server.py:152-207):
+  ready_req.type  'R'          -> registration (SW/CTW)                              :154-157
+  update_req.type 'P'          -> global parameters                                  :158-161
+  update_req.type 'T'          -> training ack (used here as a heartbeat)            :162-169
+  update_req.type 'L'          -> log-file chunk upload (appends; reference truncates, §A7)   :170-175
+  update_req.type 'D'          -> TRAIN_DONE + weights -> RESP_ACY / RESP_ARY(+params) / FIN  :176-196
+  version_req.type 'P'         -> WAIT / NOT_WAIT(+params) / FIN                     :197-207
+Extra READY reply keys (ignored by reference clients): ``rank``, ``world_size``, ``dist_addr``, ``dist_port``,
+``data_plane`` - the server doubles as the RCCL rendezvous for on-node GPU clients.
+``UpdateReq.file_len`` on a 'D' request carries the client's sample count n_k for weighted FedAvg.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from concurrent import futures
+from typing import Callable, Dict, Optional
+
+import grpc
+import numpy as np
+
+from ..config import FLConfig
+from ..models.spec import ParamTable
+from . import codec
+from . import proto as P
+from .rpc import TransportServiceServicer, add_TransportServiceServicer_to_server, channel_options
+from .state import CTW, FIN, NOT_WAIT, RESP_ACY, RESP_ARY, SW, WAIT, RoundRecord, RoundState
+
+
+def _scalar(v) -> "P.Scalar":
+    if isinstance(v, bool):
+        return P.Scalar(scint32=int(v))
+    if isinstance(v, int):
+        return P.Scalar(scint32=v)
+    if isinstance(v, float):
+        return P.Scalar(scfloat=v)
+    return P.Scalar(scstring=str(v))
+
+
+def _cfg(d: Dict[str, object]):
+    return {k: _scalar(v) for k, v in d.items()}
+
+
+class FLServer(TransportServiceServicer):
+    def __init__(self, cfg: FLConfig, global_flat: Optional[np.ndarray] = None, table: Optional[ParamTable] = None,
+                 evaluator: Optional[Callable[[np.ndarray], Dict[str, float]]] = None):
+        self.cfg = cfg
+        self.table = table or ParamTable()
+        start_round, version = 0, cfg.initial_model_version
+        if global_flat is None:
+            global_flat = self.table.init_flat(cfg.seed)
+        if cfg.resume and cfg.snapshot_dir:
+            snap = load_snapshot(cfg.snapshot_dir, self.table)
+            if snap is not None:
+                global_flat, start_round, version = snap
+                print(f"[fl_server] resumed from snapshot: round {start_round}, version {version}")
+        self.evaluator = evaluator
+        self.state = RoundState(global_flat, max_rounds=cfg.max_rounds, register_window_s=cfg.register_window_s,
+                                num_clients=cfg.num_clients, initial_version=version,
+                                weighted=(cfg.aggregation == "weighted"), round_deadline_s=cfg.round_deadline_s,
+                                quorum=cfg.quorum, start_round=start_round, on_aggregate=self._on_aggregate)
+        self._blob_lock = threading.Lock()
+        self._blob_cache: Dict[int, bytes] = {}
+        self.server: Optional[grpc.Server] = None
+        self.port: Optional[int] = None
+        self.dist_port = 0
+        self.done = threading.Event()
+        self.log_root = os.path.abspath(os.path.join(cfg.work_dir, "."))
+
+    # -- parameters --------------------------------------------------------------------------------
+    def send_parameter(self) -> bytes:
+        """fl_server.py:23-24 (``eval_model.get_weights(made_model)``) - here the current global average."""
+        with self.state.cv:
+            v, flat = self.state.model_version, self.state.global_flat
+        with self._blob_lock:
+            blob = self._blob_cache.get(v)
+            if blob is None:
+                blob = codec.encode(self.table.to_list(flat), self.cfg.codec, wire_dtype=self.cfg.wire_dtype)
+                self._blob_cache = {v: blob}
+            return blob
+
+    def global_weights(self):
+        with self.state.cv:
+            return self.table.to_list(self.state.global_flat)
+
+    def _on_aggregate(self, st: RoundState, rec: RoundRecord) -> None:
+        dt = rec.t_end - rec.t_start
+        print(f"[fl_server] round {rec.round} aggregated over {len(rec.clients)} client(s) "
+              f"(n={[int(n) for n in rec.n_samples]}) in {dt:.2f}s -> version {st.model_version}"
+              + (" (FIN)" if st.finished else ""))
+        if self.cfg.server_weight_file:   # reference: ./server_weights/weights.pickle (fl_server.py:104-105)
+            codec.save_weight_file(os.path.join(self.cfg.work_dir, self.cfg.server_weight_file)
+                                   if not os.path.isabs(self.cfg.server_weight_file) else self.cfg.server_weight_file,
+                                   self.table.to_list(st.global_flat))
+        if self.cfg.snapshot_dir:
+            save_snapshot(self.cfg.snapshot_dir, self.table, st.global_flat, st.current_round, st.model_version,
+                          st.finished)
+        if self.evaluator is not None:   # fl_server.py:27-37 (dead code in the reference)
+            res = self.evaluator(st.global_flat)
+            print(f"[fl_server] Evaluate Loss : {res.get('loss')} Evaluate Accuracy : {res.get('accuracy')}")
+        if st.finished:
+            self.done.set()
+
+    # -- RPC ---------------------------------------------------------------------------------------
+    def transport(self, request_iterator, context):
+        opened = set()
+        for req in request_iterator:
+            if req.ready_req.type == "R":
+                yield self._ready(req.ready_req)
+            elif req.update_req.type == "P":
+                yield P.transportResponse(update_rep=P.UpdateRep(type="P", buffer_chunk=self.send_parameter(),
+                                                                title="parameters"))
+            elif req.update_req.type == "T":
+                self.state.heartbeat(req.update_req.cname)
+                yield P.transportResponse(update_rep=P.UpdateRep(type="T"))
+            elif req.update_req.type == "L":
+                self._save_chunk(req.update_req.title, req.update_req.buffer_chunk, opened)
+                yield P.transportResponse(update_rep=P.UpdateRep(type="L", title=req.update_req.title))
+            elif req.update_req.type == "D":
+                yield self._train_done(req.update_req, context)
+            elif req.version_req.type == "P":
+                yield self._version(req.version_req)
+            else:
+                yield P.transportResponse()
+
+    def _ready(self, r):
+        client_round = r.config["current_round"].scint32 if "current_round" in r.config else 0
+        if self.cfg.ready_stall_s > 0:
+            time.sleep(self.cfg.ready_stall_s)      # fl_server.py:56 (kept for compat; presets set 0)
+        conf = self.state.ready(r.cname, client_round)
+        if conf["state"] == SW:
+            print(f"### Check Train Round ### {r.cname} registered as rank {conf['rank']}")
+            conf["model_type"] = self.cfg.model_type
+            conf["data_plane"] = self.cfg.data_plane
+            if self.cfg.data_plane == "rccl":
+                conf["world_size"] = self.state.wait_window_closed(timeout=self.cfg.register_window_s + 5)
+                conf["dist_port"] = self.dist_port
+                conf["dist_addr"] = "127.0.0.1"
+        return P.transportResponse(ready_rep=P.ReadyRep(config=_cfg(conf)))
+
+    def _train_done(self, u, context):
+        print(f"### Start rounds management ### {u.cname} round {u.current_round}")
+        flat = None
+        n = float(u.file_len)
+        if u.buffer_chunk:
+            try:
+                arrays, hdr = codec.decode(u.buffer_chunk)
+                flat = self.table.from_list(arrays)
+                n = float(hdr.get("n_samples") or n or 1.0)
+            except Exception as e:
+                print(f"[fl_server] rejected payload from {u.cname}: {e}")
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad weight payload: {e}")
+        try:
+            state, conf = self.state.submit(u.cname, u.current_round, flat, max(n, 1.0))
+        except ValueError as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        conf = dict(conf, state=state)
+        print(f"### Current state: {state} ###")
+        chunk = self.send_parameter() if state == RESP_ARY else b""
+        return P.transportResponse(update_rep=P.UpdateRep(type="D", buffer_chunk=chunk, config=_cfg(conf)))
+
+    def _version(self, v):
+        mv = v.config["model_version"].scint32 if "model_version" in v.config else 0
+        cr = v.config["current_round"].scint32 if "current_round" in v.config else 0
+        wait = v.config["wait_s"].scfloat if "wait_s" in v.config else 0.0
+        state, conf = self.state.version(mv, cr, min(wait, self.cfg.long_poll_s))
+        if state == NOT_WAIT:
+            return P.transportResponse(version_rep=P.VersionRep(state=P.NOT_WAIT, buffer_chunk=self.send_parameter(),
+                                                                config=_cfg(conf)))
+        if state == FIN:
+            return P.transportResponse(version_rep=P.VersionRep(state=P.FIN, config=_cfg(conf)))
+        return P.transportResponse(version_rep=P.VersionRep(state=P.WAIT, config=_cfg(conf)))
+
+    def _save_chunk(self, title: str, chunk: bytes, opened: set) -> None:
+        """fl_server.py:84-89, with append for multi-chunk files (§A7) and no path escape."""
+        rel = title[11:] if title.startswith("./send_logs") else title.lstrip("./")
+        dest = os.path.abspath(os.path.join(self.log_root, rel.lstrip("/")))
+        if not dest.startswith(self.log_root + os.sep):
+            raise ValueError(f"log path escapes the server directory: {title}")
+        os.makedirs(os.path.dirname(dest), exist_ok=True)
+        with open(dest, "ab" if dest in opened else "wb") as f:
+            f.write(chunk)
+        opened.add(dest)
+
+    # -- lifecycle -----------------------------------------------------------------------------------
+    def start(self, port: Optional[int] = None) -> int:
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=self.cfg.server_threads),
+                                  options=channel_options(self.cfg.max_message_mb))
+        add_TransportServiceServicer_to_server(self, self.server)
+        port = self.cfg.port if port is None else port
+        self.port = self.server.add_insecure_port(f"{self.cfg.bind}:{port}")
+        self.server.start()
+        return self.port
+
+    def stop(self, grace: float = 0.5) -> None:
+        self.state.stop()
+        if self.server is not None:
+            self.server.stop(grace)
+
+    def serve_forever(self, exit_on_fin: bool = True) -> None:
+        try:
+            while True:
+                if exit_on_fin and self.done.wait(1.0):
+                    time.sleep(2.0)   # let the last clients collect FIN
+                    break
+                if not exit_on_fin:
+                    time.sleep(3600)
+        except KeyboardInterrupt:
+            pass
+        finally:
+            self.stop(0)
+
+
+# -- snapshot / resume ---------------------------------------------------------------------------------
+def save_snapshot(d: str, table: ParamTable, flat: np.ndarray, current_round: int, version: int,
+                  finished: bool) -> None:
+    from ..ckpt.h5 import save_weights_h5
+    os.makedirs(d, exist_ok=True)
+    h5 = os.path.join(d, "global.h5")
+    save_weights_h5(h5 + ".tmp", table, flat)
+    os.replace(h5 + ".tmp", h5)
+    st = {"current_round": current_round, "model_version": version, "finished": finished, "time": time.time()}
+    with open(os.path.join(d, "state.json.tmp"), "w") as f:
+        json.dump(st, f)
+    os.replace(os.path.join(d, "state.json.tmp"), os.path.join(d, "state.json"))
+
+
+def load_snapshot(d: str, table: ParamTable):
+    from ..ckpt.h5 import load_weights_h5
+    sp = os.path.join(d, "state.json")
+    if not os.path.exists(sp):
+        return None
+    with open(sp) as f:
+        st = json.load(f)
+    flat = load_weights_h5(os.path.join(d, "global.h5"), table)
+    return flat, int(st["current_round"]), int(st["model_version"])

@@ -1,0 +1,162 @@
+"""Local fit loop of one FL client (the reference's ``learning_fit``, client_fit_model.py:46-240).
+
+Per round (``train_round``), as the reference does at client_fit_model.py:152-174, 225-240:
+  * fresh Adam state (the reference rebuilds + recompiles the model every round, :155-157)
+  * ``epochs`` passes over the training split, Keras Sequence semantics: ``len = n // batch`` (remainder dropped,
+    :27-28) and batch order shuffled every epoch (Keras ``fit(shuffle=True)`` on a Sequence)
+  * validation pass per epoch (``validation_data=val_gen``, :166)
+  * at ``predict_round`` run prediction + crack contour analysis (:235-237; fixed)
+The numeric work is delegated to a backend: ``HipBackend`` (models/engine.py, MI355X) or ``RefBackend`` (fp32
+PyTorch oracle, CPU plumbing config).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, List, Optional, Protocol
+
+import numpy as np
+
+from ..config import FLConfig
+from ..data.synthetic import CrackDataset
+from ..models.spec import ParamTable
+
+
+class StepBackend(Protocol):
+    def set_flat(self, flat: np.ndarray) -> None: ...
+
+    def get_flat(self) -> np.ndarray: ...
+
+    def reset_optimizer(self) -> None: ...
+
+    def train_batches(self, batches: np.ndarray) -> Dict[str, float]: ...
+
+    def eval_batches(self, batches: np.ndarray) -> Dict[str, float]: ...
+
+    def predict(self, idx: np.ndarray) -> np.ndarray: ...
+
+
+def epoch_batches(idx: np.ndarray, batch: int, steps: int, seed: int) -> np.ndarray:
+    """[steps, batch] dataset indices; Sequence.__len__ = n // batch, batch order shuffled per epoch."""
+    nb = len(idx) // batch
+    if nb == 0:
+        raise ValueError(f"split of {len(idx)} samples is smaller than one batch of {batch}")
+    order = np.random.default_rng(seed).permutation(nb)
+    if steps and steps > nb:
+        order = np.concatenate([order] * (-(-steps // nb)))
+    if steps:
+        order = order[:steps]
+    return np.stack([idx[b * batch:(b + 1) * batch] for b in order])
+
+
+class RefBackend:
+    """fp32 PyTorch reference backend (CPU path)."""
+
+    def __init__(self, cfg: FLConfig, data: CrackDataset, table: ParamTable, device: str = "cpu"):
+        import torch
+        from ..models.unet_ref import RefTrainer
+        self.torch = torch
+        self.data = data
+        self.table = table
+        self.tr = RefTrainer(table, table.init_flat(cfg.seed), device, cfg.lr, cfg.beta1, cfg.beta2, cfg.adam_eps,
+                             cfg.bn_momentum, cfg.bn_eps, cfg.loss)
+        self.device = device
+
+    def _batch(self, ids):
+        t = self.torch
+        x = t.from_numpy(self.data.images[ids].astype(np.float32) / 255.0).to(self.device)
+        y = t.from_numpy(self.data.masks[ids].astype(np.float32)[..., None]).to(self.device)
+        return x, y
+
+    def set_flat(self, flat):
+        self.tr.flat = self.torch.as_tensor(np.asarray(flat, np.float32), device=self.device).clone()
+
+    def get_flat(self):
+        return self.tr.flat.detach().cpu().numpy().copy()
+
+    def reset_optimizer(self):
+        self.tr.reset_optimizer()
+
+    def train_batches(self, batches):
+        ls, acc = [], []
+        for ids in batches:
+            m = self.tr.train_step(*self._batch(ids))
+            ls.append(m["loss"])
+            acc.append(m["accuracy"])
+        return {"loss": float(np.mean(ls)), "accuracy": float(np.mean(acc))}
+
+    def eval_batches(self, batches):
+        ls, acc = [], []
+        for ids in batches:
+            m = self.tr.evaluate(*self._batch(ids))
+            ls.append(m["loss"])
+            acc.append(m["accuracy"])
+        return {"loss": float(np.mean(ls)), "accuracy": float(np.mean(acc))}
+
+    def predict(self, idx):
+        x, _ = self._batch(idx)
+        return self.tr.predict(x)[..., 0].cpu().numpy()
+
+
+class LocalFit:
+    def __init__(self, cfg: FLConfig, data: CrackDataset, backend: StepBackend, table: Optional[ParamTable] = None,
+                 client: str = "client"):
+        self.cfg = cfg
+        self.data = data
+        self.backend = backend
+        self.table = table or ParamTable()
+        self.client = client
+        self.n_samples = int(len(data.train_idx))
+        self.steps = cfg.steps_per_epoch or (len(data.train_idx) // cfg.batch_size)
+        self.metrics_path = cfg.metrics_file
+        self.last: Dict[str, float] = {}
+
+    def set_weights(self, arrays: List[np.ndarray]) -> None:
+        self.backend.set_flat(self.table.from_list(arrays))
+
+    def get_weights(self) -> List[np.ndarray]:
+        return self.table.to_list(self.backend.get_flat())
+
+    def _log(self, rec: Dict) -> None:
+        line = json.dumps(rec)
+        print(line)
+        if self.metrics_path:
+            os.makedirs(os.path.dirname(os.path.abspath(self.metrics_path)), exist_ok=True)
+            with open(self.metrics_path, "a") as f:
+                f.write(line + "\n")
+
+    def train_round(self, current_round: int) -> Dict[str, float]:
+        cfg = self.cfg
+        print(f"### Model Training - Round: {current_round} ###")
+        self.backend.reset_optimizer()
+        out: Dict[str, float] = {}
+        for ep in range(cfg.epochs):
+            seed = (cfg.data_seed * 1000003 + current_round * 1009 + ep) & 0x7FFFFFFF
+            batches = epoch_batches(self.data.train_idx, cfg.batch_size, self.steps, seed)
+            t0 = time.perf_counter()
+            m = self.backend.train_batches(batches)
+            dt = time.perf_counter() - t0
+            rec = {"client": self.client, "round": current_round, "epoch": ep + 1, "loss": m["loss"],
+                   "accuracy": m["accuracy"], "images": int(batches.size), "train_s": dt,
+                   "images_per_s": batches.size / max(dt, 1e-9)}
+            if cfg.validate and len(self.data.val_idx) >= cfg.batch_size:
+                vb = epoch_batches(self.data.val_idx, cfg.batch_size, 0, 0)
+                v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
+                rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
+            self._log(rec)
+            out = rec
+        if current_round == cfg.predict_round and len(self.data.val_idx):
+            out["predict"] = self.predict_and_analyze(self.data.val_idx[:min(4, len(self.data.val_idx))])
+        self.last = out
+        return out
+
+    def predict_and_analyze(self, idx: np.ndarray) -> List[Dict[str, float]]:
+        """client_fit_model.py:176-223 + test/Segmentation2.py:114-141: predict, threshold, crack contours."""
+        from ..post.contour import crack_metrics
+        probs = self.backend.predict(idx)
+        res = []
+        for p in probs:
+            res.append(crack_metrics((np.clip(p, 0, 1) * 255).astype(np.uint8)))
+        print(f"### predict done ### {res}")
+        return res
