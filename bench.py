@@ -1,0 +1,128 @@
+"""Headline benchmark: images/sec/node per FL round (+ wall-clock per round), U-Net 256^2, one FL client per GPU.
+
+BASELINE.json metric: "images/sec/node per FL round + wall-clock/round, U-Net 256^2 at 8 clients".
+One benchmark *step* is one FL round, exactly as a client runs it (client_fit_model.py:152-174 + fl_server.py:92-105):
+  fresh Adam state -> ``local_steps`` full training iterations (fwd + bwd + Adam + BN moving stats, batch ``batch``
+  per client, hipGraph replay of the HIP-kernel engine) -> FedAvg: weighted RCCL all-reduce of the whole flat
+  model (all 112 Keras arrays incl. BN moving statistics) across the N clients -> repack weights.
+value = N * local_steps * batch / round_seconds (whole node, training images; weak scaling: per-client work fixed).
+Data: synthetic crack images/masks rendered on the device (per-client shard); weights: Keras-default random init.
+
+Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed FL rounds")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed FL rounds")
+    ap.add_argument("--img", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=16, help="per-client batch (reference: 16)")
+    ap.add_argument("--local-steps", type=int, default=388, help="iterations per round (reference epoch: 6213//16)")
+    ap.add_argument("--samples", type=int, default=8000, help="synthetic images per client")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
+    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import FedAvgAllReduce
+    from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
+
+    table = ParamTable()
+    data = make_synthetic_device(args.samples, args.img, seed=1000 + rank, split=min(6213, args.samples))
+    eng = UNetEngine(table, args.batch, args.img, dev)
+    eng.bind_data(data.images, data.masks)
+    eng.set_flat(table.init_flat(0))                     # same global init on every client
+    agg = FedAvgAllReduce(eng.flat, table, world) if world > 1 else None
+    n_local = len(data.train_idx)
+    batches = torch.as_tensor(epoch_batches(data.train_idx, args.batch, args.local_steps, seed=rank),
+                              dtype=torch.int32, device=dev)
+    use_graph = not args.no_graph
+
+    if args.profile_steps:
+        for s in range(args.profile_steps):
+            eng.idx.copy_(batches[s % batches.shape[0]])
+            eng.train_step(use_graph)
+        torch.cuda.synchronize()
+        print(json.dumps({"profile_steps": args.profile_steps, "metrics": eng.read_metrics("train")}))
+        return 0
+
+    def fl_round() -> None:
+        eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
+        for s in range(args.local_steps):
+            eng.idx.copy_(batches[s])
+            eng.train_step(use_graph)
+        if agg is not None:
+            agg.average(float(n_local))                    # weighted FedAvg over RCCL/xGMI
+        eng.pack()
+
+    for _ in range(args.warmup):
+        fl_round()
+    eng.read_metrics("train")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fl_round()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m = eng.read_metrics("train")
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    round_s = dt / args.steps
+    imgs_per_round = world * args.local_steps * args.batch
+    value = imgs_per_round / round_s
+    if rank == 0:
+        out = {"metric": "images/sec/node per FL round", "value": round(value, 2), "unit": "images/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(round_s * 1000.0, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-rendered crack masks, random init)",
+               "wall_clock_per_round_s": round(round_s, 4),
+               "ms_per_iteration": round(round_s * 1000.0 / args.local_steps, 4),
+               "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
+               "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",
+                          "img_size": args.img, "global_batch": args.batch * world, "per_client_batch": args.batch,
+                          "seq_len": None, "local_steps_per_round": args.local_steps,
+                          "parallelism": f"fedavg-dp{world} (1 FL client per GPU, RCCL weighted all-reduce)",
+                          "graph": use_graph}}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -132,6 +132,7 @@ class FLClient:
         n = getattr(self.trainer, "n_samples", 0)
         if self.aggregator is not None:
             arrays = self.aggregator.average(arrays, n)          # weighted all-reduce over RCCL
+            self.trainer.set_weights(arrays)                     # local model <- global average
             if self.aggregator.rank != 0:
                 return b""
         if self.cfg.fault_corrupt:

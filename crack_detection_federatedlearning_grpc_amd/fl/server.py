@@ -191,6 +191,8 @@ class FLServer(TransportServiceServicer):
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=self.cfg.server_threads),
                                   options=channel_options(self.cfg.max_message_mb))
         add_TransportServiceServicer_to_server(self, self.server)
+        if self.cfg.data_plane == "rccl" and not self.dist_port:
+            self.dist_port = _free_port()     # RCCL rendezvous handed to clients in the READY reply
         port = self.cfg.port if port is None else port
         self.port = self.server.add_insecure_port(f"{self.cfg.bind}:{port}")
         self.server.start()
@@ -213,6 +215,13 @@ class FLServer(TransportServiceServicer):
             pass
         finally:
             self.stop(0)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 # -- snapshot / resume ---------------------------------------------------------------------------------

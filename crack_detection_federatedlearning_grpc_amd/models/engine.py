@@ -1,0 +1,522 @@
+"""MI355X training engine for the crack U-Net: a static forward/backward schedule over hand-written HIP kernels.
+
+No autograd and no tracing compiler: the network is fixed (client_fit_model.py:92-150), so the engine lays out every
+activation, gradient and statistics buffer once (sized for the batch; 288 GB of HBM is never the constraint) and
+issues a fixed launch sequence that is captured into ONE hipGraph per train step (forward, backward, Adam, BN
+moving-stat update, weight repack). Per step the host only copies the batch's dataset indices and replays.
+
+Folds that keep the high-resolution tensors from ever being written:
+* BatchNorm apply + ReLU are applied when the NEXT kernel loads the raw conv output (``InXform``);
+* every decoder UpSampling2D commutes with the residual add and with the 1x1 convs, so each decoder block's
+  output is kept at half resolution (``x_lo``) and the upsample is folded into the consumers' indexing; the head's
+  logits are computed at 128^2 for a 256^2 image and each one scores a 2x2 block of the target mask;
+* batch assembly, /255 normalisation and mask lookup are folded into the entry conv and the head (dataset resident
+  in HBM, indexed by a batch index vector).
+
+Layouts: activations NHWC bf16; master weights, grads, Adam moments fp32 in one flat buffer (Keras order,
+``models/spec.py``); GEMM operands repacked to bf16 [N][K] by one ``pack_weights`` launch per step.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .._native_loader import hip
+from .spec import DEC_FILTERS, ENC_FILTERS, ENTRY_FILTERS, ParamTable
+
+PK_CONV, PK_CONV_DGRAD1x1, PK_CONVT, PK_CONVT_DGRAD, PK_PW, PK_PW_DGRAD = range(6)
+GM_NONE, GM_SAME, GM_SCATTER2, GM_SUM2X2, GM_MAXPOOL = range(5)
+
+
+@dataclass
+class Lazy:
+    """A tensor as seen by its consumers: stored raw values + optional BN coefficients + ReLU."""
+    t: torch.Tensor
+    ab: Optional[torch.Tensor]
+    relu: int
+    H: int
+    C: int
+
+
+class UNetEngine:
+    def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
+                 lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
+                 bn_momentum: float = 0.99, bn_eps: float = 1e-3):
+        if img % 16:
+            raise ValueError("image size must be a multiple of 16")
+        self.C = hip()
+        self.table = table
+        self.B, self.S = batch, img
+        self.dev = torch.device(device)
+        self.dice = 1 if loss == "bce_dice" else 0
+        self.lr, self.b1, self.b2, self.adam_eps = lr, beta1, beta2, adam_eps
+        self.momentum, self.bn_eps = bn_momentum, bn_eps
+        self.names = [ly.name for ly in table.weighted_layers()]
+        dev = self.dev
+        f32 = dict(dtype=torch.float32, device=dev)
+        # ---- parameters / optimizer state (flat fp32) ----
+        self.flat = torch.zeros(table.total, **f32)
+        self.grad = torch.zeros(table.total, **f32)
+        self.m = torch.zeros(table.total, **f32)
+        self.v = torch.zeros(table.total, **f32)
+        self.trainable = torch.as_tensor(table.trainable_mask().astype(np.uint8), device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.eval_metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self._build_pack()
+        self._alloc()
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.images: Optional[torch.Tensor] = None
+        self.masks: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------------------------------------ params
+    def P(self, layer: str, w: str) -> torch.Tensor:
+        e = self.table.entry(layer, w)
+        return self.flat[e.offset:e.offset + e.size]
+
+    def G(self, layer: str, w: str) -> torch.Tensor:
+        e = self.table.entry(layer, w)
+        return self.grad[e.offset:e.offset + e.size]
+
+    def _build_pack(self) -> None:
+        views, self.packed_at = [], {}
+        off, max_el = 0, 0
+
+        def add(kind, layer, wname, ks, cin, cout):
+            nonlocal off, max_el
+            e = self.table.entry(layer, wname)
+            n = ks * ks * cin * cout
+            views.append((kind, e.offset, off, ks, cin, cout))
+            self.packed_at[(layer, kind)] = (off, n)
+            off += (n + 63) // 64 * 64
+            max_el = max(max_el, n)
+
+        for ly in self.table.weighted_layers():
+            if ly.kind == "sepconv":
+                add(PK_PW, ly.name, "pointwise_kernel", 1, ly.cin, ly.cout)
+                add(PK_PW_DGRAD, ly.name, "pointwise_kernel", 1, ly.cin, ly.cout)
+            elif ly.kind == "convt":
+                add(PK_CONVT, ly.name, "kernel", 3, ly.cin, ly.cout)
+                add(PK_CONVT_DGRAD, ly.name, "kernel", 3, ly.cin, ly.cout)
+            elif ly.kind == "conv" and ly.ksize == 1 and ly.cout > 1:
+                add(PK_CONV, ly.name, "kernel", 1, ly.cin, ly.cout)
+                add(PK_CONV_DGRAD1x1, ly.name, "kernel", 1, ly.cin, ly.cout)
+        self.packed = torch.zeros(off, dtype=torch.int16, device=self.dev)
+        self.pack_table = self.C.make_pack_table(views, self.flat)
+        self.n_views, self.max_pack = len(views), max_el
+
+    def W(self, layer: str, kind: int) -> torch.Tensor:
+        off, n = self.packed_at[(layer, kind)]
+        return self.packed[off:off + n]
+
+    # ------------------------------------------------------------------------------------------------ buffers
+    def _t(self, *shape, dtype=torch.int16):
+        return torch.zeros(*shape, dtype=dtype, device=self.dev)
+
+    def _alloc(self) -> None:
+        B, S = self.B, self.S
+        r = [S // 2, S // 4, S // 8, S // 16]
+        self.r = r
+        t = self._t
+        R = self.C.STAT_REPLICAS
+        bn_layers = [ly for ly in self.table.weighted_layers() if ly.kind == "bn"]
+        self.bn_names = [ly.name for ly in bn_layers]
+        tot_c = sum(ly.cout for ly in bn_layers)
+        self.stats_all = torch.zeros(R * 2 * tot_c, dtype=torch.float32, device=self.dev)
+        self.sums_all = torch.zeros(2 * tot_c, dtype=torch.float32, device=self.dev)
+        self.ab_all = torch.zeros(4 * tot_c, dtype=torch.float32, device=self.dev)
+        self.bn: Dict[str, Dict[str, torch.Tensor]] = {}
+        so = 0
+        for ly in bn_layers:
+            c = ly.cout
+            self.bn[ly.name] = dict(C=c, stats=self.stats_all[R * 2 * so:R * 2 * (so + c)],
+                                    sums=self.sums_all[2 * so:2 * (so + c)], ab=self.ab_all[4 * so:4 * (so + c)])
+            so += c
+        # forward activations (raw bf16) -------------------------------------------------------------
+        A = self.act = {}
+        A["y0"] = t(B, r[0], r[0], ENTRY_FILTERS)
+        cin = ENTRY_FILTERS
+        for k, F in enumerate(ENC_FILTERS):
+            H = r[k]
+            A[f"e{k}_d1"] = t(B, H, H, cin)
+            A[f"e{k}_y1"] = t(B, H, H, F)
+            A[f"e{k}_d2"] = t(B, H, H, F)
+            A[f"e{k}_y2"] = t(B, H, H, F)
+            A[f"e{k}_res"] = t(B, H // 2, H // 2, F)
+            A[f"e{k}_x"] = t(B, H // 2, H // 2, F)
+            A[f"e{k}_am"] = torch.zeros(B, H // 2, H // 2, F, dtype=torch.uint8, device=self.dev)
+            cin = F
+        for k, F in enumerate(DEC_FILTERS):
+            Rk = r[3] << k
+            A[f"d{k}_c1"] = t(B, Rk, Rk, F)
+            A[f"d{k}_c2"] = t(B, Rk, Rk, F)
+            qres = Rk if k == 0 else Rk // 2
+            A[f"d{k}_q"] = t(B, qres, qres, F)
+            A[f"d{k}_xlo"] = t(B, Rk, Rk, F)
+        self.h = torch.zeros(B, r[0], r[0], dtype=torch.float32, device=self.dev)
+        # backward buffers ----------------------------------------------------------------------------------
+        D = self.dg = {}
+        D["dxlo3"] = t(B, r[0], r[0], DEC_FILTERS[-1])
+        for k, F in enumerate(DEC_FILTERS):
+            Rk = r[3] << k
+            cprev = ENC_FILTERS[-1] if k == 0 else DEC_FILTERS[k - 1]
+            prevres = Rk if k == 0 else Rk // 2
+            D[f"d{k}_g"] = t(B, Rk, Rk, F)          # BN node grads (reused A / B)
+            D[f"d{k}_dc"] = t(B, Rk, Rk, F)         # dy of a conv output
+            D[f"d{k}_dz"] = t(B, Rk, Rk, F)         # dgrad of convT2 (grad of relu(BN_A(c1)))
+            D[f"d{k}_dxin"] = t(B, Rk, Rk, cprev)   # dgrad of convT1 at block resolution
+            D[f"d{k}_dq"] = t(B, qres_of(k, Rk), qres_of(k, Rk), F)
+            D[f"d{k}_dres"] = t(B, prevres, prevres, cprev)
+            D[f"d{k}_dprev"] = t(B, prevres, prevres, cprev)
+        cin = ENTRY_FILTERS
+        for k, F in enumerate(ENC_FILTERS):
+            H = r[k]
+            D[f"e{k}_g"] = t(B, H, H, F)
+            D[f"e{k}_dy"] = t(B, H, H, F)
+            D[f"e{k}_dd2"] = t(B, H, H, F)
+            D[f"e{k}_dz1"] = t(B, H, H, F)
+            D[f"e{k}_dd1"] = t(B, H, H, cin)
+            D[f"e{k}_dz0"] = t(B, H, H, cin)
+            D[f"e{k}_dres"] = t(B, H // 2, H // 2, cin)
+            D[f"e{k}_dx"] = t(B, H, H, cin) if k > 0 else None
+            cin = F
+        D["g0"] = t(B, r[0], r[0], ENTRY_FILTERS)
+        D["dy0"] = t(B, r[0], r[0], ENTRY_FILTERS)
+        # BN moving-stat table
+        self.moving_table = self.C.make_bn_moving_table([
+            (self.bn[n]["stats"], self.P(n, "moving_mean"), self.P(n, "moving_variance"), self.bn[n]["C"],
+             float(self.bn_count(n))) for n in self.bn_names])
+
+    def bn_count(self, name: str) -> int:
+        """Pixels per channel in the batch statistics of a BN layer."""
+        i = self.bn_names.index(name)
+        B, r = self.B, self.r
+        if i == 0:
+            return B * r[0] * r[0]
+        if i <= 6:
+            k = (i - 1) // 2
+            return B * r[k] * r[k]
+        k = (i - 7) // 2
+        Rk = r[3] << k
+        return B * Rk * Rk
+
+    def nbytes(self) -> int:
+        tot = 0
+        for d in (self.act, self.dg):
+            tot += sum(v.numel() * v.element_size() for v in d.values() if v is not None)
+        return tot
+
+    # ------------------------------------------------------------------------------------------------ data
+    def bind_data(self, images: torch.Tensor, masks: torch.Tensor) -> None:
+        if images.device != self.dev or images.dtype != torch.uint8 or images.shape[1:] != (self.S, self.S, 3):
+            raise ValueError(f"images must be uint8 [N,{self.S},{self.S},3] on {self.dev}")
+        if masks.shape[1:] != (self.S, self.S) or masks.dtype != torch.uint8:
+            raise ValueError("masks must be uint8 [N,S,S]")
+        self.images, self.masks = images.contiguous(), masks.contiguous()
+        self.n_data = images.shape[0]
+
+    # ------------------------------------------------------------------------------------------------ schedule
+    def _bn_final(self, name: str, train: bool) -> torch.Tensor:
+        b = self.bn[name]
+        self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
+                           self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
+                           float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
+        return b["ab"]
+
+    def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
+              Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor]) -> None:
+        pad = (ks - 1) // 2 if stride == 1 else 0
+        B = self.B
+        self.C.conv_igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
+                          N, ks, stride, pad, pad)
+
+    def forward(self, train: bool = True) -> None:
+        C, B, r, A = self.C, self.B, self.r, self.act
+        n = iter(self.names)
+        e_conv, e_bn = next(n), next(n)
+        st = self.bn[e_bn]["stats"] if train else None
+        C.entry_fwd(self.images, self.idx, self.P(e_conv, "kernel"), self.P(e_conv, "bias"), A["y0"], st, B, self.S,
+                    ENTRY_FILTERS)
+        ab0 = self._bn_final(e_bn, train)
+        x = Lazy(A["y0"], ab0, 1, r[0], ENTRY_FILTERS)     # a0 = relu(BN0(y0))
+        for k, F in enumerate(ENC_FILTERS):
+            s1, b1, s2, b2, rc = (next(n) for _ in range(5))
+            H = r[k]
+            C.dw_fwd(x.t, self.P(s1, "depthwise_kernel"), A[f"e{k}_d1"], x.ab, 1, B, H, H, x.C)
+            self._conv(Lazy(A[f"e{k}_d1"], None, 0, H, x.C), s1, PK_PW, A[f"e{k}_y1"], F, 1, 1, 0, H,
+                       self.P(s1, "bias"), self.bn[b1]["stats"] if train else None)
+            ab1 = self._bn_final(b1, train)
+            C.dw_fwd(A[f"e{k}_y1"], self.P(s2, "depthwise_kernel"), A[f"e{k}_d2"], ab1, 1, B, H, H, F)
+            self._conv(Lazy(A[f"e{k}_d2"], None, 0, H, F), s2, PK_PW, A[f"e{k}_y2"], F, 1, 1, 0, H,
+                       self.P(s2, "bias"), self.bn[b2]["stats"] if train else None)
+            ab2 = self._bn_final(b2, train)
+            self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None)
+            C.pool_res_fwd(A[f"e{k}_y2"], ab2, A[f"e{k}_res"], A[f"e{k}_x"], A[f"e{k}_am"], B, H, H, F)
+            x = Lazy(A[f"e{k}_x"], None, 0, H // 2, F)
+        prev = x                                             # x3 at r[3]
+        for k, F in enumerate(DEC_FILTERS):
+            t1, b1, t2, b2, rc = (next(n) for _ in range(5))
+            Rk = r[3] << k
+            up = 0 if k == 0 else 1
+            self._conv(Lazy(prev.t, None, 1, prev.H, prev.C), t1, PK_CONVT, A[f"d{k}_c1"], F, 3, 1, up, Rk,
+                       self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
+            abA = self._bn_final(b1, train)
+            self._conv(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, PK_CONVT, A[f"d{k}_c2"], F, 3, 1, 0, Rk,
+                       self.P(t2, "bias"), self.bn[b2]["stats"] if train else None)
+            abB = self._bn_final(b2, train)
+            self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
+            C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
+            prev = Lazy(A[f"d{k}_xlo"], None, 0, Rk, F)
+        hl = next(n)
+        C.head_fwd(prev.t, self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
+                   self.metrics if train else self.eval_metrics, B, r[0], DEC_FILTERS[-1], self.dice)
+
+    def backward(self) -> None:
+        C, B, r, A, D = self.C, self.B, self.r, self.act, self.dg
+        names = self.names
+        hl = names[-1]
+        C.head_bwd(A["d3_xlo"], self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
+                   self.metrics, D["dxlo3"], self.G(hl, "kernel"), self.G(hl, "bias"), B, r[0], DEC_FILTERS[-1],
+                   self.dice)
+        dxlo = D["dxlo3"]
+        for k in range(3, -1, -1):
+            F = DEC_FILTERS[k]
+            base = 17 + 5 * k
+            t1, b1, t2, b2, rc = names[base:base + 5]
+            Rk = r[3] << k
+            cprev = ENC_FILTERS[-1] if k == 0 else DEC_FILTERS[k - 1]
+            prev_t = A["e2_x"] if k == 0 else A[f"d{k - 1}_xlo"]
+            prevres = Rk if k == 0 else Rk // 2
+            up = 0 if k == 0 else 1
+            bnB, bnA = self.bn[b2], self.bn[b1]
+            # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU)
+            C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, D[f"d{k}_g"], bnB["sums"],
+                       B, Rk, Rk, F)
+            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
+                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F)
+            # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
+            if k == 0:
+                dq = dxlo
+            else:
+                dq = D[f"d{k}_dq"]
+                C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, prev_t, None, 0, dq, None, B, prevres, prevres, F)
+            C.conv_wgrad(prev_t, dq, self.G(rc, "kernel"), None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
+                         F, 1, 1, 0, 0, 0, 0)
+            self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dq) == sum(g_B) (the BN_B node has no ReLU)
+            C.conv_igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
+                         prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
+            # convT2: input relu(BN_A(c1))
+            C.conv_wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], self.G(t2, "kernel"), bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
+                         F, 3, 1, 1, 1, 1, 0)
+            C.conv_igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_dz"], None, None, 0, B, Rk, Rk, F,
+                         0, Rk, Rk, F, 3, 1, 1, 1)
+            C.node_bwd(D[f"d{k}_dz"], GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c1"], bnA["ab"], 1, D[f"d{k}_g"],
+                       bnA["sums"], B, Rk, Rk, F)
+            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc"],
+                           self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F)
+            # convT1: input relu(up?(prev))
+            C.conv_wgrad(prev_t, D[f"d{k}_dc"], self.G(t1, "kernel"), None, 1, B, prevres, prevres, cprev, up, Rk,
+                         Rk, F, 3, 1, 1, 1, 1, 0)
+            C.conv_igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
+                         F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
+            # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
+            C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None, prev_t,
+                       None, 0, D[f"d{k}_dprev"], None, B, prevres, prevres, cprev)
+            dxlo = D[f"d{k}_dprev"]
+        # encoder
+        dx_out = dxlo                                         # grad of x3
+        for k in range(2, -1, -1):
+            F = ENC_FILTERS[k]
+            base = 2 + 5 * k
+            s1, b1, s2, b2, rc = names[base:base + 5]
+            H = r[k]
+            cin = ENTRY_FILTERS if k == 0 else ENC_FILTERS[k - 1]
+            if k == 0:
+                xin = Lazy(A["y0"], self.bn[names[1]]["ab"], 1, H, cin)
+            else:
+                xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
+            bnb, bna = self.bn[b2], self.bn[b1]
+            # BN_b node: routed through the max-pool (no ReLU)
+            C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
+                       bnb["sums"], B, H, H, F)
+            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"], self.G(b2, "gamma"),
+                           self.G(b2, "beta"), B * H * H, F)
+            # pointwise 2
+            C.conv_wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], self.G(s2, "pointwise_kernel"), None, 0, B, H, H, F, 0, H, H,
+                         F, 1, 1, 0, 0, 0, 0)
+            C.conv_igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
+                         H, H, F, 1, 1, 0, 0)
+            # depthwise 2 on relu(BN_a(y1))
+            C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.G(s2, "depthwise_kernel"), bna["ab"], 1, B, H, H, F)
+            C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_dz1"], B, H, H, F)
+            C.node_bwd(D[f"e{k}_dz1"], GM_SAME, 0, None, 0, 0, None, A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_g"],
+                       bna["sums"], B, H, H, F)
+            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy"], self.G(b1, "gamma"),
+                           self.G(b1, "beta"), B * H * H, F)
+            # pointwise 1
+            C.conv_wgrad(A[f"e{k}_d1"], D[f"e{k}_dy"], self.G(s1, "pointwise_kernel"), None, 0, B, H, H, cin, 0, H,
+                         H, F, 1, 1, 0, 0, 0, 0)
+            C.conv_igemm(D[f"e{k}_dy"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
+                         H, H, cin, 1, 1, 0, 0)
+            # depthwise 1 on relu(x_in)
+            C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.G(s1, "depthwise_kernel"), xin.ab, 1, B, H, H, cin)
+            C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
+            # residual 1x1 stride-2 conv on x_in (dres = dx_out)
+            C.conv_wgrad(xin.t, dx_out, self.G(rc, "kernel"), xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
+                         1, 2, 0, 0, 0, 0)
+            self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dx_out) == sum(g_b): max-pool routing keeps sums
+            C.conv_igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
+                         H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
+            if k > 0:
+                C.node_bwd(D[f"e{k}_dz0"], GM_SAME, 1, D[f"e{k}_dres"], GM_SCATTER2, 0, None, xin.t, None, 0,
+                           D[f"e{k}_dx"], None, B, H, H, cin)
+                dx_out = D[f"e{k}_dx"]
+            else:
+                bn0 = self.bn[names[1]]
+                C.node_bwd(D["e0_dz0"], GM_SAME, 0, D["e0_dres"], GM_SCATTER2, 0, None, A["y0"], bn0["ab"], 1,
+                           D["g0"], bn0["sums"], B, H, H, cin)
+                C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
+                               self.G(names[1], "beta"), B * H * H, cin)
+                C.entry_wgrad(self.images, self.idx, D["dy0"], self.G(names[0], "kernel"), B, self.S, ENTRY_FILTERS)
+
+    def optimizer_step(self) -> None:
+        C = self.C
+        C.adam_update(self.flat, self.grad, self.m, self.v, self.trainable, self.lr, self.b1, self.b2, self.adam_eps,
+                      self.step_t)
+        C.adam_step_done(self.step_t)
+        C.bn_moving_update(self.moving_table, len(self.bn_names), self.momentum)
+        self.pack()
+
+    def pack(self) -> None:
+        self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack)
+
+    def _zero_step(self) -> None:
+        self.grad.zero_()
+        self.stats_all.zero_()
+        self.sums_all.zero_()
+        self.metrics[4:8].zero_()
+
+    def train_step_eager(self) -> None:
+        self._zero_step()
+        self.forward(True)
+        self.backward()
+        self.optimizer_step()
+
+    # ------------------------------------------------------------------------------------------------ graph
+    def capture(self) -> None:
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            # warm-up launch outside capture (module load, lazy init) on a scratch copy of the state
+            saved = [t.clone() for t in (self.flat, self.m, self.v, self.step_t, self.metrics)]
+            self.train_step_eager()
+            for t, c in zip((self.flat, self.m, self.v, self.step_t, self.metrics), saved):
+                t.copy_(c)
+            self.pack()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.train_step_eager()
+        self.graph = g
+
+    def train_step(self, use_graph: bool = True) -> None:
+        if use_graph:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+        else:
+            self.train_step_eager()
+
+    # ------------------------------------------------------------------------------------------------ state
+    def set_flat(self, flat: np.ndarray) -> None:
+        self.flat.copy_(torch.as_tensor(np.asarray(flat, np.float32)).to(self.dev))
+        self.pack()
+
+    def get_flat(self) -> np.ndarray:
+        return self.flat.detach().cpu().numpy().copy()
+
+    def reset_optimizer(self) -> None:
+        self.m.zero_()
+        self.v.zero_()
+        self.step_t.zero_()
+
+    def read_metrics(self, which: str = "train", reset: bool = True) -> Dict[str, float]:
+        mt = self.metrics if which == "train" else self.eval_metrics
+        v = mt.cpu().numpy()
+        if reset:
+            mt.zero_()
+        n = max(v[2], 1.0)
+        return {"loss": float(v[0] / n) * 1.0, "bce_sum": float(v[0]), "accuracy": float(v[1] / n),
+                "pixels": float(v[2]), "dice_sum": float(v[3])}
+
+    def predict_probs(self) -> torch.Tensor:
+        """Sigmoid probabilities at full resolution for the current ``idx`` batch (eval-mode BN)."""
+        self.forward(False)
+        p = torch.sigmoid(self.h)
+        return p.repeat_interleave(2, 1).repeat_interleave(2, 2)
+
+
+def qres_of(k: int, Rk: int) -> int:
+    return Rk if k == 0 else Rk // 2
+
+
+class HipBackend:
+    """``train.local.StepBackend`` on the MI355X engine."""
+
+    def __init__(self, cfg, data, table: ParamTable):
+        self.cfg = cfg
+        self.table = table
+        self.eng = UNetEngine(table, cfg.batch_size, data.img_size, "cuda", cfg.loss, cfg.lr, cfg.beta1, cfg.beta2,
+                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps)
+        images = data.images if isinstance(data.images, torch.Tensor) else torch.as_tensor(data.images)
+        masks = data.masks if isinstance(data.masks, torch.Tensor) else torch.as_tensor(data.masks)
+        self.eng.bind_data(images.to(self.eng.dev), masks.to(self.eng.dev))
+        self.eng.set_flat(table.init_flat(cfg.seed))
+        self.use_graph = cfg.use_graph
+
+    def set_flat(self, flat):
+        self.eng.set_flat(flat)
+
+    def get_flat(self):
+        return self.eng.get_flat()
+
+    def reset_optimizer(self):
+        self.eng.reset_optimizer()
+
+    def train_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        e = self.eng
+        dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)
+        e.metrics.zero_()
+        for s in range(dev_b.shape[0]):
+            e.idx.copy_(dev_b[s])
+            e.train_step(self.use_graph)
+        m = e.read_metrics("train")
+        if e.dice:
+            m["loss"] = m["loss"] + m["dice_sum"] / max(1, len(batches))
+        return m
+
+    def eval_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        e = self.eng
+        dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)
+        e.eval_metrics.zero_()
+        for s in range(dev_b.shape[0]):
+            e.idx.copy_(dev_b[s])
+            e.forward(False)
+        return e.read_metrics("eval")
+
+    def predict(self, idx: np.ndarray) -> np.ndarray:
+        e = self.eng
+        out = []
+        idx = np.asarray(idx, np.int32)
+        for s in range(0, len(idx), e.B):
+            chunk = idx[s:s + e.B]
+            pad = np.concatenate([chunk, np.repeat(chunk[-1:], e.B - len(chunk))])
+            e.idx.copy_(torch.as_tensor(pad).to(e.dev))
+            out.append(e.predict_probs()[:len(chunk)].cpu().numpy())
+        return np.concatenate(out)

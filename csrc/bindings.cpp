@@ -1,0 +1,358 @@
+// PyTorch bindings of the gfx950 kernels (module _C). Every op takes preallocated tensors (no allocation on the
+// hot path, graph-capture safe) and launches on the current HIP stream of the tensors' device.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels/launch.h"
+
+namespace {
+
+using OptT = std::optional<at::Tensor>;
+
+void check(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+T* ptr(const at::Tensor& t, const char* name) {
+  check(t, name);
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+template <typename T>
+T* optr(const OptT& t, const char* name) {
+  if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+  return ptr<T>(*t, name);
+}
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void ok(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " failed (code " + std::to_string(rc) + ")");
+}
+
+InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(ab, "ab"), C, relu}; }
+
+void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
+                   int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
+                   int pad_l) {
+  ConvParams p{};
+  p.x = ptr<const bf16_t>(x, "x");
+  p.wt = ptr<const bf16_t>(wt, "wt");
+  p.bias = optr<const float>(bias, "bias");
+  p.y = ptr<bf16_t>(y, "y");
+  p.stats = optr<float>(stats, "stats");
+  p.xf = xf(ab, Cin, relu);
+  p.B = B; p.Hin = Hin; p.Win = Win; p.Cin = Cin; p.up_in = up_in;
+  p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
+  p.M = B * Ho * Wo;
+  p.K = ks * ks * Cin;
+  TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv_igemm: x size");
+  TORCH_CHECK(wt.numel() >= (int64_t)N * p.K, "conv_igemm: wt size");
+  TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv_igemm: y size");
+  TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
+  ok(conv_igemm(p, stream()), "conv_igemm");
+}
+
+void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win, int Cin,
+                   int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t, int pad_l, int dst_mode,
+                   int m_chunk) {
+  WgradParams p{};
+  p.x = ptr<const bf16_t>(x, "x");
+  p.dy = ptr<const bf16_t>(dy, "dy");
+  p.dw = ptr<float>(dw, "dw");
+  p.xf = xf(ab, Cin, relu);
+  p.B = B; p.Hin = Hin; p.Win = Win; p.Cin = Cin; p.up_in = up_in;
+  p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
+  p.M = B * Ho * Wo;
+  p.K = ks * ks * Cin;
+  p.dst_mode = dst_mode;
+  p.m_chunk = m_chunk;
+  TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv_wgrad: x size");
+  TORCH_CHECK(dy.numel() == (int64_t)p.M * N, "conv_wgrad: dy size");
+  TORCH_CHECK(dw.numel() >= (int64_t)p.K * N, "conv_wgrad: dw size");
+  ok(conv_wgrad(p, stream()), "conv_wgrad");
+}
+
+DwParams dwp(int B, int H, int W, int C) {
+  DwParams p{};
+  p.B = B; p.H = H; p.W = W; p.C = C;
+  return p;
+}
+
+void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int B, int H, int W, int C) {
+  DwParams p = dwp(B, H, W, C);
+  p.x = ptr<const bf16_t>(x, "x");
+  p.w = ptr<const float>(w, "w");
+  p.y = ptr<bf16_t>(y, "y");
+  p.xf = xf(ab, C, relu);
+  TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && y.numel() == x.numel() && w.numel() == 9 * C, "dw_fwd sizes");
+  ok(dw_fwd(p, stream()), "dw_fwd");
+}
+
+void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W, int C) {
+  DwParams p = dwp(B, H, W, C);
+  p.dy = ptr<const bf16_t>(dy, "dy");
+  p.w = ptr<const float>(w, "w");
+  p.y = ptr<bf16_t>(dx, "dx");
+  TORCH_CHECK(dy.numel() == (int64_t)B * H * W * C && dx.numel() == dy.numel() && w.numel() == 9 * C, "dw_dgrad sizes");
+  ok(dw_dgrad(p, stream()), "dw_dgrad");
+}
+
+void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C) {
+  DwParams p = dwp(B, H, W, C);
+  p.x = ptr<const bf16_t>(x, "x");
+  p.dy = ptr<const bf16_t>(dy, "dy");
+  p.dw = ptr<float>(dw, "dw");
+  p.xf = xf(ab, C, relu);
+  TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && dy.numel() == x.numel() && dw.numel() == 9 * C, "dw_wgrad sizes");
+  ok(dw_wgrad(p, stream()), "dw_wgrad");
+}
+
+void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bias, at::Tensor y, OptT stats, int B,
+                  int S, int Cout) {
+  EntryParams p{};
+  p.images = ptr<const uint8_t>(images, "images");
+  p.idx = ptr<const int32_t>(idx, "idx");
+  p.w = ptr<const float>(w, "w");
+  p.bias = ptr<const float>(bias, "bias");
+  p.y = ptr<bf16_t>(y, "y");
+  p.stats = optr<float>(stats, "stats");
+  p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
+  TORCH_CHECK(idx.numel() == B && y.numel() == (int64_t)B * p.Ho * p.Wo * Cout && w.numel() == 27 * Cout, "entry_fwd sizes");
+  ok(entry_fwd(p, stream()), "entry_fwd");
+}
+
+void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor dw, int B, int S, int Cout) {
+  EntryParams p{};
+  p.images = ptr<const uint8_t>(images, "images");
+  p.idx = ptr<const int32_t>(idx, "idx");
+  p.dy = ptr<const bf16_t>(dy, "dy");
+  p.dw = ptr<float>(dw, "dw");
+  p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
+  TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout && dw.numel() == 27 * Cout, "entry_wgrad sizes");
+  ok(entry_wgrad(p, stream()), "entry_wgrad");
+}
+
+void bn_finalize_op(OptT stats, at::Tensor gamma, at::Tensor beta, at::Tensor mm, at::Tensor mv, at::Tensor ab, int C,
+                    double count, double eps, int train) {
+  TORCH_CHECK(ab.numel() >= 4 * C, "bn_finalize: ab size");
+  ok(bn_finalize(optr<const float>(stats, "stats"), ptr<const float>(gamma, "gamma"), ptr<const float>(beta, "beta"),
+                 ptr<const float>(mm, "mm"), ptr<const float>(mv, "mv"), ptr<float>(ab, "ab"), C, (float)count,
+                 (float)eps, train, stream()),
+     "bn_finalize");
+}
+
+// layers: list of (stats, moving_mean, moving_var, C, count) -> device table (uint8 tensor)
+at::Tensor make_bn_moving_table(std::vector<std::tuple<at::Tensor, at::Tensor, at::Tensor, int, double>> layers) {
+  std::vector<BnMoving> h;
+  at::Device dev = std::get<0>(layers.at(0)).device();
+  for (auto& l : layers) {
+    BnMoving b{};
+    b.stats = ptr<const float>(std::get<0>(l), "stats");
+    b.mmean = ptr<float>(std::get<1>(l), "mmean");
+    b.mvar = ptr<float>(std::get<2>(l), "mvar");
+    b.C = std::get<3>(l);
+    b.count = (float)std::get<4>(l);
+    h.push_back(b);
+  }
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(BnMoving))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(BnMoving));
+  return cpu.to(dev);
+}
+
+void bn_moving_update_op(at::Tensor table, int n_layers, double momentum) {
+  TORCH_CHECK(table.numel() == (int64_t)n_layers * (int64_t)sizeof(BnMoving), "bn_moving_update: table size");
+  ok(bn_moving_update(ptr<const BnMoving>(table, "table"), n_layers, 0, (float)momentum, stream()), "bn_moving_update");
+}
+
+void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask1, OptT argmax, at::Tensor v, OptT ab,
+                 int relu_node, at::Tensor out, OptT sums, int B, int H, int W, int C) {
+  NodeBwdParams p{};
+  p.src[0] = GradSrc{optr<const bf16_t>(src0, "src0"), src0.has_value() ? mode0 : 0, mask0};
+  p.src[1] = GradSrc{optr<const bf16_t>(src1, "src1"), src1.has_value() ? mode1 : 0, mask1};
+  if (!p.src[0].p) p.src[0].mode = GM_NONE;
+  if (!p.src[1].p) p.src[1].mode = GM_NONE;
+  p.argmax = optr<const uint8_t>(argmax, "argmax");
+  p.v = ptr<const bf16_t>(v, "v");
+  p.ab = optr<const float>(ab, "ab");
+  p.relu_node = relu_node;
+  p.out = ptr<bf16_t>(out, "out");
+  p.sums = optr<float>(sums, "sums");
+  p.B = B; p.H = H; p.W = W; p.C = C;
+  const int64_t n = (int64_t)B * H * W * C;
+  TORCH_CHECK(v.numel() == n && out.numel() == n, "node_bwd: v/out size");
+  const int64_t half = (int64_t)B * ((H + 1) / 2) * ((W + 1) / 2) * C;
+  for (int s = 0; s < 2; ++s) {
+    const OptT& t = s ? src1 : src0;
+    if (!p.src[s].p) continue;
+    const int m = p.src[s].mode;
+    const int64_t want = m == GM_SAME ? n : m == GM_SUM2X2 ? 4 * n : half;
+    TORCH_CHECK(t->numel() == want, "node_bwd: source ", s, " size ", t->numel(), " != ", want);
+    if (m == GM_MAXPOOL) TORCH_CHECK(p.argmax && argmax->numel() == half, "node_bwd: argmax size");
+  }
+  ok(node_bwd(p, stream()), "node_bwd");
+}
+
+void bn_bwd_apply_op(at::Tensor g, at::Tensor y, at::Tensor ab, at::Tensor sums, at::Tensor dy, OptT dgamma,
+                     OptT dbeta, int M, int C) {
+  BnBwdApplyParams p{};
+  p.g = ptr<const bf16_t>(g, "g");
+  p.y = ptr<const bf16_t>(y, "y");
+  p.ab = ptr<const float>(ab, "ab");
+  p.sums = ptr<const float>(sums, "sums");
+  p.dy = ptr<bf16_t>(dy, "dy");
+  p.dgamma = optr<float>(dgamma, "dgamma");
+  p.dbeta = optr<float>(dbeta, "dbeta");
+  p.M = M; p.C = C;
+  TORCH_CHECK(g.numel() == (int64_t)M * C && y.numel() == g.numel() && dy.numel() == g.numel(), "bn_bwd_apply sizes");
+  ok(bn_bwd_apply(p, stream()), "bn_bwd_apply");
+}
+
+void pool_res_fwd_op(at::Tensor y, at::Tensor ab, at::Tensor res, at::Tensor out, at::Tensor argmax, int B, int H,
+                     int W, int C) {
+  PoolResParams p{};
+  p.y = ptr<const bf16_t>(y, "y");
+  p.ab = ptr<const float>(ab, "ab");
+  p.res = ptr<const bf16_t>(res, "res");
+  p.out = ptr<bf16_t>(out, "out");
+  p.argmax = ptr<uint8_t>(argmax, "argmax");
+  p.B = B; p.H = H; p.W = W; p.C = C; p.Ho = (H + 1) / 2; p.Wo = (W + 1) / 2;
+  const int64_t no = (int64_t)B * p.Ho * p.Wo * C;
+  TORCH_CHECK(y.numel() == (int64_t)B * H * W * C && res.numel() == no && out.numel() == no && argmax.numel() == no,
+              "pool_res_fwd sizes");
+  ok(pool_res_fwd(p, stream()), "pool_res_fwd");
+}
+
+void bn_add_fwd_op(at::Tensor y, at::Tensor ab, at::Tensor q, int q_up, at::Tensor out, int B, int H, int W, int C) {
+  BnAddParams p{};
+  p.y = ptr<const bf16_t>(y, "y");
+  p.ab = ptr<const float>(ab, "ab");
+  p.q = ptr<const bf16_t>(q, "q");
+  p.q_up = q_up;
+  p.out = ptr<bf16_t>(out, "out");
+  p.B = B; p.H = H; p.W = W; p.C = C;
+  const int64_t n = (int64_t)B * H * W * C;
+  TORCH_CHECK(y.numel() == n && out.numel() == n && q.numel() == (q_up ? n / 4 : n), "bn_add_fwd sizes");
+  ok(bn_add_fwd(p, stream()), "bn_add_fwd");
+}
+
+HeadParams headp(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, at::Tensor idx, at::Tensor h,
+                 at::Tensor metrics, int B, int R, int Cin, int dice) {
+  HeadParams p{};
+  p.x = ptr<const bf16_t>(x, "x");
+  p.w = ptr<const float>(w, "w");
+  p.bias = ptr<const float>(bias, "bias");
+  p.masks = ptr<const uint8_t>(masks, "masks");
+  p.idx = ptr<const int32_t>(idx, "idx");
+  p.h = ptr<float>(h, "h");
+  p.metrics = ptr<double>(metrics, "metrics");
+  p.B = B; p.R = R; p.Cin = Cin; p.dice = dice;
+  TORCH_CHECK(x.numel() == (int64_t)B * R * R * Cin && h.numel() == (int64_t)B * R * R && idx.numel() == B &&
+              metrics.numel() >= 8 && masks.size(-1) == 2 * R, "head sizes");
+  return p;
+}
+
+void head_fwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, at::Tensor idx, at::Tensor h,
+                 at::Tensor metrics, int B, int R, int Cin, int dice) {
+  ok(head_fwd(headp(x, w, bias, masks, idx, h, metrics, B, R, Cin, dice), stream()), "head_fwd");
+}
+
+void head_bwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, at::Tensor idx, at::Tensor h,
+                 at::Tensor metrics, at::Tensor dx, at::Tensor dw, at::Tensor db, int B, int R, int Cin, int dice) {
+  HeadParams p = headp(x, w, bias, masks, idx, h, metrics, B, R, Cin, dice);
+  p.dx = ptr<bf16_t>(dx, "dx");
+  p.dw = ptr<float>(dw, "dw");
+  p.db = ptr<float>(db, "db");
+  TORCH_CHECK(dx.numel() == x.numel(), "head_bwd: dx size");
+  ok(head_bwd(p, stream()), "head_bwd");
+}
+
+void adam_update_op(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor trainable, double lr, double b1,
+                    double b2, double eps, at::Tensor step) {
+  AdamParams a{};
+  a.p = ptr<float>(p, "p");
+  a.g = ptr<const float>(g, "g");
+  a.m = ptr<float>(m, "m");
+  a.v = ptr<float>(v, "v");
+  a.trainable = ptr<const uint8_t>(trainable, "trainable");
+  a.n = p.numel();
+  a.lr = (float)lr; a.b1 = (float)b1; a.b2 = (float)b2; a.eps = (float)eps;
+  a.step = ptr<int>(step, "step");
+  TORCH_CHECK(g.numel() == a.n && m.numel() == a.n && v.numel() == a.n && trainable.numel() == a.n, "adam sizes");
+  ok(adam_update(a, stream()), "adam_update");
+}
+
+void adam_step_done_op(at::Tensor step) { ok(adam_step_done(ptr<int>(step, "step"), stream()), "adam_step_done"); }
+
+// views: list of (kind, src_offset, dst_offset, ks, cin, cout)
+at::Tensor make_pack_table(std::vector<std::tuple<int, int64_t, int64_t, int, int, int>> views, at::Tensor like) {
+  std::vector<PackView> h;
+  for (auto& v : views) {
+    PackView p{};
+    p.kind = std::get<0>(v); p.src = std::get<1>(v); p.dst = std::get<2>(v);
+    p.ks = std::get<3>(v); p.cin = std::get<4>(v); p.cout = std::get<5>(v);
+    h.push_back(p);
+  }
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(PackView))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(PackView));
+  return cpu.to(like.device());
+}
+
+void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n_views, int max_elems) {
+  TORCH_CHECK(table.numel() == (int64_t)n_views * (int64_t)sizeof(PackView), "pack: table size");
+  ok(pack_weights(ptr<const float>(flat, "flat"), ptr<bf16_t>(packed, "packed"), ptr<const PackView>(table, "table"),
+                  n_views, max_elems, stream()),
+     "pack_weights");
+}
+
+void render_cracks_op(at::Tensor segs, at::Tensor params, at::Tensor images, at::Tensor masks, int n, int img,
+                      int max_seg) {
+  TORCH_CHECK(images.numel() == (int64_t)n * img * img * 3 && masks.numel() == (int64_t)n * img * img &&
+              segs.numel() == (int64_t)n * max_seg * 6 && params.numel() == (int64_t)n * 8, "render sizes");
+  ok(render_cracks(ptr<const float>(segs, "segs"), ptr<const float>(params, "params"), ptr<uint8_t>(images, "images"),
+                   ptr<uint8_t>(masks, "masks"), n, img, max_seg, stream()),
+     "render_cracks");
+}
+
+void gather_rows_u8_op(at::Tensor src, at::Tensor idx, at::Tensor dst, int64_t row_bytes) {
+  TORCH_CHECK(dst.numel() == idx.numel() * row_bytes, "gather_rows sizes");
+  ok(gather_rows_u8(ptr<const uint8_t>(src, "src"), ptr<const int32_t>(idx, "idx"), ptr<uint8_t>(dst, "dst"),
+                    (int)idx.numel(), row_bytes, stream()),
+     "gather_rows_u8");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "CDNA4 (gfx950) HIP kernels of the crack-segmentation FL trainer";
+  m.attr("STAT_REPLICAS") = STAT_REPLICAS;
+  m.def("conv_igemm", &conv_igemm_op);
+  m.def("conv_wgrad", &conv_wgrad_op);
+  m.def("dw_fwd", &dw_fwd_op);
+  m.def("dw_dgrad", &dw_dgrad_op);
+  m.def("dw_wgrad", &dw_wgrad_op);
+  m.def("entry_fwd", &entry_fwd_op);
+  m.def("entry_wgrad", &entry_wgrad_op);
+  m.def("bn_finalize", &bn_finalize_op);
+  m.def("make_bn_moving_table", &make_bn_moving_table);
+  m.def("bn_moving_update", &bn_moving_update_op);
+  m.def("node_bwd", &node_bwd_op);
+  m.def("bn_bwd_apply", &bn_bwd_apply_op);
+  m.def("pool_res_fwd", &pool_res_fwd_op);
+  m.def("bn_add_fwd", &bn_add_fwd_op);
+  m.def("head_fwd", &head_fwd_op);
+  m.def("head_bwd", &head_bwd_op);
+  m.def("adam_update", &adam_update_op);
+  m.def("adam_step_done", &adam_step_done_op);
+  m.def("make_pack_table", &make_pack_table);
+  m.def("pack_weights", &pack_weights_op);
+  m.def("render_cracks", &render_cracks_op);
+  m.def("gather_rows_u8", &gather_rows_u8_op);
+}

@@ -1,0 +1,92 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels: bf16 bit conversions, vector types, wave64 reductions.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * activations are NHWC bf16 stored as uint16_t (RNE rounding, NaN preserved);
+//   * accumulation, BN statistics, gradients of weights and the optimizer are fp32;
+//   * wave = 64 lanes; block sizes are multiples of 64;
+//   * launchers take a hipStream_t and never allocate / synchronise (graph-capture safe).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CFL_DEVICE __device__ __forceinline__
+
+typedef uint16_t bf16_t;
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+CFL_DEVICE float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+CFL_DEVICE bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)0x7fc0;   // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// 8 bf16 <-> 8 float through one 16-byte vector
+CFL_DEVICE void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+CFL_DEVICE uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+CFL_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+CFL_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum of one value per thread (blockDim.x multiple of 64, <= 1024). Result valid in thread 0.
+template <int NT>
+CFL_DEVICE float block_sum(float v, float* red /* >= NT/64 floats of LDS */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+  }
+  __syncthreads();
+  return t;
+}
+
+CFL_DEVICE int imin(int a, int b) { return a < b ? a : b; }
+CFL_DEVICE int imax(int a, int b) { return a > b ? a : b; }
+
+// BN per-channel coefficients produced by bn_finalize (csrc/kernels/bn.hip): 4 rows of C floats
+//   ab[0*C + c] = scale a = gamma * rstd     ab[1*C + c] = shift b = beta - mean * a
+//   ab[2*C + c] = mean                       ab[3*C + c] = rstd
+// A "transform" applied on load to a raw conv output y is  relu?(a*y + b).
+struct InXform {
+  const float* ab;   // nullptr = identity
+  int C;             // channel count of ab
+  int relu;          // apply ReLU after the affine (or alone when ab == nullptr)
+};
+
+CFL_DEVICE float xform1(float v, const InXform& t, int c) {
+  if (t.ab) v = fmaf(t.ab[c], v, t.ab[t.C + c]);
+  if (t.relu) v = fmaxf(v, 0.f);
+  return v;
+}

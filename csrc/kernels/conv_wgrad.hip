@@ -1,0 +1,167 @@
+// Convolution weight gradient on gfx950 MFMA:  dW[k][n] = sum_m im2col(T(x))[m][k] * dy[m][n].
+//
+// The reduction runs over pixels (M = B*Ho*Wo, up to millions), which in NHWC is the OUTER dimension of both
+// operands. Both tiles are therefore staged in their natural [m][k] / [m][n] row layout (16-byte coalesced
+// global loads, the producer's BN-apply + ReLU folded into the x load) and the MFMA operands - which need 8
+// consecutive m per lane - are read with the CDNA4 transposing LDS read ds_read_b64_tr_b16
+// (__builtin_amdgcn_ds_read_tr16_b64): no register or LDS transpose pass.
+//
+// Output tile BKO(k) x BNO(n), 4 waves 2x2, reduction step 32 pixels, register-staged double buffer.
+// The M range is split over gridDim.z; partial tiles are combined with fp32 atomics directly into the layer's
+// slot of the flat gradient buffer, writing Keras layouts (HWIO for Conv2D / pointwise, (kh,kw,out,in) with the
+// spatial flip for Conv2DTranspose: dst_mode 1).
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+constexpr int RM = 32;     // reduction step (pixels)
+constexpr int NT = 256;
+
+typedef short s4v_lds __attribute__((ext_vector_type(4)));
+
+CFL_DEVICE s4v tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(p));
+}
+
+template <int BKO, int BNO>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
+  constexpr int TK = BKO / 2, TN = BNO / 2;
+  constexpr int FK = TK / 16, FN = TN / 16;
+  constexpr int LDX = BKO + 8, LDG = BNO + 8;
+  constexpr int XC = RM * BKO / 8, GC = RM * BNO / 8;   // 16-byte chunks per tile
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][RM][LDX];
+  __shared__ __attribute__((aligned(16))) bf16_t sG[2][RM][LDG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid >> 1, wn = wid & 1;
+  const int kBlock = blockIdx.x * BKO, nBlock = blockIdx.y * BNO;
+  const int m_begin = blockIdx.z * chunk;
+  const int m_end = imin(p.M, m_begin + chunk);
+  if (m_begin >= m_end) return;
+  const int HWo = p.Ho * p.Wo;
+  const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
+
+  // this thread's x chunk: fixed k (channel group), row within the step
+  const bool has_x = tid < XC, has_g = tid < GC;
+  const int xm = tid / (BKO / 8), xk = kBlock + (tid % (BKO / 8)) * 8;
+  const int tap = xk / p.Cin, xc = xk - tap * p.Cin;
+  const int ky = tap / p.ks, kx = tap - ky * p.ks;
+  const int gm = tid / (BNO / 8), gn = nBlock + (tid % (BNO / 8)) * 8;
+
+  uint4 rx = make_uint4(0, 0, 0, 0), rg = make_uint4(0, 0, 0, 0);
+  auto load = [&](int m0) {
+    if (has_x) {
+      const int m = m0 + xm;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < m_end) {
+        const int b = m / HWo, r = m - b * HWo;
+        const int oh = r / p.Wo, ow = r - oh * p.Wo;
+        const int ih = oh * p.stride - p.pad_t + ky, iw = ow * p.stride - p.pad_l + kx;
+        if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
+          v = *reinterpret_cast<const uint4*>(
+              p.x + (((size_t)b * p.Hin + (ih >> p.up_in)) * p.Win + (iw >> p.up_in)) * p.Cin + xc);
+          if (p.xf.ab || p.xf.relu) {
+            float f[8];
+            unpack8(v, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = xform1(f[j], p.xf, xc + j);
+            v = pack8(f);
+          }
+        }
+      }
+      rx = v;
+    }
+    if (has_g) {
+      const int m = m0 + gm;
+      rg = (m < m_end) ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.N + gn) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int buf) {
+    if (has_x) *reinterpret_cast<uint4*>(&sX[buf][xm][(tid % (BKO / 8)) * 8]) = rx;
+    if (has_g) *reinterpret_cast<uint4*>(&sG[buf][gm][(tid % (BNO / 8)) * 8]) = rg;
+  };
+
+  f4v acc[FK][FN];
+#pragma unroll
+  for (int i = 0; i < FK; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  load(m_begin);
+  store(0);
+  __syncthreads();
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  int buf = 0;
+  for (int m0 = m_begin; m0 < m_end; m0 += RM) {
+    const bool more = m0 + RM < m_end;
+    if (more) load(m0 + RM);
+    s8v af[FK], bfg[FN];
+#pragma unroll
+    for (int i = 0; i < FK; ++i) {
+      const int kc = wk * TK + i * 16 + 4 * pq;
+      const s4v lo = tr_read(&sX[buf][8 * g + q][kc]);
+      const s4v hi = tr_read(&sX[buf][8 * g + 4 + q][kc]);
+      af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int nc = wn * TN + j * 16 + 4 * pq;
+      const s4v lo = tr_read(&sG[buf][8 * g + q][nc]);
+      const s4v hi = tr_read(&sG[buf][8 * g + 4 + q][nc]);
+      bfg[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < FK; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // epilogue: D[k][n], col n = lane&15, row k = (lane>>4)*4 + r
+#pragma unroll
+  for (int i = 0; i < FK; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nBlock + wn * TN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kBlock + wk * TK + i * 16 + (lane >> 4) * 4 + r;
+        size_t dst;
+        if (p.dst_mode == 1) {
+          const int t = k / p.Cin, c = k - t * p.Cin;
+          dst = ((size_t)(p.ks * p.ks - 1 - t) * p.N + n) * p.Cin + c;
+        } else {
+          dst = (size_t)k * p.N + n;
+        }
+        atomicAdd(&p.dw[dst], acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace
+
+int conv_wgrad(const WgradParams& p, hipStream_t st) {
+  if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
+  const int bko = (p.K % 64 == 0) ? 64 : 32;
+  const int bno = (p.N % 64 == 0) ? 64 : 32;
+  const int tiles = (p.K / bko) * (p.N / bno);
+  int chunk = p.m_chunk;
+  if (chunk <= 0) {
+    int splits = (2048 + tiles - 1) / tiles;
+    const int max_splits = (p.M + 255) / 256;
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    chunk = (p.M + splits - 1) / splits;
+  }
+  chunk = (chunk + RM - 1) / RM * RM;
+  const int zs = (p.M + chunk - 1) / chunk;
+  dim3 grid(p.K / bko, p.N / bno, zs), blk(NT);
+  if (bko == 64 && bno == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 64>), grid, blk, 0, st, p, chunk);
+  else if (bko == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 32>), grid, blk, 0, st, p, chunk);
+  else if (bno == 64) hipLaunchKernelGGL((conv_wgrad_kernel<32, 64>), grid, blk, 0, st, p, chunk);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<32, 32>), grid, blk, 0, st, p, chunk);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}

@@ -1,0 +1,182 @@
+// Host-callable launchers of the gfx950 kernels (no torch dependency; raw device pointers + hipStream_t).
+// Every launcher returns 0 on success, nonzero on an unsupported shape or a launch error.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+// BN batch statistics are accumulated into STAT_REPLICAS replica rows [rep][2][C] (sum, sum of squares) so the
+// per-block atomics of thousands of workgroups do not all hit the same 2*C words; bn_finalize sums the replicas.
+#define STAT_REPLICAS 32
+
+// ---------------------------------------------------------------- implicit-GEMM conv (conv_igemm.hip)
+struct ConvParams {
+  const bf16_t* x;     // [B, Hin, Win, Cin] NHWC (physical; logical = upsample2 if up_in)
+  const bf16_t* wt;    // [N][K] packed bf16 weights, K = ks*ks*Cin, k = (ky*ks + kx)*Cin + ci
+  const float* bias;   // [N] or nullptr
+  bf16_t* y;           // [B, Ho, Wo, N]
+  float* stats;        // [STAT_REPLICAS][2][N] (sum, sum of squares), atomically accumulated, or nullptr
+  InXform xf;          // transform applied to x on load
+  int B, Hin, Win, Cin, up_in;
+  int Ho, Wo, N, ks, stride, pad_t, pad_l;
+  int M, K;
+};
+int conv_igemm(const ConvParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- weight gradient (conv_wgrad.hip)
+struct WgradParams {
+  const bf16_t* x;     // conv input (as in ConvParams)
+  const bf16_t* dy;    // [M][N] gradient w.r.t. the conv output
+  float* dw;           // fp32 destination (atomic accumulate)
+  InXform xf;
+  int B, Hin, Win, Cin, up_in;
+  int Ho, Wo, N, ks, stride, pad_t, pad_l;
+  int M, K;
+  int dst_mode;        // 0: dw[k*N + n] (Keras HWIO / pointwise layout)   1: Conv2DTranspose (kh,kw,out,in) flip
+  int m_chunk;         // pixels per block along M (multiple of 32), 0 = auto
+};
+int conv_wgrad(const WgradParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- depthwise 3x3 (dwconv.hip)
+struct DwParams {
+  const bf16_t* x;     // [B,H,W,C] (transform applied on load)
+  const float* w;      // Keras depthwise kernel (3,3,C,1) fp32
+  const bf16_t* dy;    // gradient of the dw output (dgrad / wgrad)
+  bf16_t* y;           // fwd output / dgrad output
+  float* dw;           // wgrad destination (fp32, atomic accumulate)
+  InXform xf;
+  int B, H, W, C;
+};
+int dw_fwd(const DwParams& p, hipStream_t st);
+int dw_dgrad(const DwParams& p, hipStream_t st);
+int dw_wgrad(const DwParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- entry conv 3x3 s2, Cin = 3 (entry.hip)
+struct EntryParams {
+  const uint8_t* images;   // dataset [Ndata, S, S, 3] uint8
+  const int32_t* idx;      // [B] dataset indices of this batch
+  const float* w;          // Keras kernel (3,3,3,Cout) fp32
+  const float* bias;       // [Cout]
+  bf16_t* y;               // [B, Ho, Wo, Cout]
+  float* stats;            // [STAT_REPLICAS][2][Cout]
+  const bf16_t* dy;        // wgrad: [B,Ho,Wo,Cout]
+  float* dw;               // wgrad destination (3,3,3,Cout) fp32
+  int B, S, Cout, Ho, Wo;
+};
+int entry_fwd(const EntryParams& p, hipStream_t st);
+int entry_wgrad(const EntryParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- BatchNorm / elementwise (bn.hip, pool_add.hip)
+// ab (4 rows of C): a = gamma*rstd, b = beta - mean*a, mean, rstd. train: batch stats from the replica rows;
+// eval: moving statistics.
+int bn_finalize(const float* stats, const float* gamma, const float* beta, const float* mmean, const float* mvar,
+                float* ab, int C, float count, float eps, int train, hipStream_t st);
+
+struct BnMoving {          // one BatchNorm layer for the moving-statistics update
+  const float* stats;      // [STAT_REPLICAS][2][C] batch sums
+  float* mmean;
+  float* mvar;
+  int C;
+  float count;
+};
+int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float momentum, hipStream_t st);
+
+enum GradMode { GM_NONE = 0, GM_SAME = 1, GM_SCATTER2 = 2, GM_SUM2X2 = 3, GM_MAXPOOL = 4 };
+struct GradSrc {
+  const bf16_t* p;
+  int mode;
+  int mask;                // multiply this source by [v > 0]
+};
+struct NodeBwdParams {
+  GradSrc src[2];
+  const uint8_t* argmax;   // GM_MAXPOOL: [B, ceil(H/2), ceil(W/2), C] in 0..8
+  const bf16_t* v;         // node value source: raw y (BN node: v = a*y+b) or plain x
+  const float* ab;         // BN coefficients (4 rows) or nullptr for a plain node
+  int relu_node;           // mask the total by [v > 0]
+  bf16_t* out;             // gradient w.r.t. the BN output (BN node) or w.r.t. x (plain node)
+  float* sums;             // [2][C]: sum g, sum g*xhat (BN node) / [C] sum g (plain node) / nullptr
+  int B, H, W, C;
+};
+int node_bwd(const NodeBwdParams& p, hipStream_t st);
+
+struct BnBwdApplyParams {
+  const bf16_t* g;         // gradient w.r.t. BN output (masked)
+  const bf16_t* y;         // raw BN input
+  const float* ab;         // 4 rows: a, b, mean, rstd
+  const float* sums;       // [2][C]
+  bf16_t* dy;              // gradient w.r.t. y
+  float* dgamma;           // flat-grad slots (written, not accumulated) or nullptr
+  float* dbeta;
+  int M, C;
+};
+int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st);
+
+struct PoolResParams {     // x = maxpool3x3s2_same(a*y + b) + res ; argmax recorded
+  const bf16_t* y;
+  const float* ab;
+  const bf16_t* res;       // [B,Ho,Wo,C]
+  bf16_t* out;
+  uint8_t* argmax;
+  int B, H, W, C, Ho, Wo;
+};
+int pool_res_fwd(const PoolResParams& p, hipStream_t st);
+
+struct BnAddParams {       // out = (a*y + b) + (up ? q[h/2][w/2] : q[h][w])
+  const bf16_t* y;
+  const float* ab;
+  const bf16_t* q;
+  int q_up;
+  bf16_t* out;
+  int B, H, W, C;
+};
+int bn_add_fwd(const BnAddParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- head + loss (head.hip)
+struct HeadParams {
+  const bf16_t* x;         // x7_lo [B, R, R, Cin] (the logits are up2(conv1x1(x)))
+  const float* w;          // (1,1,Cin,1)
+  const float* bias;       // (1,)
+  const uint8_t* masks;    // dataset masks [Ndata, 2R, 2R]
+  const int32_t* idx;      // [B]
+  float* h;                // [B, R, R] logits at low resolution
+  double* metrics;         // [8]: bce_sum, correct, sum(p*t), sum(p), sum(t), n_pix, batches, unused
+  bf16_t* dx;              // [B,R,R,Cin]
+  float* dw;               // grad slots for w (Cin) and bias (1) - accumulated
+  float* db;
+  int B, R, Cin;
+  int dice;                // add the Dice loss
+};
+int head_fwd(const HeadParams& p, hipStream_t st);
+int head_bwd(const HeadParams& p, hipStream_t st);
+
+// ---------------------------------------------------------------- optimizer / packing (optim.hip)
+struct AdamParams {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  const uint8_t* trainable;
+  int64_t n;
+  float lr, b1, b2, eps;
+  int* step;               // device step counter (incremented by adam_step_done)
+};
+int adam_update(const AdamParams& p, hipStream_t st);
+int adam_step_done(int* step, hipStream_t st);
+
+enum PackKind { PK_CONV = 0, PK_CONV_DGRAD1x1 = 1, PK_CONVT = 2, PK_CONVT_DGRAD = 3, PK_PW = 4, PK_PW_DGRAD = 5 };
+struct PackView {
+  int kind;
+  int64_t src;             // offset in the flat fp32 buffer
+  int64_t dst;             // offset in the bf16 pack buffer
+  int ks, cin, cout;       // layer geometry (Keras meaning)
+};
+int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
+                 hipStream_t st);
+
+// ---------------------------------------------------------------- misc (optim.hip / datagen.hip)
+int fill_f32(float* p, float v, int64_t n, hipStream_t st);
+int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int rows, int64_t row_bytes,
+                   hipStream_t st);
+int render_cracks(const float* segs, const float* params, uint8_t* images, uint8_t* masks, int n, int img,
+                  int max_seg, hipStream_t st);

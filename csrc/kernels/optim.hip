@@ -1,0 +1,131 @@
+// Optimizer and weight packing.
+//   adam_update:   Keras OptimizerV2 Adam (compile(optimizer="Adam"), client_fit_model.py:157; defaults lr 1e-3,
+//                  beta_1 0.9, beta_2 0.999, epsilon 1e-7) over the single flat fp32 master buffer, trainable
+//                  entries only (BN moving statistics are skipped):
+//                    lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  m,v EMA;  w -= lr_t * m / (sqrt(v) + eps)
+//                  t lives on the device so the whole step can be replayed as one hipGraph.
+//   pack_weights:  fp32 master (Keras layouts) -> bf16 GEMM operands [N][K] for conv_igemm, forward and dgrad,
+//                  including the Conv2DTranspose flip/transposition; one launch for all layers (descriptor table).
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
+  const int t = *p.step + 1;
+  const float lr_t = p.lr * sqrtf(1.f - powf(p.b2, (float)t)) / (1.f - powf(p.b1, (float)t));
+  const int64_t n4 = p.n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+    const uint32_t tm = *reinterpret_cast<const uint32_t*>(p.trainable + 4 * i);
+    if (!tm) continue;
+    float4 w = reinterpret_cast<float4*>(p.p)[i];
+    const float4 g = reinterpret_cast<const float4*>(p.g)[i];
+    float4 m = reinterpret_cast<float4*>(p.m)[i];
+    float4 v = reinterpret_cast<float4*>(p.v)[i];
+    float* wp = &w.x;
+    const float* gp = &g.x;
+    float* mp = &m.x;
+    float* vp = &v.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((tm >> (8 * j)) & 0xffu)) continue;
+      mp[j] = p.b1 * mp[j] + (1.f - p.b1) * gp[j];
+      vp[j] = p.b2 * vp[j] + (1.f - p.b2) * gp[j] * gp[j];
+      wp[j] -= lr_t * mp[j] / (sqrtf(vp[j]) + p.eps);
+    }
+    reinterpret_cast<float4*>(p.p)[i] = w;
+    reinterpret_cast<float4*>(p.m)[i] = m;
+    reinterpret_cast<float4*>(p.v)[i] = v;
+  }
+}
+
+__global__ void step_done_kernel(int* step) { *step += 1; }
+
+__global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* packed, const PackView* views) {
+  const PackView v = views[blockIdx.y];
+  const int taps = v.ks * v.ks;
+  int N, K;
+  switch (v.kind) {
+    case PK_CONV: N = v.cout; K = taps * v.cin; break;
+    case PK_CONV_DGRAD1x1: N = v.cin; K = v.cout; break;
+    case PK_CONVT: N = v.cout; K = 9 * v.cin; break;
+    case PK_CONVT_DGRAD: N = v.cin; K = 9 * v.cout; break;
+    case PK_PW: N = v.cout; K = v.cin; break;
+    default: N = v.cin; K = v.cout; break;   // PK_PW_DGRAD
+  }
+  const int64_t total = (int64_t)N * K;
+  const float* src = flat + v.src;
+  bf16_t* dst = packed + v.dst;
+  for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < total; e += (int64_t)gridDim.x * NT) {
+    const int n = (int)(e / K), k = (int)(e - (int64_t)n * K);
+    int64_t s;
+    switch (v.kind) {
+      case PK_CONV: s = (int64_t)k * v.cout + n; break;                          // HWIO [tap][ci][co]
+      case PK_CONV_DGRAD1x1: s = (int64_t)n * v.cout + k; break;                 // [ci][co] as [N=ci][K=co]
+      case PK_CONVT: {                                                          // (3,3,out,in), flipped
+        const int tap = k / v.cin, c = k - tap * v.cin;
+        s = ((int64_t)(8 - tap) * v.cout + n) * v.cin + c;
+        break;
+      }
+      case PK_CONVT_DGRAD: {                                                    // k = tap*cout + o, n = c
+        const int tap = k / v.cout, o = k - tap * v.cout;
+        s = ((int64_t)tap * v.cout + o) * v.cin + n;
+        break;
+      }
+      case PK_PW: s = (int64_t)k * v.cout + n; break;                           // (1,1,C,F): [c][f]
+      default: s = (int64_t)n * v.cout + k; break;                              // pw dgrad: [N=c][K=f]
+    }
+    dst[e] = f2bf(src[s]);
+  }
+}
+
+__global__ void fill_kernel(float* p, float v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) p[i] = v;
+}
+
+__global__ void gather_rows_kernel(const uint8_t* src, const int32_t* idx, uint8_t* dst, int rows, int64_t row_bytes) {
+  const int r = blockIdx.y;
+  const uint8_t* s = src + (int64_t)idx[r] * row_bytes;
+  uint8_t* d = dst + (int64_t)r * row_bytes;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < row_bytes; i += (int64_t)gridDim.x * NT) d[i] = s[i];
+}
+
+}  // namespace
+
+int adam_update(const AdamParams& p, hipStream_t st) {
+  if (p.n % 4) return 1;
+  int64_t blocks = (p.n / 4 + NT - 1) / NT;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(adam_kernel, dim3((int)blocks), dim3(NT), 0, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int adam_step_done(int* step, hipStream_t st) {
+  hipLaunchKernelGGL(step_done_kernel, dim3(1), dim3(1), 0, st, step);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
+                 hipStream_t st) {
+  int bx = (max_elems + NT - 1) / NT;
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int fill_f32(float* p, float v, int64_t n, hipStream_t st) {
+  int64_t blocks = (n + NT - 1) / NT;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fill_kernel, dim3((int)(blocks < 1 ? 1 : blocks)), dim3(NT), 0, st, p, v, n);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int rows, int64_t row_bytes,
+                   hipStream_t st) {
+  int bx = (int)((row_bytes + NT - 1) / NT);
+  if (bx > 64) bx = 64;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(bx, rows), dim3(NT), 0, st, src, idx, dst, rows, row_bytes);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}

@@ -1,0 +1,260 @@
+"""HIP kernel numerics vs plain fp32 PyTorch references (run on an MI355X via gpurun; marked gpu)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from crack_detection_federatedlearning_grpc_amd._native_loader import hip  # noqa: E402
+from crack_detection_federatedlearning_grpc_amd.models import unet_ref as R  # noqa: E402
+
+DEV = torch.device("cuda")
+PK_CONV, PK_CONV_DGRAD1x1, PK_CONVT, PK_CONVT_DGRAD, PK_PW, PK_PW_DGRAD = range(6)
+
+
+def bf(x):
+    """fp32 tensor -> (bf16 bits as int16 on device, fp32 value of the bf16 rounding)."""
+    b = x.to(torch.bfloat16)
+    return b.view(torch.int16).contiguous().to(DEV), b.float()
+
+
+def from_bits(t):
+    return t.view(torch.bfloat16).float().cpu()
+
+
+def pack(kind, w_keras, ks, cin, cout):
+    flat = w_keras.reshape(-1).float().contiguous().to(DEV)
+    n = ks * ks * cin * cout
+    out = torch.zeros(n, dtype=torch.int16, device=DEV)
+    C = hip()
+    table = C.make_pack_table([(kind, 0, 0, ks, cin, cout)], flat)
+    C.pack_weights(flat, out, table, 1, n)
+    return out
+
+
+def rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def ab_for(c, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.rand(c, generator=g) + 0.5
+    b = torch.randn(c, generator=g) * 0.3
+    ab = torch.zeros(4 * c)
+    ab[:c], ab[c:2 * c] = a, b
+    return ab, a, b
+
+
+@pytest.mark.parametrize("relu,use_ab", [(1, True), (0, False)])
+def test_conv_igemm_3x3_bn_relu_stats(relu, use_ab):
+    torch.manual_seed(0)
+    B, H, Cin, N = 2, 12, 64, 128
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    w = torch.randn(3, 3, Cin, N) * 0.05
+    wb = pack(PK_CONV, w, 3, Cin, N)
+    bias = torch.randn(N) * 0.1
+    ab, a, b = ab_for(Cin)
+    y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+    stats = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
+    hip().conv_igemm(xb, wb, bias.to(DEV), y, stats, ab.to(DEV) if use_ab else None, relu, B, H, H, Cin, 0, H, H, N,
+                     3, 1, 1, 1)
+    t = xf * a + b if use_ab else xf
+    if relu:
+        t = t.relu()
+    t = t.to(torch.bfloat16).float()
+    wr = w.to(torch.bfloat16).float()
+    ref = F.conv2d(t.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), bias, padding=1).permute(0, 2, 3, 1)
+    out = from_bits(y)
+    assert rel(out, ref) < 1e-2
+    st = stats.view(-1, 2, N).sum(0).cpu()
+    assert torch.allclose(st[0], out.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[1], (out * out).sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+
+
+def test_conv_igemm_convT_upsampled_input():
+    torch.manual_seed(1)
+    B, Hs, Cin, N = 2, 6, 32, 64
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    wk = torch.randn(3, 3, N, Cin) * 0.05          # Keras Conv2DTranspose (kh,kw,out,in)
+    wb = pack(PK_CONVT, wk, 3, Cin, N)
+    y = torch.zeros(B, 2 * Hs, 2 * Hs, N, dtype=torch.int16, device=DEV)
+    hip().conv_igemm(xb, wb, None, y, None, None, 1, B, Hs, Hs, Cin, 1, 2 * Hs, 2 * Hs, N, 3, 1, 1, 1)
+    x_up = R.upsample2(xf.permute(0, 3, 1, 2).relu())
+    ref = R.convt_same(x_up, wk.to(torch.bfloat16).float(), None).permute(0, 2, 3, 1)
+    assert rel(from_bits(y), ref) < 1e-2
+
+
+def test_conv_igemm_1x1_stride2_and_partial_tile():
+    torch.manual_seed(2)
+    B, H, Cin, N = 3, 10, 32, 32                   # M = 3*5*5 = 75 < 128: partial M tile
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    w = torch.randn(1, 1, Cin, N) * 0.1
+    wb = pack(PK_CONV, w, 1, Cin, N)
+    y = torch.zeros(B, 5, 5, N, dtype=torch.int16, device=DEV)
+    hip().conv_igemm(xb, wb, None, y, None, None, 0, B, H, H, Cin, 0, 5, 5, N, 1, 2, 0, 0)
+    ref = R.conv2d_same(xf.permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), None, 2).permute(0, 2, 3, 1)
+    assert rel(from_bits(y), ref) < 1e-2
+
+
+def test_convT_dgrad_and_wgrad_match_autograd():
+    torch.manual_seed(3)
+    B, H, Cin, N = 2, 8, 64, 32
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    dyb, dyf = bf(torch.randn(B, H, H, N))
+    wk = (torch.randn(3, 3, N, Cin) * 0.05).to(torch.bfloat16).float()
+    ab, a, b = ab_for(Cin, 4)
+    x = xf.clone().requires_grad_(True)
+    w = wk.clone().requires_grad_(True)
+    t = (x * a + b).relu()
+    out = R.convt_same(t.permute(0, 3, 1, 2), w, None).permute(0, 2, 3, 1)
+    (out * dyf).sum().backward()
+    # dgrad (gradient w.r.t. the transformed input t)
+    tt = (xf * a + b).relu().requires_grad_(True)
+    out2 = R.convt_same(tt.permute(0, 3, 1, 2), wk, None).permute(0, 2, 3, 1)
+    (out2 * dyf).sum().backward()
+    wd = pack(PK_CONVT_DGRAD, wk, 3, Cin, N)
+    dx = torch.zeros(B, H, H, Cin, dtype=torch.int16, device=DEV)
+    hip().conv_igemm(dyb, wd, None, dx, None, None, 0, B, H, H, N, 0, H, H, Cin, 3, 1, 1, 1)
+    assert rel(from_bits(dx), tt.grad) < 1e-2
+    dw = torch.zeros(3 * 3 * N * Cin, device=DEV)
+    hip().conv_wgrad(xb, dyb, dw, ab.to(DEV), 1, B, H, H, Cin, 0, H, H, N, 3, 1, 1, 1, 1, 0)
+    assert rel(dw.view(3, 3, N, Cin).cpu(), w.grad) < 2e-2
+
+
+@pytest.mark.parametrize("stride,up", [(1, 0), (2, 0), (1, 1)])
+def test_conv_wgrad_1x1_and_up(stride, up):
+    torch.manual_seed(5)
+    B, H, Cin, N = 2, 8, 32, 64
+    Ho = H // 2 if stride == 2 else H * (2 if up else 1)
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, N))
+    w = torch.zeros(1, 1, Cin, N, requires_grad=True)
+    xin = xf.permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    out = R.conv2d_same(xin, w, None, stride).permute(0, 2, 3, 1)
+    (out * dyf).sum().backward()
+    dw = torch.zeros(Cin * N, device=DEV)
+    hip().conv_wgrad(xb, dyb, dw, None, 0, B, H, H, Cin, up, Ho, Ho, N, 1, stride, 0, 0, 0, 0)
+    assert rel(dw.view(1, 1, Cin, N).cpu(), w.grad) < 2e-2
+
+
+def test_depthwise_fwd_dgrad_wgrad():
+    torch.manual_seed(6)
+    B, H, C = 2, 10, 64
+    xb, xf = bf(torch.randn(B, H, H, C))
+    dyb, dyf = bf(torch.randn(B, H, H, C))
+    wk = torch.randn(3, 3, C, 1) * 0.2
+    ab, a, b = ab_for(C, 7)
+    C_ = hip()
+    y = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
+    C_.dw_fwd(xb, wk.reshape(-1).to(DEV), y, ab.to(DEV), 1, B, H, H, C)
+    t = (xf * a + b).relu().requires_grad_(True)
+    w = wk.clone().requires_grad_(True)
+    out = F.conv2d(F.pad(t.permute(0, 3, 1, 2), (1, 1, 1, 1)), w.permute(2, 3, 0, 1), None, groups=C)
+    assert rel(from_bits(y), out.permute(0, 2, 3, 1).detach()) < 1e-2
+    (out.permute(0, 2, 3, 1) * dyf).sum().backward()
+    dx = torch.zeros_like(y)
+    C_.dw_dgrad(dyb, wk.reshape(-1).to(DEV), dx, B, H, H, C)
+    assert rel(from_bits(dx), t.grad) < 1e-2
+    dw = torch.zeros(9 * C, device=DEV)
+    C_.dw_wgrad(xb, dyb, dw, ab.to(DEV), 1, B, H, H, C)
+    assert rel(dw.view(3, 3, C, 1).cpu(), w.grad) < 1e-2
+
+
+def test_datagen_matches_numpy():
+    from crack_detection_federatedlearning_grpc_amd.data.device import render_device
+    from crack_detection_federatedlearning_grpc_amd.data.synthetic import image_params, render_numpy
+    n, img = 6, 64
+    imd, mkd = render_device(n, img, seed=3)
+    segs, par = image_params(n, img, 3)
+    imh, mkh = render_numpy(segs, par, img)
+    assert (mkd.cpu().numpy() == mkh).mean() > 0.999
+    assert np.abs(imd.cpu().numpy().astype(int) - imh.astype(int)).max() <= 1
+
+
+def _engine_and_ref(S=64, B=2, seed=0):
+    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
+    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    data = make_synthetic_device(8, S, seed=seed)
+    eng = UNetEngine(table, B, S)
+    eng.bind_data(data.images, data.masks)
+    flat = table.init_flat(seed)
+    eng.set_flat(flat)
+    idx = torch.arange(B, dtype=torch.int32)
+    eng.idx.copy_(idx.to(DEV))
+    x = data.images[:B].float().cpu() / 255.0
+    y = data.masks[:B].float().cpu()[..., None]
+    return table, eng, flat, x, y
+
+
+def test_engine_gradients_match_fp32_reference():
+    table, eng, flat, x, y = _engine_and_ref()
+    eng._zero_step()
+    eng.forward(True)
+    eng.backward()
+    torch.cuda.synchronize()
+    g_eng = eng.grad.cpu()
+    loss_eng = eng.read_metrics("train")["loss"]
+    p = torch.as_tensor(flat).clone().requires_grad_(True)
+    logits, _ = R.unet_forward(p, x, table)
+    loss = R.bce_with_logits_mean(logits, y)
+    g_ref, = torch.autograd.grad(loss, p)
+    assert abs(loss_eng - float(loss)) < 2e-2 * max(1.0, float(loss))
+    bad = []
+    for e in table.entries:
+        if not e.trainable or e.wname == "bias" and e.layer not in ("conv2d_1", "conv2d_2", "conv2d_3", "conv2d_4",
+                                                                   "conv2d_5", "conv2d_6", "conv2d_7", "conv2d_8"):
+            continue
+        a = g_eng[e.offset:e.offset + e.size]
+        b = g_ref[e.offset:e.offset + e.size]
+        cos = float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-20))
+        if cos < 0.98 or rel(a, b) > 0.2:
+            bad.append((e.keras_name, round(cos, 4), round(rel(a, b), 4)))
+    assert not bad, bad
+
+
+def test_engine_bn_moving_stats_and_adam_match_reference():
+    table, eng, flat, x, y = _engine_and_ref(seed=1)
+    eng.train_step(use_graph=False)
+    torch.cuda.synchronize()
+    ref = R.RefTrainer(table, flat)
+    ref.train_step(x, y)
+    new_e = eng.get_flat()
+    new_r = ref.flat.numpy()
+    for e in table.entries:
+        a, b = new_e[e.offset:e.offset + e.size], new_r[e.offset:e.offset + e.size]
+        if e.wname in ("moving_mean", "moving_variance"):
+            assert np.allclose(a, b, rtol=2e-2, atol=2e-3), e.keras_name
+    # first Adam step moves every trainable weight by ~lr * sign(g): compare the update directions
+    d_e = new_e - flat
+    d_r = new_r - flat
+    m = table.trainable_mask() > 0
+    agree = np.mean(np.sign(d_e[m]) == np.sign(d_r[m]))
+    assert agree > 0.9
+
+
+def test_engine_graph_replay_matches_eager_and_learns():
+    table, eng, flat, x, y = _engine_and_ref(seed=2)
+    eng.train_step(use_graph=False)
+    torch.cuda.synchronize()
+    after_eager = eng.get_flat()
+    eng.set_flat(flat)
+    eng.reset_optimizer()
+    eng.train_step(use_graph=True)
+    torch.cuda.synchronize()
+    after_graph = eng.get_flat()
+    assert np.allclose(after_eager, after_graph, atol=1e-5)
+    eng.read_metrics("train")
+    losses = []
+    for i in range(40):
+        eng.train_step(use_graph=True)
+        if i % 10 == 9:
+            losses.append(eng.read_metrics("train")["loss"])
+    assert losses[-1] < losses[0]
