@@ -52,6 +52,8 @@ class UNetEngine:
         self.table = table
         self.B, self.S = batch, img
         self.dev = torch.device(device)
+        if self.dev.type == "cuda" and self.dev.index is None:
+            self.dev = torch.device("cuda", torch.cuda.current_device())
         self.dice = 1 if loss == "bce_dice" else 0
         self.lr, self.b1, self.b2, self.adam_eps = lr, beta1, beta2, adam_eps
         self.momentum, self.bn_eps = bn_momentum, bn_eps
@@ -304,7 +306,7 @@ class UNetEngine:
                 dq = dxlo
             else:
                 dq = D[f"d{k}_dq"]
-                C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, prev_t, None, 0, dq, None, B, prevres, prevres, F)
+                C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
             C.conv_wgrad(prev_t, dq, self.G(rc, "kernel"), None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
                          F, 1, 1, 0, 0, 0, 0)
             self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dq) == sum(g_B) (the BN_B node has no ReLU)

@@ -1,0 +1,53 @@
+"""RCCL data plane of the FL client, rehearsed over gloo with world_size 2 (separate processes, CPU)."""
+import multiprocessing as mp
+import os
+import threading
+
+import numpy as np
+import pytest
+
+
+def _client_proc(port, name, delta, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.client import FLClient
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+    from fakes import FakeTrainer
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=2, register_window_s=20, ready_stall_s=0,
+                   poll_period_s=0.05, long_poll_s=1.0, max_rounds=2, client_weight_file="", rpc_timeout_s=60)
+    table = ParamTable()
+    tr = FakeTrainer(table, delta, n_samples=10 if delta < 2 else 30)
+    c = FLClient(cfg, lambda: tr, name=name, target=f"127.0.0.1:{port}",
+                 aggregator_factory=lambda info: RcclAggregator.from_ready_info(info, cfg))
+    st = c.run()
+    e = table.entries[0]
+    q.put((name, st, float(tr.flat[e.offset])))
+
+
+def test_rccl_mode_two_processes(tmp_path):
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=2, register_window_s=20, ready_stall_s=0,
+                   max_rounds=2, work_dir=str(tmp_path), server_weight_file="", long_poll_s=1.0)
+    srv = FLServer(cfg, global_flat=np.zeros(table.total, np.float32), table=table)
+    port = srv.start(0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_client_proc, args=(port, f"c{i}", d, q)) for i, d in enumerate([1.0, 5.0])]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(30)
+    srv.stop()
+    # weighted: round1 avg = (1*10 + 5*30)/40 = 4 ; round2: each adds its delta to 4 -> (5*10 + 9*30)/40 = 8
+    vals = {n: v for n, _, v in res}
+    assert all(st == "FIN" for _, st, _ in res)
+    assert np.isclose(vals["c0"], 8.0) and np.isclose(vals["c1"], 8.0)
+    e = table.entries[0]
+    assert np.isclose(srv.state.global_flat[e.offset], 8.0)     # rank 0 uploaded the all-reduced model
