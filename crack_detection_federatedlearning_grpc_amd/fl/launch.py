@@ -1,0 +1,60 @@
+"""One-node FL launcher: the gRPC server + one client process per GPU.
+
+    python -m crack_detection_federatedlearning_grpc_amd.fl.launch --num-clients 8 --preset gpu8-256
+
+Replaces the reference's manual procedure (start ``fl_server.py``, then start N ``fl_client.py`` by hand on the
+same host, all on one GPU - SURVEY §4). Each client process gets ``LOCAL_RANK`` = its GPU, registers over gRPC,
+and - with ``--data-plane rccl`` - joins the RCCL communicator whose rendezvous the server hands out in the READY
+reply; the FedAvg of every round is then a weighted all-reduce over xGMI. ``--device cpu`` runs the same topology
+with gloo (CPU plumbing).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
+from typing import List, Optional
+
+from .. import config as _config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cfg = _config.parse(argv)
+    n = cfg.num_clients or 1
+    cfg.num_clients = n
+    from .server import FLServer
+    srv = FLServer(cfg)
+    port = srv.start()
+    print(f"[launch] server on :{port}, starting {n} client process(es) (data plane {cfg.data_plane})", flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    procs = []
+    for r in range(n):
+        e = dict(env, LOCAL_RANK=str(r), FL_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "fl_client.py"), *argv,
+                                       "--port", str(port), "--host", "127.0.0.1"], env=e))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            time.sleep(0.5)
+        rc = max(p.returncode or 0 for p in procs)
+        srv.done.wait(5.0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        srv.stop(0.5)
+    hist = srv.state.history
+    if hist:
+        print(f"[launch] {len(hist)} round(s); last round wall-clock "
+              f"{hist[-1].t_end - hist[-1].t_start:.2f}s; clients {hist[-1].clients}")
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

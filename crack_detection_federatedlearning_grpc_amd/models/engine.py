@@ -70,6 +70,7 @@ class UNetEngine:
         self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
         self.eval_metrics = torch.zeros(8, dtype=torch.float64, device=dev)
         self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         self._build_pack()
         self._alloc()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -230,11 +231,22 @@ class UNetEngine:
                            float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
         return b["ab"]
 
+    def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
+               pad_l) -> None:
+        """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture)."""
+        need = self.C.conv_splits(B * Ho * Wo, N, ks * ks * Cin, Cin)
+        if need > 1 and need * B * Ho * Wo * N > self.ws.numel():
+            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("split-K workspace must be sized before graph capture")
+            self.ws = torch.empty(need * B * Ho * Wo * N, dtype=torch.float32, device=self.dev)
+        self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
+                          pad_l, self.ws if need > 1 else None)
+
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
               Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor]) -> None:
         pad = (ks - 1) // 2 if stride == 1 else 0
         B = self.B
-        self.C.conv_igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
+        self._igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
                           N, ks, stride, pad, pad)
 
     def forward(self, train: bool = True) -> None:
@@ -310,12 +322,12 @@ class UNetEngine:
             C.conv_wgrad(prev_t, dq, self.G(rc, "kernel"), None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
                          F, 1, 1, 0, 0, 0, 0)
             self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dq) == sum(g_B) (the BN_B node has no ReLU)
-            C.conv_igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
+            self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
             # convT2: input relu(BN_A(c1))
             C.conv_wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], self.G(t2, "kernel"), bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
                          F, 3, 1, 1, 1, 1, 0)
-            C.conv_igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_dz"], None, None, 0, B, Rk, Rk, F,
+            self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_dz"], None, None, 0, B, Rk, Rk, F,
                          0, Rk, Rk, F, 3, 1, 1, 1)
             C.node_bwd(D[f"d{k}_dz"], GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c1"], bnA["ab"], 1, D[f"d{k}_g"],
                        bnA["sums"], B, Rk, Rk, F)
@@ -324,7 +336,7 @@ class UNetEngine:
             # convT1: input relu(up?(prev))
             C.conv_wgrad(prev_t, D[f"d{k}_dc"], self.G(t1, "kernel"), None, 1, B, prevres, prevres, cprev, up, Rk,
                          Rk, F, 3, 1, 1, 1, 1, 0)
-            C.conv_igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
+            self._igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
                          F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
             C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None, prev_t,
@@ -351,7 +363,7 @@ class UNetEngine:
             # pointwise 2
             C.conv_wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], self.G(s2, "pointwise_kernel"), None, 0, B, H, H, F, 0, H, H,
                          F, 1, 1, 0, 0, 0, 0)
-            C.conv_igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
+            self._igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
                          H, H, F, 1, 1, 0, 0)
             # depthwise 2 on relu(BN_a(y1))
             C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.G(s2, "depthwise_kernel"), bna["ab"], 1, B, H, H, F)
@@ -363,7 +375,7 @@ class UNetEngine:
             # pointwise 1
             C.conv_wgrad(A[f"e{k}_d1"], D[f"e{k}_dy"], self.G(s1, "pointwise_kernel"), None, 0, B, H, H, cin, 0, H,
                          H, F, 1, 1, 0, 0, 0, 0)
-            C.conv_igemm(D[f"e{k}_dy"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
+            self._igemm(D[f"e{k}_dy"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
                          H, H, cin, 1, 1, 0, 0)
             # depthwise 1 on relu(x_in)
             C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.G(s1, "depthwise_kernel"), xin.ab, 1, B, H, H, cin)
@@ -372,7 +384,7 @@ class UNetEngine:
             C.conv_wgrad(xin.t, dx_out, self.G(rc, "kernel"), xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                          1, 2, 0, 0, 0, 0)
             self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dx_out) == sum(g_b): max-pool routing keeps sums
-            C.conv_igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
+            self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                          H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
             if k > 0:
                 C.node_bwd(D[f"e{k}_dz0"], GM_SAME, 1, D[f"e{k}_dres"], GM_SCATTER2, 0, None, xin.t, None, 0,

@@ -81,11 +81,22 @@ def upsample2(x):
     return x.repeat_interleave(2, dim=2).repeat_interleave(2, dim=3)
 
 
+def _bf16_st(t: torch.Tensor) -> torch.Tensor:
+    """bf16 rounding with a straight-through gradient (emulates bf16 activation storage)."""
+    return t + (t.to(torch.bfloat16).float() - t).detach()
+
+
 def unet_forward(flat: torch.Tensor, x_nhwc: torch.Tensor, table: Optional[ParamTable] = None,
-                 training: bool = True, momentum: float = 0.99, eps: float = 1e-3
+                 training: bool = True, momentum: float = 0.99, eps: float = 1e-3, emulate_bf16: bool = False
                  ) -> Tuple[torch.Tensor, Dict[str, Tuple[torch.Tensor, torch.Tensor]]]:
-    """x_nhwc: (B,H,W,3) float in [0,1]. Returns (logits NHWC (B,H,W,1), {bn_layer: (new_mm, new_mv)})."""
+    """x_nhwc: (B,H,W,3) float in [0,1]. Returns (logits NHWC (B,H,W,1), {bn_layer: (new_mm, new_mv)}).
+
+    ``emulate_bf16``: round to bf16 at exactly the points where the MI355X engine stores activations or feeds bf16
+    MFMA operands (conv outputs, depthwise outputs, residual joins, MFMA-packed weights, transformed MFMA inputs);
+    gradients pass straight through. Used to separate dataflow bugs from bf16 storage error in the GPU tests.
+    """
     table = table or ParamTable()
+    r = _bf16_st if emulate_bf16 else (lambda t: t)
     P = lambda l, w: _p(flat, table, l, w)  # noqa: E731
     bn_updates: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
 
@@ -95,29 +106,34 @@ def unet_forward(flat: torch.Tensor, x_nhwc: torch.Tensor, table: Optional[Param
         bn_updates[name] = (nm, nv)
         return y
 
+    def sep(x, s):
+        c = x.shape[1]
+        d = r(F.conv2d(F.pad(x, (1, 1, 1, 1)), P(s, "depthwise_kernel").permute(2, 3, 0, 1), None, groups=c))
+        return r(F.conv2d(d, r(P(s, "pointwise_kernel")).permute(3, 2, 0, 1), P(s, "bias")))
+
     names = iter([ly.name for ly in table.weighted_layers()])
     x = x_nhwc.permute(0, 3, 1, 2)
     n = next(names)
-    x = conv2d_same(x, P(n, "kernel"), P(n, "bias"), 2)
+    x = r(conv2d_same(x, P(n, "kernel"), P(n, "bias"), 2))
     x = F.relu(bn(x, next(names)))
     prev = x
     for _f in ENC_FILTERS:
-        s1, b1, s2, b2, r = next(names), next(names), next(names), next(names), next(names)
+        s1, b1, s2, b2, rc = next(names), next(names), next(names), next(names), next(names)
         x = F.relu(x)
-        x = bn(sepconv_same(x, P(s1, "depthwise_kernel"), P(s1, "pointwise_kernel"), P(s1, "bias")), b1)
+        x = bn(sep(x, s1), b1)
         x = F.relu(x)
-        x = bn(sepconv_same(x, P(s2, "depthwise_kernel"), P(s2, "pointwise_kernel"), P(s2, "bias")), b2)
+        x = bn(sep(x, s2), b2)
         x = maxpool_same(x)
-        x = x + conv2d_same(prev, P(r, "kernel"), P(r, "bias"), 2)
+        x = r(x + r(conv2d_same(r(prev), r(P(rc, "kernel")), P(rc, "bias"), 2)))
         prev = x
     for _f in DEC_FILTERS:
-        t1, b1, t2, b2, r = next(names), next(names), next(names), next(names), next(names)
+        t1, b1, t2, b2, rc = next(names), next(names), next(names), next(names), next(names)
         x = F.relu(x)
-        x = bn(convt_same(x, P(t1, "kernel"), P(t1, "bias")), b1)
-        x = F.relu(x)
-        x = bn(convt_same(x, P(t2, "kernel"), P(t2, "bias")), b2)
+        x = bn(r(convt_same(x, r(P(t1, "kernel")), P(t1, "bias"))), b1)
+        x = r(F.relu(x))
+        x = bn(r(convt_same(x, r(P(t2, "kernel")), P(t2, "bias"))), b2)
         x = upsample2(x)
-        x = x + conv2d_same(upsample2(prev), P(r, "kernel"), P(r, "bias"), 1)
+        x = r(x + r(conv2d_same(upsample2(prev), r(P(rc, "kernel")), P(rc, "bias"), 1)))
         prev = x
     h = next(names)
     logits = conv2d_same(x, P(h, "kernel"), P(h, "bias"), 1)

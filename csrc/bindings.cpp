@@ -41,7 +41,7 @@ InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(a
 
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
-                   int pad_l) {
+                   int pad_l, OptT ws) {
   ConvParams p{};
   p.x = ptr<const bf16_t>(x, "x");
   p.wt = ptr<const bf16_t>(wt, "wt");
@@ -53,11 +53,19 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
   p.M = B * Ho * Wo;
   p.K = ks * ks * Cin;
+  p.ws = optr<float>(ws, "ws");
+  p.ws_elems = p.ws ? ws->numel() : 0;
   TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv_igemm: x size");
   TORCH_CHECK(wt.numel() >= (int64_t)N * p.K, "conv_igemm: wt size");
   TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv_igemm: y size");
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
   ok(conv_igemm(p, stream()), "conv_igemm");
+}
+
+int conv_splits_op(int M, int N, int K, int Cin) {
+  ConvParams p{};
+  p.M = M; p.N = N; p.K = K; p.Cin = Cin;
+  return conv_igemm_splits(p);
 }
 
 void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win, int Cin,
@@ -333,7 +341,11 @@ void gather_rows_u8_op(at::Tensor src, at::Tensor idx, at::Tensor dst, int64_t r
 PYBIND11_MODULE(_C, m) {
   m.doc() = "CDNA4 (gfx950) HIP kernels of the crack-segmentation FL trainer";
   m.attr("STAT_REPLICAS") = STAT_REPLICAS;
-  m.def("conv_igemm", &conv_igemm_op);
+  m.def("conv_igemm", &conv_igemm_op, py::arg("x"), py::arg("wt"), py::arg("bias"), py::arg("y"), py::arg("stats"),
+        py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"),
+        py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"),
+        py::arg("pad_l"), py::arg("ws") = py::none());
+  m.def("conv_splits", &conv_splits_op);
   m.def("conv_wgrad", &conv_wgrad_op);
   m.def("dw_fwd", &dw_fwd_op);
   m.def("dw_dgrad", &dw_dgrad_op);

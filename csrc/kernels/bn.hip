@@ -224,7 +224,7 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
   const int lanes = NT / (p.C / 8);
   const int64_t npix = (int64_t)p.B * p.H * p.W;
   int64_t blocks = (npix + lanes - 1) / lanes;
-  if (blocks > 512) blocks = 512;   // bounded grid: one set of channel atomics per block
+  if (blocks > 2048) blocks = 2048;   // bounded grid: one set of channel atomics per block
   hipLaunchKernelGGL(node_bwd_kernel, dim3((int)blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

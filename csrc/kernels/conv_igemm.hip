@@ -11,73 +11,105 @@
 // permutation lives in the packed weight matrix (csrc/kernels/optim.hip, pack kernel), so the same kernel serves
 // the transposed conv and every data-gradient (dgrad = forward conv of dy with the dgrad-packed weights).
 //
-// Tiling: block 128(M) x BN(N), K-step 32, 256 threads = 4 waves (WM x WN), each wave (128/WM) x (BN/WN) of
-// 16x16 MFMA fragments. Operands are register-staged (global_load_dwordx4 -> transform -> ds_write_b128) into two
-// LDS buffers; the next K-tile's global loads are issued before the current tile's MFMAs (one barrier per K-step).
-// LDS rows are padded to 40 bf16 (80 B) so the 16 row-reads of a ds_read_b128 lane group hit distinct bank slots.
+// Tiling: block BM(M) x BN(N), K-step 32, 256 threads = 4 waves (WM x WN) of 16x16 MFMA fragments.
+// Operands are register-staged (global_load_dwordx4 -> BN/ReLU transform -> ds_write_b128) into two LDS buffers;
+// the next K-tile's global loads are issued before the current tile's MFMAs (one barrier per K-step). LDS rows are
+// padded to 40 bf16 (80 B). The (tap, channel) position of a thread's K chunk advances incrementally (no integer
+// division in the K loop). Epilogue: the bf16 tile is staged through LDS so every store is a full 16-byte vector
+// and the BN statistics are summed from the rounded values; per-block partial sums go to one of STAT_REPLICAS
+// replica rows to keep atomic contention low.
+// Deep low-M layers (e.g. 16x16 maps with K = 2304) split K over gridDim.z into an fp32 workspace; a second kernel
+// adds the partials and runs the same epilogue.
 #include "common.h"
 #include "launch.h"
 
 namespace {
 
-constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int LDK = BK + 8;   // padded LDS row (bf16 elements)
 constexpr int NT = 256;
 
-template <int BN_, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p) {
+template <int BM_, int BN_, int WM, int WN>
+__global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_per_split, float* __restrict__ ws) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int TM = BM / WM, TN = BN_ / WN;
+  constexpr int TM = BM_ / WM, TN = BN_ / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int B_CHUNKS = BN_ * BK / 8;                 // 16-byte chunks in one B tile
+  constexpr int A_PER_T = BM_ / 64;                      // 16-byte A chunks per thread per K-step
+  constexpr int B_CHUNKS = BN_ * BK / 8;
   constexpr int B_PER_T = (B_CHUNKS + NT - 1) / NT;
+  constexpr int SA = 2 * BM_ * LDK, SB = 2 * BN_ * LDK;  // bf16 elements
+  constexpr int LDC = BN_ + 8;
+  static_assert(BM_ * LDC <= SA + SB, "C staging tile must fit in the operand buffers");
 
-  __shared__ __attribute__((aligned(16))) bf16_t sA[2][BM][LDK];
-  __shared__ __attribute__((aligned(16))) bf16_t sB[2][BN_][LDK];
-  __shared__ float sred[2][WM][BN_];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SA + SB];
+  __shared__ float sred[2][NT / 64][BN_];
+  bf16_t (*sA)[BM_][LDK] = reinterpret_cast<bf16_t (*)[BM_][LDK]>(smem);
+  bf16_t (*sB)[BN_][LDK] = reinterpret_cast<bf16_t (*)[BN_][LDK]>(smem + SA);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int mBlock = blockIdx.x * BM, nBlock = blockIdx.y * BN_;
+  const int mBlock = blockIdx.x * BM_, nBlock = blockIdx.y * BN_;
   const int HWo = p.Ho * p.Wo;
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
+  const int KT = p.K / BK;
+  const int kt0 = blockIdx.z * kt_per_split;
+  const int kt1 = imin(KT, kt0 + kt_per_split);
 
   // ---- per-thread A rows (fixed over the K loop) ----
   const int kq = tid & 3;
-  int a_b[2], a_ih[2], a_iw[2];
-  bool a_ok[2];
+  int a_off[A_PER_T], a_ih[A_PER_T], a_iw[A_PER_T];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < A_PER_T; ++i) {
     const int m = mBlock + (tid >> 2) + i * 64;
-    a_ok[i] = m < p.M;
-    const int mm = a_ok[i] ? m : 0;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
     const int b = mm / HWo, r = mm - b * HWo;
     const int oh = r / p.Wo, ow = r - oh * p.Wo;
-    a_b[i] = b;
-    a_ih[i] = oh * p.stride - p.pad_t;
+    a_off[i] = b * p.Hin * p.Win;
+    a_ih[i] = ok ? oh * p.stride - p.pad_t : -(1 << 28);   // invalid rows never pass the bounds test
     a_iw[i] = ow * p.stride - p.pad_l;
   }
+  // (tap, channel) of this thread's chunk at kt0
+  int c, ky, kx;
+  {
+    const int k0 = kt0 * BK + kq * 8;
+    const int tap = k0 / p.Cin;
+    c = k0 - tap * p.Cin;
+    ky = tap / p.ks;
+    kx = tap - ky * p.ks;
+  }
+  const bool has_ab = p.xf.ab != nullptr;
+  const int relu = p.xf.relu;
 
-  uint4 ra[2], rb[B_PER_T];
-  const int KT = p.K / BK;
-
+  uint4 ra[A_PER_T], rb[B_PER_T];
   auto load_tiles = [&](int kt) {
-    const int k0 = kt * BK + kq * 8;
-    const int tap = k0 / p.Cin, c = k0 - tap * p.Cin;
-    const int ky = tap / p.ks, kx = tap - ky * p.ks;
+    float ca[8], cb[8];
+    if (has_ab) {
+      const float4 a0 = *reinterpret_cast<const float4*>(p.xf.ab + c);
+      const float4 a1 = *reinterpret_cast<const float4*>(p.xf.ab + c + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(p.xf.ab + p.xf.C + c);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.xf.ab + p.xf.C + c + 4);
+      ca[0] = a0.x; ca[1] = a0.y; ca[2] = a0.z; ca[3] = a0.w; ca[4] = a1.x; ca[5] = a1.y; ca[6] = a1.z; ca[7] = a1.w;
+      cb[0] = b0.x; cb[1] = b0.y; cb[2] = b0.z; cb[3] = b0.w; cb[4] = b1.x; cb[5] = b1.y; cb[6] = b1.z; cb[7] = b1.w;
+    }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < A_PER_T; ++i) {
       const int ih = a_ih[i] + ky, iw = a_iw[i] + kx;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (a_ok[i] && ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
-        const size_t off = (((size_t)a_b[i] * p.Hin + (ih >> p.up_in)) * p.Win + (iw >> p.up_in)) * p.Cin + c;
+      if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
+        const size_t off = ((size_t)a_off[i] + (size_t)(ih >> p.up_in) * p.Win + (iw >> p.up_in)) * p.Cin + c;
         v = *reinterpret_cast<const uint4*>(p.x + off);
-        if (p.xf.ab || p.xf.relu) {
+        if (has_ab || relu) {
           float f[8];
           unpack8(v, f);
+          if (has_ab) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = xform1(f[j], p.xf, c + j);
+            for (int j = 0; j < 8; ++j) f[j] = fmaf(ca[j], f[j], cb[j]);
+          }
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          }
           v = pack8(f);
         }
       }
@@ -91,12 +123,20 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p) {
         rb[i] = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + n) * p.K + kt * BK + q * 8);
       }
     }
+    // advance (tap, channel) to the next K-step
+    c += BK;
+    if (c >= p.Cin) {
+      c -= p.Cin;
+      if (++kx == p.ks) {
+        kx = 0;
+        ++ky;
+      }
+    }
   };
 
   auto store_tiles = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<uint4*>(&sA[buf][(tid >> 2) + i * 64][kq * 8]) = ra[i];
+    for (int i = 0; i < A_PER_T; ++i) *reinterpret_cast<uint4*>(&sA[buf][(tid >> 2) + i * 64][kq * 8]) = ra[i];
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int ch = tid + i * NT;
@@ -110,14 +150,17 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  load_tiles(0);
-  store_tiles(0);
+  if (kt0 < kt1) {
+    load_tiles(kt0);
+    store_tiles(0);
+  }
   __syncthreads();
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_tiles(kt + 1);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) load_tiles(kt + 1);
     s8v af[FM], bfg[FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const s8v*>(&sA[cur][wm * TM + i * 16 + fr][fk]);
@@ -126,72 +169,183 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
-    if (kt + 1 < KT) store_tiles(cur ^ 1);
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    if (more) store_tiles(cur ^ 1);
     __syncthreads();
   }
 
-  // ---- epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r ----
+  // ---- split-K: raw fp32 partials, the reduce kernel runs the epilogue ----
+  if (ws != nullptr) {
+    float* dst = ws + (size_t)blockIdx.z * p.M * p.N;
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = nBlock + wn * TN + j * 16 + (lane & 15);
-    const float bias = p.bias ? p.bias[n] : 0.f;
-    float s = 0.f, s2 = 0.f;
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
+      for (int j = 0; j < FN; ++j) {
+        const int n = nBlock + wn * TN + j * 16 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mBlock + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < p.M) {
-          const bf16_t yb = f2bf(acc[i][j][r] + bias);
-          p.y[(size_t)m * p.N + n] = yb;
-          const float yv = bf2f(yb);
-          s += yv;
-          s2 += yv * yv;
+        for (int r = 0; r < 4; ++r) {
+          const int m = mBlock + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (m < p.M) dst[(size_t)m * p.N + n] = acc[i][j][r];
         }
       }
-    }
-    if (p.stats) {
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 16) {
-        sred[0][wm][wn * TN + j * 16 + lane] = s;
-        sred[1][wm][wn * TN + j * 16 + lane] = s2;
+    return;
+  }
+
+  // ---- epilogue: bias, bf16, stage through LDS (C/D layout: col = lane&15, row = (lane>>4)*4 + r) ----
+  bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int cl = wn * TN + j * 16 + (lane & 15);
+    const float bias = p.bias ? p.bias[nBlock + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sC[wm * TM + i * 16 + (lane >> 4) * 4 + r][cl] = f2bf(acc[i][j][r] + bias);
+  }
+  __syncthreads();
+  constexpr int CG = BN_ / 8;                 // 16-byte column groups per row
+  constexpr int ROWS_PER_PASS = NT / CG;
+  const int cg = tid % CG;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int r0 = 0; r0 < BM_; r0 += ROWS_PER_PASS) {
+    const int row = r0 + tid / CG;
+    const int m = mBlock + row;
+    if (m < p.M) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + nBlock + cg * 8) = v;
+      if (p.stats) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          s[q] += f[q];
+          s2[q] += f[q] * f[q];
+        }
       }
     }
   }
   if (p.stats) {
-    // combine the WM wave rows, then one atomic per (stat, column) into this block's replica row
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      for (int o = CG; o < 64; o <<= 1) {
+        s[q] += __shfl_xor(s[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
+    if (lane < CG) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        sred[0][wid][cg * 8 + q] = s[q];
+        sred[1][wid][cg * 8 + q] = s2[q];
+      }
+    }
     __syncthreads();
     float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
-      const int st = e / BN_, c = e - st * BN_;
+      const int st = e / BN_, cc = e - st * BN_;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) v += sred[st][w][c];
-      atomicAdd(&rep[st * p.N + nBlock + c], v);
+      for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
+      atomicAdd(&rep[st * p.N + nBlock + cc], v);
     }
   }
 }
 
+// sum split-K partials + bias -> bf16, with the BN statistics epilogue
+__global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const float* __restrict__ ws, int splits) {
+  __shared__ float red[2][NT / 64][256];
+  const int G = p.N >> 3, lanes = NT / G;
+  const int cg = threadIdx.x % G, c0 = cg * 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float bias[8], s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bias[q] = p.bias ? p.bias[c0 + q] : 0.f;
+  const size_t plane = (size_t)p.M * p.N;
+  for (int m = blockIdx.x * lanes + threadIdx.x / G; m < p.M; m += gridDim.x * lanes) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = bias[q];
+    const float* src = ws + (size_t)m * p.N + c0;
+    for (int z = 0; z < splits; ++z) {
+      const float4 u0 = *reinterpret_cast<const float4*>(src + z * plane);
+      const float4 u1 = *reinterpret_cast<const float4*>(src + z * plane + 4);
+      v[0] += u0.x; v[1] += u0.y; v[2] += u0.z; v[3] += u0.w;
+      v[4] += u1.x; v[5] += u1.y; v[6] += u1.z; v[7] += u1.w;
+    }
+    const uint4 o = pack8(v);
+    *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + c0) = o;
+    float f[8];
+    unpack8(o, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      s[q] += f[q];
+      s2[q] += f[q] * f[q];
+    }
+  }
+  if (!p.stats) return;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    for (int o = G; o < 64; o <<= 1) {
+      s[q] += __shfl_xor(s[q], o, 64);
+      s2[q] += __shfl_xor(s2[q], o, 64);
+    }
+  if (lane < G) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[0][wid][c0 + q] = s[q];
+      red[1][wid][c0 + q] = s2[q];
+    }
+  }
+  __syncthreads();
+  float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+  for (int e = threadIdx.x; e < 2 * p.N; e += NT) {
+    const int st = e / p.N, cc = e - st * p.N;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) v += red[st][w][cc];
+    atomicAdd(&rep[st * p.N + cc], v);
+  }
+}
+
+template <int BM_, int BN_, int WM, int WN>
+void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
+  const int KT = p.K / BK;
+  const int per = (KT + splits - 1) / splits;
+  dim3 grid((p.M + BM_ - 1) / BM_, p.N / BN_, splits);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? ws : nullptr);
+}
+
 }  // namespace
 
+int conv_igemm_splits(const ConvParams& p) {
+  const int KT = p.K / BK;
+  const int bm = (p.N <= 64 && p.M >= 256 * 512) ? 256 : 128;
+  const int bn = p.N >= 128 ? 128 : p.N;
+  const int blocks = ((p.M + bm - 1) / bm) * (p.N / bn);
+  if (blocks >= 192 || KT < 16) return 1;
+  int s = (384 + blocks - 1) / blocks;
+  if (s > KT / 8) s = KT / 8;
+  if (s > 16) s = 16;
+  return s < 1 ? 1 : s;
+}
+
 int conv_igemm(const ConvParams& p, hipStream_t st) {
-  if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin) return 1;
-  dim3 blk(NT);
-  if (p.N % 128 == 0 && p.N >= 128) {
-    dim3 grid((p.M + BM - 1) / BM, p.N / 128);
-    hipLaunchKernelGGL((conv_igemm_kernel<128, 2, 2>), grid, blk, 0, st, p);
-  } else if (p.N % 64 == 0) {
-    dim3 grid((p.M + BM - 1) / BM, p.N / 64);
-    hipLaunchKernelGGL((conv_igemm_kernel<64, 2, 2>), grid, blk, 0, st, p);
-  } else if (p.N % 32 == 0) {
-    dim3 grid((p.M + BM - 1) / BM, p.N / 32);
-    hipLaunchKernelGGL((conv_igemm_kernel<32, 4, 1>), grid, blk, 0, st, p);
-  } else {
-    return 2;
+  if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
+  int splits = conv_igemm_splits(p);
+  if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
+  const bool big_m = p.M >= 256 * 512;
+  if (p.N % 128 == 0) launch<128, 128, 2, 2>(p, splits, p.ws, st);
+  else if (p.N == 64 && big_m) launch<256, 64, 4, 1>(p, splits, p.ws, st);
+  else if (p.N == 64) launch<128, 64, 2, 2>(p, splits, p.ws, st);
+  else if (p.N == 32 && big_m) launch<256, 32, 4, 1>(p, splits, p.ws, st);
+  else if (p.N == 32) launch<128, 32, 4, 1>(p, splits, p.ws, st);
+  else return 2;
+  if (splits > 1) {
+    const int G = p.N / 8, lanes = NT / G;
+    int blocks = (p.M + lanes - 1) / lanes;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(NT), 0, st, p, p.ws, splits);
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

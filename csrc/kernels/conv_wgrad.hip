@@ -2,14 +2,15 @@
 //
 // The reduction runs over pixels (M = B*Ho*Wo, up to millions), which in NHWC is the OUTER dimension of both
 // operands. Both tiles are therefore staged in their natural [m][k] / [m][n] row layout (16-byte coalesced
-// global loads, the producer's BN-apply + ReLU folded into the x load) and the MFMA operands - which need 8
+// global loads, the producer's BN-apply + ReLU folded into the x load with coefficients held in registers - a
+// block's k range is fixed, so each thread's channels never change) and the MFMA operands - which need 8
 // consecutive m per lane - are read with the CDNA4 transposing LDS read ds_read_b64_tr_b16
 // (__builtin_amdgcn_ds_read_tr16_b64): no register or LDS transpose pass.
 //
-// Output tile BKO(k) x BNO(n), 4 waves 2x2, reduction step 32 pixels, register-staged double buffer.
-// The M range is split over gridDim.z; partial tiles are combined with fp32 atomics directly into the layer's
-// slot of the flat gradient buffer, writing Keras layouts (HWIO for Conv2D / pointwise, (kh,kw,out,in) with the
-// spatial flip for Conv2DTranspose: dst_mode 1).
+// Output tile BKO(k) x BNO(n) (128x128 for the big K*N layers, down to 32x32), 4 waves 2x2, reduction step 32
+// pixels, register-staged double buffer. The M range is split over gridDim.z so the grid holds ~512 long-running
+// blocks; partial tiles are combined with fp32 atomics directly into the layer's slot of the flat gradient buffer,
+// writing Keras layouts (HWIO for Conv2D / pointwise; (kh,kw,out,in) with the spatial flip for Conv2DTranspose).
 #include "common.h"
 #include "launch.h"
 
@@ -30,6 +31,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
   constexpr int FK = TK / 16, FN = TN / 16;
   constexpr int LDX = BKO + 8, LDG = BNO + 8;
   constexpr int XC = RM * BKO / 8, GC = RM * BNO / 8;   // 16-byte chunks per tile
+  constexpr int XPT = (XC + NT - 1) / NT, GPT = (GC + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) bf16_t sX[2][RM][LDX];
   __shared__ __attribute__((aligned(16))) bf16_t sG[2][RM][LDG];
 
@@ -42,44 +44,68 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
   const int HWo = p.Ho * p.Wo;
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
 
-  // this thread's x chunk: fixed k (channel group), row within the step
-  const bool has_x = tid < XC, has_g = tid < GC;
-  const int xm = tid / (BKO / 8), xk = kBlock + (tid % (BKO / 8)) * 8;
+  // x chunks: fixed channel group (k range of this block), rows xm + i * (NT / (BKO/8))
+  constexpr int XW = BKO / 8;
+  const int xk = kBlock + (tid % XW) * 8;
   const int tap = xk / p.Cin, xc = xk - tap * p.Cin;
   const int ky = tap / p.ks, kx = tap - ky * p.ks;
-  const int gm = tid / (BNO / 8), gn = nBlock + (tid % (BNO / 8)) * 8;
+  const bool has_ab = p.xf.ab != nullptr;
+  float ca[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = has_ab ? p.xf.ab[xc + j] : 1.f;
+    cb[j] = has_ab ? p.xf.ab[p.xf.C + xc + j] : 0.f;
+  }
+  constexpr int GW = BNO / 8;
+  const int gn = nBlock + (tid % GW) * 8;
 
-  uint4 rx = make_uint4(0, 0, 0, 0), rg = make_uint4(0, 0, 0, 0);
+  uint4 rx[XPT], rg[GPT];
   auto load = [&](int m0) {
-    if (has_x) {
-      const int m = m0 + xm;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int ch = tid + i * NT;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (m < m_end) {
+      const int m = m0 + ch / XW;
+      if (ch < XC && m < m_end) {
         const int b = m / HWo, r = m - b * HWo;
         const int oh = r / p.Wo, ow = r - oh * p.Wo;
         const int ih = oh * p.stride - p.pad_t + ky, iw = ow * p.stride - p.pad_l + kx;
         if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
           v = *reinterpret_cast<const uint4*>(
               p.x + (((size_t)b * p.Hin + (ih >> p.up_in)) * p.Win + (iw >> p.up_in)) * p.Cin + xc);
-          if (p.xf.ab || p.xf.relu) {
+          if (has_ab || p.xf.relu) {
             float f[8];
             unpack8(v, f);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = xform1(f[j], p.xf, xc + j);
+            for (int j = 0; j < 8; ++j) {
+              f[j] = fmaf(ca[j], f[j], cb[j]);
+              if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
+            }
             v = pack8(f);
           }
         }
       }
-      rx = v;
+      rx[i] = v;
     }
-    if (has_g) {
-      const int m = m0 + gm;
-      rg = (m < m_end) ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.N + gn) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      const int ch = tid + i * NT;
+      const int m = m0 + ch / GW;
+      rg[i] = (ch < GC && m < m_end) ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.N + gn)
+                                     : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&](int buf) {
-    if (has_x) *reinterpret_cast<uint4*>(&sX[buf][xm][(tid % (BKO / 8)) * 8]) = rx;
-    if (has_g) *reinterpret_cast<uint4*>(&sG[buf][gm][(tid % (BNO / 8)) * 8]) = rg;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int ch = tid + i * NT;
+      if (ch < XC) *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = rx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      const int ch = tid + i * NT;
+      if (ch < GC) *reinterpret_cast<uint4*>(&sG[buf][ch / GW][(ch % GW) * 8]) = rg[i];
+    }
   };
 
   f4v acc[FK][FN];
@@ -114,7 +140,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
 #pragma unroll
     for (int i = 0; i < FK; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
@@ -141,27 +168,32 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
     }
 }
 
-}  // namespace
-
-int conv_wgrad(const WgradParams& p, hipStream_t st) {
-  if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
-  const int bko = (p.K % 64 == 0) ? 64 : 32;
-  const int bno = (p.N % 64 == 0) ? 64 : 32;
-  const int tiles = (p.K / bko) * (p.N / bno);
+template <int BKO, int BNO>
+void launch(const WgradParams& p, hipStream_t st) {
+  const int tiles = (p.K / BKO) * (p.N / BNO);
   int chunk = p.m_chunk;
   if (chunk <= 0) {
-    int splits = (2048 + tiles - 1) / tiles;
-    const int max_splits = (p.M + 255) / 256;
+    int splits = (512 + tiles - 1) / tiles;
+    const int max_splits = (p.M + 511) / 512;   // keep >= 512 pixels (16 reduction steps) per block
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     chunk = (p.M + splits - 1) / splits;
   }
   chunk = (chunk + RM - 1) / RM * RM;
   const int zs = (p.M + chunk - 1) / chunk;
-  dim3 grid(p.K / bko, p.N / bno, zs), blk(NT);
-  if (bko == 64 && bno == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 64>), grid, blk, 0, st, p, chunk);
-  else if (bko == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 32>), grid, blk, 0, st, p, chunk);
-  else if (bno == 64) hipLaunchKernelGGL((conv_wgrad_kernel<32, 64>), grid, blk, 0, st, p, chunk);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<32, 32>), grid, blk, 0, st, p, chunk);
+  dim3 grid(p.K / BKO, p.N / BNO, zs);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BKO, BNO>), grid, dim3(NT), 0, st, p, chunk);
+}
+
+}  // namespace
+
+int conv_wgrad(const WgradParams& p, hipStream_t st) {
+  if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
+  const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
+  if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) launch<128, 128>(p, st);
+  else if (p.K % 64 == 0 && p.N % 64 == 0) launch<64, 64>(p, st);
+  else if (p.K % 64 == 0) launch<64, 32>(p, st);
+  else if (p.N % 64 == 0) launch<32, 64>(p, st);
+  else launch<32, 32>(p, st);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

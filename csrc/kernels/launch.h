@@ -21,8 +21,11 @@ struct ConvParams {
   int B, Hin, Win, Cin, up_in;
   int Ho, Wo, N, ks, stride, pad_t, pad_l;
   int M, K;
+  float* ws;           // split-K fp32 workspace (nullptr: no split)
+  int64_t ws_elems;
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
+int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
 
 // ---------------------------------------------------------------- weight gradient (conv_wgrad.hip)
 struct WgradParams {

@@ -195,7 +195,7 @@ def _engine_and_ref(S=64, B=2, seed=0):
 
 
 def test_engine_gradients_match_fp32_reference():
-    table, eng, flat, x, y = _engine_and_ref()
+    table, eng, flat, x, y = _engine_and_ref(S=128, B=4)
     eng._zero_step()
     eng.forward(True)
     eng.backward()
@@ -203,10 +203,12 @@ def test_engine_gradients_match_fp32_reference():
     g_eng = eng.grad.cpu()
     loss_eng = eng.read_metrics("train")["loss"]
     p = torch.as_tensor(flat).clone().requires_grad_(True)
-    logits, _ = R.unet_forward(p, x, table)
+    # oracle: fp32 reference with bf16 rounding (straight-through) at the engine's storage points - separates
+    # dataflow errors from bf16 storage error (plain fp32 oracle: cos >= 0.91 on the first layers at this size)
+    logits, _ = R.unet_forward(p, x, table, emulate_bf16=True)
     loss = R.bce_with_logits_mean(logits, y)
     g_ref, = torch.autograd.grad(loss, p)
-    assert abs(loss_eng - float(loss)) < 2e-2 * max(1.0, float(loss))
+    assert abs(loss_eng - float(loss.detach())) < 2e-2 * max(1.0, float(loss.detach()))
     bad = []
     for e in table.entries:
         if not e.trainable or e.wname == "bias" and e.layer not in ("conv2d_1", "conv2d_2", "conv2d_3", "conv2d_4",
