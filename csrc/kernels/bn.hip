@@ -1,11 +1,12 @@
 // BatchNormalization (training mode, Keras defaults: axis -1, momentum 0.99, eps 1e-3; client_fit_model.py:101,
-// 110, 114, 130, 134) as three small pieces around the convolutions that carry the heavy traffic:
+// 110, 114, 130, 134) as small pieces around the convolutions that carry the heavy traffic:
 //   bn_finalize      batch (or moving) statistics -> per-channel (a, b, mean, rstd); consumers apply a*y+b on load
 //   bn_moving_update moving_mean / moving_variance (unbiased batch variance, TF fused-BN convention)
 //   node_bwd         gradient of a graph node: sum of up to two incoming gradients, each with its own placement
 //                    (same / stride-2 scatter / 2x2 upsample-sum / max-pool routing) and ReLU mask, the node's own
 //                    ReLU mask, and the BN-backward reductions sum(g), sum(g * xhat) per channel
 //   bn_bwd_apply     dy = a * (g - sum(g)/M - xhat * sum(g*xhat)/M); writes dgamma / dbeta
+// Elementwise kernels walk whole NHWC rows per block (32-bit indices, shifts; see common.h).
 #include "common.h"
 #include "launch.h"
 
@@ -19,9 +20,10 @@ __global__ void bn_finalize_kernel(const float* stats, const float* gamma, const
     float mean, var;
     if (train) {
       float s = 0.f, s2 = 0.f;
+#pragma unroll 8
       for (int r = 0; r < STAT_REPLICAS; ++r) {
-        s += stats[(size_t)r * 2 * C + c];
-        s2 += stats[(size_t)r * 2 * C + C + c];
+        s += stats[r * 2 * C + c];
+        s2 += stats[r * 2 * C + C + c];
       }
       mean = s / count;
       var = fmaxf(s2 / count - mean * mean, 0.f);
@@ -43,8 +45,8 @@ __global__ void bn_moving_kernel(const BnMoving* layers, float momentum) {
   for (int c = threadIdx.x; c < L.C; c += blockDim.x) {
     float s = 0.f, s2 = 0.f;
     for (int r = 0; r < STAT_REPLICAS; ++r) {
-      s += L.stats[(size_t)r * 2 * L.C + c];
-      s2 += L.stats[(size_t)r * 2 * L.C + L.C + c];
+      s += L.stats[r * 2 * L.C + c];
+      s2 += L.stats[r * 2 * L.C + L.C + c];
     }
     const float mean = s / L.count;
     const float var = fmaxf(s2 / L.count - mean * mean, 0.f);
@@ -54,155 +56,146 @@ __global__ void bn_moving_kernel(const BnMoving* layers, float momentum) {
   }
 }
 
-CFL_DEVICE void load8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
-
 __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
-  __shared__ float red[2][NT / 64][256];
-  const int G = p.C >> 3, lanes = NT / G;
-  const int cg = threadIdx.x % G, c0 = cg * 8;
-  const int64_t npix = (int64_t)p.B * p.H * p.W;
+  __shared__ float red[2][4][256];
+  const int G = p.C >> 3, lg = ilog2(G);
+  const int cg = threadIdx.x & (G - 1), c0 = cg * 8;
   const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
+  const int rows = p.B * p.H, items = p.W << lg;
   float a[8], bb[8], mean[8], rstd[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    a[j] = p.ab ? p.ab[c0 + j] : 1.f;
-    bb[j] = p.ab ? p.ab[p.C + c0 + j] : 0.f;
-    mean[j] = p.ab ? p.ab[2 * p.C + c0 + j] : 0.f;
-    rstd[j] = p.ab ? p.ab[3 * p.C + c0 + j] : 0.f;
+  if (p.ab) {
+    load_f8(p.ab + c0, a);
+    load_f8(p.ab + p.C + c0, bb);
+    load_f8(p.ab + 2 * p.C + c0, mean);
+    load_f8(p.ab + 3 * p.C + c0, rstd);
   }
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t pix = (int64_t)blockIdx.x * lanes + threadIdx.x / G; pix < npix; pix += (int64_t)gridDim.x * lanes) {
-    const int w = (int)(pix % p.W), h = (int)((pix / p.W) % p.H);
-    const int64_t b = pix / ((int64_t)p.W * p.H);
-    float y[8], v[8], g[8];
-    load8(p.v + pix * p.C + c0, y);
+  float s[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[j] = p.ab ? fmaf(a[j], y[j], bb[j]) : y[j];
-      g[j] = 0.f;
-    }
+  for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int b = row / p.H, h = row - b * p.H;
+    for (int it = threadIdx.x; it < items; it += NT) {
+      const int w = it >> lg;
+      const int pix = row * p.W + w;
+      float y[8], v[8], g[8];
+      load8(p.v + (size_t)pix * p.C + c0, y);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const GradSrc src = p.src[s];
-      if (src.mode == GM_NONE) continue;
-      float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (src.mode == GM_SAME) {
-        load8(src.p + pix * p.C + c0, t);
-      } else if (src.mode == GM_SCATTER2) {
-        if (((h | w) & 1) == 0) load8(src.p + ((b * Hh + (h >> 1)) * Wh + (w >> 1)) * p.C + c0, t);
-      } else if (src.mode == GM_SUM2X2) {
-        const int W2 = p.W * 2;
+      for (int j = 0; j < 8; ++j) {
+        v[j] = p.ab ? fmaf(a[j], y[j], bb[j]) : y[j];
+        g[j] = 0.f;
+      }
 #pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
+      for (int si = 0; si < 2; ++si) {
+        const GradSrc src = p.src[si];
+        if (src.mode == GM_NONE) continue;
+        float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (src.mode == GM_SAME) {
+          load8(src.p + (size_t)pix * p.C + c0, t);
+        } else if (src.mode == GM_SCATTER2) {
+          if (((h | w) & 1) == 0) load8(src.p + ((size_t)(b * Hh + (h >> 1)) * Wh + (w >> 1)) * p.C + c0, t);
+        } else if (src.mode == GM_SUM2X2) {
+          const int W2 = p.W * 2;
 #pragma unroll
-          for (int dx = 0; dx < 2; ++dx) {
-            float u[8];
-            load8(src.p + ((b * (2 * p.H) + 2 * h + dy) * W2 + 2 * w + dx) * p.C + c0, u);
+          for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) t[j] += u[j];
-          }
-      } else if (src.mode == GM_MAXPOOL) {
-        // pooled outputs whose 3x3/s2 window contains (h, w): oh = h>>1 (ky = h&1) and, for even h >= 2,
-        // oh = h/2 - 1 (ky = 2); same for w
-        const int ohs[2] = {h >> 1, ((h & 1) == 0 && h >= 2) ? (h >> 1) - 1 : -1};
-        const int kys[2] = {h & 1, 2};
-        const int ows[2] = {w >> 1, ((w & 1) == 0 && w >= 2) ? (w >> 1) - 1 : -1};
-        const int kxs[2] = {w & 1, 2};
+            for (int dx = 0; dx < 2; ++dx) {
+              float u[8];
+              load8(src.p + ((size_t)(b * 2 * p.H + 2 * h + dy) * W2 + 2 * w + dx) * p.C + c0, u);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (ohs[i] < 0 || ohs[i] >= Hh) continue;
+              for (int j = 0; j < 8; ++j) t[j] += u[j];
+            }
+        } else if (src.mode == GM_MAXPOOL) {
+          // pooled outputs whose 3x3/s2 window contains (h, w): oh = h>>1 (ky = h&1) and, for even h >= 2,
+          // oh = h/2 - 1 (ky = 2); same for w
+          const int ohs[2] = {h >> 1, ((h & 1) == 0 && h >= 2) ? (h >> 1) - 1 : -1};
+          const int kys[2] = {h & 1, 2};
+          const int ows[2] = {w >> 1, ((w & 1) == 0 && w >= 2) ? (w >> 1) - 1 : -1};
+          const int kxs[2] = {w & 1, 2};
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            if (ows[k] < 0 || ows[k] >= Wh) continue;
-            const int64_t o = ((b * Hh + ohs[i]) * Wh + ows[k]) * p.C + c0;
-            const uint2 am = *reinterpret_cast<const uint2*>(p.argmax + o);
-            const int want = kys[i] * 3 + kxs[k];
-            float u[8];
-            load8(src.p + o, u);
+          for (int i = 0; i < 2; ++i) {
+            if (ohs[i] < 0 || ohs[i] >= Hh) continue;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const uint32_t word = j < 4 ? am.x : am.y;
-              if ((int)((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[j];
+            for (int k = 0; k < 2; ++k) {
+              if (ows[k] < 0 || ows[k] >= Wh) continue;
+              const size_t o = ((size_t)(b * Hh + ohs[i]) * Wh + ows[k]) * p.C + c0;
+              const uint2 am = *reinterpret_cast<const uint2*>(p.argmax + o);
+              const int want = kys[i] * 3 + kxs[k];
+              float u[8];
+              load8(src.p + o, u);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const uint32_t word = j < 4 ? am.x : am.y;
+                if ((int)((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[j];
+              }
             }
           }
         }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] += src.mask ? (v[j] > 0.f ? t[j] : 0.f) : t[j];
       }
+      if (p.relu_node) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] += src.mask ? (v[j] > 0.f ? t[j] : 0.f) : t[j];
-    }
-    if (p.relu_node) {
+        for (int j = 0; j < 8; ++j) g[j] = v[j] > 0.f ? g[j] : 0.f;
+      }
+      const uint4 gv = pack8(g);
+      *reinterpret_cast<uint4*>(p.out + (size_t)pix * p.C + c0) = gv;
+      if (p.sums) {
+        float gr[8];
+        unpack8(gv, gr);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = v[j] > 0.f ? g[j] : 0.f;
-    }
-    const uint4 gv = pack8(g);
-    *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
-    if (p.sums) {
-      float gr[8];
-      unpack8(gv, gr);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s1[j] += gr[j];
-        if (p.ab) s2[j] += gr[j] * (y[j] - mean[j]) * rstd[j];
+        for (int j = 0; j < 8; ++j) {
+          s[0][j] += gr[j];
+          if (p.ab) s[1][j] += gr[j] * (y[j] - mean[j]) * rstd[j];
+        }
       }
     }
   }
   if (!p.sums) return;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (p.ab) block_channel_atomics<2>(s, G, p.C, p.sums, red);
+  else {
+    float s1[1][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    for (int o = G; o < 64; o <<= 1) {
-      s1[j] += __shfl_xor(s1[j], o, 64);
-      s2[j] += __shfl_xor(s2[j], o, 64);
-    }
-  }
-  if (lane < G) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[0][wid][c0 + j] = s1[j];
-      red[1][wid][c0 + j] = s2[j];
-    }
-  }
-  __syncthreads();
-  const int nst = p.ab ? 2 : 1;
-  for (int e = threadIdx.x; e < nst * p.C; e += NT) {
-    const int st = e / p.C, c = e - st * p.C;
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w) v += red[st][w][c];
-    atomicAdd(&p.sums[st * p.C + c], v);
+    for (int j = 0; j < 8; ++j) s1[0][j] = s[0][j];
+    block_channel_atomics<1>(s1, G, p.C, p.sums, red);
   }
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
-  const int G = p.C >> 3;
+  const int G = p.C >> 3, lg = ilog2(G);
   const float invM = 1.f / (float)p.M;
-  const int64_t total = (int64_t)p.M * G;
+  const int total = p.M << lg;
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < p.C; c += NT) {
       if (p.dbeta) p.dbeta[c] = p.sums[c];
       if (p.dgamma) p.dgamma[c] = p.sums[p.C + c];
     }
   }
-  for (int64_t t = (int64_t)blockIdx.x * NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
-    const int c0 = (int)(t % G) * 8;
-    const int64_t m = t / G;
+  // grid stride is a multiple of G, so a thread's channel group never changes
+  const int c0 = (threadIdx.x & (G - 1)) * 8;
+  float a[8], mean[8], rstd[8], k1[8], k2[8];
+  load_f8(p.ab + c0, a);
+  load_f8(p.ab + 2 * p.C + c0, mean);
+  load_f8(p.ab + 3 * p.C + c0, rstd);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = p.sums[c0 + j] * invM;
+    k2[j] = p.sums[p.C + c0 + j] * invM;
+  }
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
+    const int m = t >> lg;
     float g[8], y[8], o[8];
-    load8(p.g + m * p.C + c0, g);
-    load8(p.y + m * p.C + c0, y);
+    load8(p.g + (size_t)m * p.C + c0, g);
+    load8(p.y + (size_t)m * p.C + c0, y);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float xhat = (y[j] - p.ab[2 * p.C + c]) * p.ab[3 * p.C + c];
-      o[j] = p.ab[c] * (g[j] - p.sums[c] * invM - xhat * p.sums[p.C + c] * invM);
+      const float xhat = (y[j] - mean[j]) * rstd[j];
+      o[j] = a[j] * (g[j] - k1[j] - xhat * k2[j]);
     }
-    *reinterpret_cast<uint4*>(p.dy + m * p.C + c0) = pack8(o);
+    *reinterpret_cast<uint4*>(p.dy + (size_t)m * p.C + c0) = pack8(o);
   }
 }
 
-int grid_cap(int64_t work, int cap) {
-  int64_t g = (work + NT - 1) / NT;
-  return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
-}
+bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
 }  // namespace
 
@@ -220,17 +213,18 @@ int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float mo
 }
 
 int node_bwd(const NodeBwdParams& p, hipStream_t st) {
-  if (p.C % 8 || p.C > 256 || (NT % (p.C / 8)) != 0) return 1;
-  const int lanes = NT / (p.C / 8);
-  const int64_t npix = (int64_t)p.B * p.H * p.W;
-  int64_t blocks = (npix + lanes - 1) / lanes;
-  if (blocks > 2048) blocks = 2048;   // bounded grid: one set of channel atomics per block
-  hipLaunchKernelGGL(node_bwd_kernel, dim3((int)blocks), dim3(NT), 0, st, p);
+  if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
+  int blocks = p.B * p.H;
+  if (blocks > 1024) blocks = 1024;   // bounded grid: one set of channel atomics per block
+  hipLaunchKernelGGL(node_bwd_kernel, dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
-  if (p.C % 8) return 1;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_cap((int64_t)p.M * (p.C / 8), 4096)), dim3(NT), 0, st, p);
+  if (p.C % 8 || !pow2(p.C / 8)) return 1;
+  int blocks = (int)(((int64_t)p.M * (p.C / 8) + NT - 1) / NT);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

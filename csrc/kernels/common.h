@@ -4,6 +4,9 @@
 //   * activations are NHWC bf16 stored as uint16_t (RNE rounding, NaN preserved);
 //   * accumulation, BN statistics, gradients of weights and the optimizer are fp32;
 //   * wave = 64 lanes; block sizes are multiples of 64;
+//   * no 64-bit integer division in any hot loop (it lowers to a ~100-instruction sequence on CDNA): NHWC
+//     elementwise kernels walk whole rows (b*H + h) per block and split a row into (pixel, 8-channel group)
+//     items with shifts - the channel-group count C/8 is a power of two for every layer of the network;
 //   * launchers take a hipStream_t and never allocate / synchronise (graph-capture safe).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -44,6 +47,14 @@ CFL_DEVICE uint4 pack8(const float* f) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+CFL_DEVICE void load8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+
+CFL_DEVICE void load_f8(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 CFL_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -74,6 +85,38 @@ CFL_DEVICE float block_sum(float v, float* red /* >= NT/64 floats of LDS */) {
 
 CFL_DEVICE int imin(int a, int b) { return a < b ? a : b; }
 CFL_DEVICE int imax(int a, int b) { return a > b ? a : b; }
+
+// log2 of a power of two (host or device)
+__host__ __device__ inline int ilog2(int x) {
+  int l = 0;
+  while ((1 << l) < x) ++l;
+  return l;
+}
+
+// Per-channel sums of 8-channel vectors held by a 256-thread block where thread t owns channel group t % G:
+// reduce the wave's lanes that share the group (stride G), then the 4 waves through LDS, then one atomic per
+// channel into dst[0..C) and (if NS == 2) dst[C..2C).
+template <int NS>
+CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* dst, float (*red)[4][256]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c0 = (threadIdx.x % G) * 8;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      for (int o = G; o < 64; o <<= 1) s[k][j] += __shfl_xor(s[k][j], o, 64);
+  if (lane < G) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[k][wid][c0 + j] = s[k][j];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NS * C; e += 256) {
+    const int k = e / C, c = e - k * C;
+    const float v = red[k][0][c] + red[k][1][c] + red[k][2][c] + red[k][3][c];
+    atomicAdd(&dst[k * C + c], v);
+  }
+}
 
 // BN per-channel coefficients produced by bn_finalize (csrc/kernels/bn.hip): 4 rows of C floats
 //   ab[0*C + c] = scale a = gamma * rstd     ab[1*C + c] = shift b = beta - mean * a

@@ -59,6 +59,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
   constexpr int GW = BNO / 8;
   const int gn = nBlock + (tid % GW) * 8;
 
+  // pixel decode (b, oh, ow) of each x chunk row, advanced incrementally by RM per step (no division in the loop)
+  int db[XPT], doh[XPT], dow[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int m = m_begin + (tid + i * NT) / XW;
+    db[i] = m / HWo;
+    const int r = m - db[i] * HWo;
+    doh[i] = r / p.Wo;
+    dow[i] = r - doh[i] * p.Wo;
+  }
   uint4 rx[XPT], rg[GPT];
   auto load = [&](int m0) {
 #pragma unroll
@@ -67,8 +77,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
       uint4 v = make_uint4(0, 0, 0, 0);
       const int m = m0 + ch / XW;
       if (ch < XC && m < m_end) {
-        const int b = m / HWo, r = m - b * HWo;
-        const int oh = r / p.Wo, ow = r - oh * p.Wo;
+        const int b = db[i], oh = doh[i], ow = dow[i];
         const int ih = oh * p.stride - p.pad_t + ky, iw = ow * p.stride - p.pad_l + kx;
         if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
           v = *reinterpret_cast<const uint4*>(
@@ -86,6 +95,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
         }
       }
       rx[i] = v;
+      dow[i] += RM;                       // advance this chunk row to the next step's pixel
+      while (dow[i] >= p.Wo) {
+        dow[i] -= p.Wo;
+        if (++doh[i] == p.Ho) {
+          doh[i] = 0;
+          ++db[i];
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {

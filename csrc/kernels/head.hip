@@ -20,12 +20,12 @@ constexpr float DICE_SMOOTH = 1.0f;
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
   __shared__ double red[5][NT / 64];
-  const int64_t npix = (int64_t)p.B * p.R * p.R;
+  const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
   double bce = 0, cor = 0, I = 0, P = 0, T = 0;
-  for (int64_t pix = (int64_t)blockIdx.x * NT + threadIdx.x; pix < npix; pix += (int64_t)gridDim.x * NT) {
-    const int j = (int)(pix % p.R), i = (int)((pix / p.R) % p.R);
-    const int b = (int)(pix / ((int64_t)p.R * p.R));
+  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
+    const int j = pix % p.R, i = (pix / p.R) % p.R;
+    const int b = pix / (p.R * p.R);
     float h = p.bias[0];
 #pragma unroll
     for (int c0 = 0; c0 < CIN; c0 += 8) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
   __shared__ float red[CIN + 1][NT / 64];
-  const int64_t npix = (int64_t)p.B * p.R * p.R;
+  const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
   const float inv_n = 1.f / (float)(npix * 4);
   float dI = 0.f, dP = 0.f, den = 1.f;
@@ -86,9 +86,9 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 #pragma unroll
   for (int c = 0; c < CIN; ++c) gw[c] = 0.f;
   float gb = 0.f;
-  for (int64_t pix = (int64_t)blockIdx.x * NT + threadIdx.x; pix < npix; pix += (int64_t)gridDim.x * NT) {
-    const int j = (int)(pix % p.R), i = (int)((pix / p.R) % p.R);
-    const int b = (int)(pix / ((int64_t)p.R * p.R));
+  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
+    const int j = pix % p.R, i = (pix / p.R) % p.R;
+    const int b = pix / (p.R * p.R);
     const float h = p.h[pix];
     const float sg = 1.f / (1.f + expf(-h));
     const uint8_t* mrow = p.masks + (int64_t)p.idx[b] * S * S;

@@ -260,3 +260,41 @@ def test_engine_graph_replay_matches_eager_and_learns():
         if i % 10 == 9:
             losses.append(eng.read_metrics("train")["loss"])
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("N", [32, 64])
+def test_conv_igemm_big_m_tiles(N):
+    """BM=256 tiles (M >= 131072) used by the 128^2 layers at 256^2 input."""
+    torch.manual_seed(8)
+    B, H, Cin = 8, 128, 32
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    w = torch.randn(1, 1, Cin, N) * 0.1
+    wb = pack(PK_PW, w, 1, Cin, N)
+    y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+    stats = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
+    hip().conv_igemm(xb, wb, None, y, stats, None, 0, B, H, H, Cin, 0, H, H, N, 1, 1, 0, 0)
+    ref = xf @ w.view(Cin, N).to(torch.bfloat16).float()
+    out = from_bits(y)
+    assert rel(out, ref) < 1e-2
+    st = stats.view(-1, 2, N).sum(0).cpu()
+    assert torch.allclose(st[0], out.sum((0, 1, 2)), rtol=1e-3, atol=0.5)
+
+
+def test_conv_igemm_split_k_with_stats():
+    """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue."""
+    torch.manual_seed(9)
+    B, H, Cin, N = 4, 8, 256, 256
+    assert hip().conv_splits(B * H * H, N, 9 * Cin, Cin) > 1
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    wk = torch.randn(3, 3, N, Cin) * 0.02
+    wb = pack(PK_CONVT, wk, 3, Cin, N)
+    bias = torch.randn(N) * 0.1
+    y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+    stats = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
+    ws = torch.zeros(16 * B * H * H * N, device=DEV)
+    hip().conv_igemm(xb, wb, bias.to(DEV), y, stats, None, 1, B, H, H, Cin, 0, H, H, N, 3, 1, 1, 1, ws)
+    ref = R.convt_same(xf.permute(0, 3, 1, 2).relu(), wk.to(torch.bfloat16).float(), bias).permute(0, 2, 3, 1)
+    out = from_bits(y)
+    assert rel(out, ref) < 1e-2
+    st = stats.view(-1, 2, N).sum(0).cpu()
+    assert torch.allclose(st[1], (out * out).sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
