@@ -234,7 +234,7 @@ class UNetEngine:
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture)."""
-        need = self.C.conv_splits(B * Ho * Wo, N, ks * ks * Cin, Cin)
+        need = self.C.conv_splits(B, Ho, Wo, N, ks, stride, pad_t, Cin)
         if need > 1 and need * B * Ho * Wo * N > self.ws.numel():
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")

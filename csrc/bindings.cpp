@@ -41,8 +41,9 @@ InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(a
 
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
-                   int pad_l, OptT ws) {
+                   int pad_l, OptT ws, int algo) {
   ConvParams p{};
+  p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
   p.wt = ptr<const bf16_t>(wt, "wt");
   p.bias = optr<const float>(bias, "bias");
@@ -62,9 +63,11 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
-int conv_splits_op(int M, int N, int K, int Cin) {
+int conv_splits_op(int B, int Ho, int Wo, int N, int ks, int stride, int pad, int Cin) {
   ConvParams p{};
-  p.M = M; p.N = N; p.K = K; p.Cin = Cin;
+  p.B = B; p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad; p.pad_l = pad; p.Cin = Cin;
+  p.M = B * Ho * Wo;
+  p.K = ks * ks * Cin;
   return conv_igemm_splits(p);
 }
 
@@ -344,7 +347,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_igemm", &conv_igemm_op, py::arg("x"), py::arg("wt"), py::arg("bias"), py::arg("y"), py::arg("stats"),
         py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"),
         py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"),
-        py::arg("pad_l"), py::arg("ws") = py::none());
+        py::arg("pad_l"), py::arg("ws") = py::none(), py::arg("algo") = 0);
   m.def("conv_splits", &conv_splits_op);
   m.def("conv_wgrad", &conv_wgrad_op);
   m.def("dw_fwd", &dw_fwd_op);

@@ -1,0 +1,306 @@
+// 3x3 / stride 1 / "same" convolution with a spatial M-tile and an LDS halo (gfx950 MFMA 16x16x32 bf16).
+//
+// Serves every Conv2DTranspose of the decoder - forward (/root/reference/client_fit_model.py:129,133) and
+// data-gradient - i.e. 66 % of the network's FLOPs. The generic implicit GEMM (conv_igemm.hip) re-loads and
+// re-transforms each input element once per tap (9x). Here a block owns a TH x TW pixel tile of one image and
+// BN output channels; for every 32-channel input chunk it loads the (TH+2) x (TW+2) halo tile ONCE into LDS -
+// applying the producer's BN-apply + ReLU and the nearest-2x upsample fold (decoder inputs are stored at half
+// resolution) on the way in - and all 9 taps read their MFMA A fragments as shifted views of that tile:
+//   A fragment of tap (ky,kx), pixel p = (py,px): halo[py+ky][px+kx][8*(lane>>4) .. +7]   (one ds_read_b128)
+// The packed weights [N][K] (K = tap*Cin + c) stream through a register-staged double buffer per (chunk, tap)
+// K-step; the next chunk's halo is prefetched into registers during the current chunk's taps and written to the
+// second halo buffer before the chunk boundary, so each K-step costs one barrier.
+// Halo pixel stride is 40 bf16 (80 B): the 16 rows of a fragment read hit 16 distinct bank slots.
+// Epilogue (bias, bf16, LDS-staged 16-byte stores, BN statistics) and split-K over input chunks (fp32 workspace
+// + splitk epilogue) are shared with conv_igemm.
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int BK = 32;          // channels per chunk (one K-step = one tap of one chunk)
+constexpr int LDH = BK + 8;     // halo pixel stride (bf16)
+constexpr int LDB = BK + 8;
+
+template <int TH, int TW, int BN_, int WM, int WN>
+__global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
+  constexpr int BM = TH * TW;
+  constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
+  constexpr int TM = BM / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int HALO_CHUNKS = HP * (BK / 8);                      // 16-byte pieces per halo tile
+  constexpr int H_PER_T = (HALO_CHUNKS + NT - 1) / NT;
+  constexpr int B_CHUNKS = BN_ * BK / 8, B_PER_T = (B_CHUNKS + NT - 1) / NT;
+  constexpr int SH = 2 * HP * LDH, SB = 2 * BN_ * LDB;
+  constexpr int LDC = BN_ + 8;
+  static_assert(BM * LDC <= SH + SB, "C staging tile must fit");
+  static_assert(WM * WN == 4 && TM % 16 == 0 && TN % 16 == 0, "wave tiling");
+
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SH + SB];
+  __shared__ float sred[2][4][BN_];
+  bf16_t* sH = smem;              // [2][HP][LDH]
+  bf16_t* sB = smem + SH;         // [2][BN_][LDB]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_w = (p.Wo + TW - 1) / TW, tiles_h = (p.Ho + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int b = t / (tiles_w * tiles_h);
+  t -= b * tiles_w * tiles_h;
+  const int ty0 = (t / tiles_w) * TH, tx0 = (t % tiles_w) * TW;
+  const int nBlock = blockIdx.y * BN_;
+  const int chunks = p.Cin / BK;
+  const int ch0 = blockIdx.z * chunks_per_split;
+  const int ch1 = imin(chunks, ch0 + chunks_per_split);
+  const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
+  const bool has_ab = p.xf.ab != nullptr;
+  const int relu = p.xf.relu;
+
+  // ---- halo loading: piece e -> halo pixel e/4, channel quarter e%4 ----
+  uint4 rh[H_PER_T];
+  auto load_halo = [&](int chunk) {
+    const int cbase = chunk * BK;
+    // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
+    float a8[8], b8[8];
+    if (has_ab) {
+      load_f8(p.xf.ab + cbase + (tid & 3) * 8, a8);
+      load_f8(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, b8);
+    }
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      const int e = tid + i * NT;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < HALO_CHUNKS) {
+        const int hp = e >> 2, q = e & 3;
+        const int hy = hp / HW, hx = hp - hy * HW;
+        const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;      // logical input coords (pad 1)
+        if (iy >= 0 && iy < Hl && ix >= 0 && ix < Wl) {
+          const int c = cbase + q * 8;
+          v = *reinterpret_cast<const uint4*>(
+              p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + c);
+          if (has_ab || relu) {
+            float f[8];
+            unpack8(v, f);
+            if (has_ab) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = fmaf(a8[j], f[j], b8[j]);
+            }
+            if (relu) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+            }
+            v = pack8(f);
+          }
+        }
+      }
+      rh[i] = v;
+    }
+  };
+  auto store_halo = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (e < HALO_CHUNKS) *reinterpret_cast<uint4*>(sH + ((size_t)buf * HP + (e >> 2)) * LDH + (e & 3) * 8) = rh[i];
+    }
+  };
+  // ---- weight tile of K-step (chunk, tap): wt[n][tap*Cin + chunk*32 .. +32) ----
+  uint4 rb[B_PER_T];
+  auto load_b = [&](int chunk, int tap) {
+    const size_t kofs = (size_t)tap * p.Cin + chunk * BK;
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (e < B_CHUNKS) rb[i] = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (e >> 2)) * p.K + kofs + (e & 3) * 8);
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (e < B_CHUNKS) *reinterpret_cast<uint4*>(sB + ((size_t)buf * BN_ + (e >> 2)) * LDB + (e & 3) * 8) = rb[i];
+    }
+  };
+
+  // per-lane fragment pixel coordinates within the tile
+  int fpy[FM], fpx[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int pp = wm * TM + i * 16 + (lane & 15);
+    fpy[i] = pp / TW;
+    fpx[i] = pp % TW;
+  }
+  const int fk = (lane >> 4) * 8;
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  if (ch0 < ch1) {
+    load_halo(ch0);
+    store_halo(0);
+    load_b(ch0, 0);
+    store_b(0);
+  }
+  __syncthreads();
+  int bbuf = 0;
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int hbuf = (ch - ch0) & 1;
+    const bool next_chunk = ch + 1 < ch1;
+    if (next_chunk) load_halo(ch + 1);                       // in flight during this chunk's 9 taps
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const bool more = tap < 8 || next_chunk;
+      if (more) {
+        if (tap < 8) load_b(ch, tap + 1);
+        else load_b(ch + 1, 0);
+      }
+      const int ky = tap / 3, kx = tap - ky * 3;
+      s8v af[FM], bfg[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const s8v*>(sH + ((size_t)hbuf * HP + (fpy[i] + ky) * HW + fpx[i] + kx) * LDH + fk);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfg[j] = *reinterpret_cast<const s8v*>(sB + ((size_t)bbuf * BN_ + wn * TN + j * 16 + (lane & 15)) * LDB + fk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      if (more) store_b(bbuf ^ 1);
+      if (tap == 8 && next_chunk) store_halo(hbuf ^ 1);
+      __syncthreads();
+      bbuf ^= 1;
+    }
+  }
+
+  // pixel index of accumulator row r of fragment i -> (m valid?, global m)
+  auto out_m = [&](int row, int& m) -> bool {
+    const int py = row / TW, px = row % TW;
+    const int oy = ty0 + py, ox = tx0 + px;
+    m = (b * p.Ho + oy) * p.Wo + ox;
+    return oy < p.Ho && ox < p.Wo;
+  };
+
+  if (ws != nullptr) {                    // split-K partials
+    float* dst = ws + (size_t)blockIdx.z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nBlock + wn * TN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m;
+          if (out_m(wm * TM + i * 16 + (lane >> 4) * 4 + r, m)) dst[(size_t)m * p.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+
+  bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int cl = wn * TN + j * 16 + (lane & 15);
+    const float bias = p.bias ? p.bias[nBlock + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sC[wm * TM + i * 16 + (lane >> 4) * 4 + r][cl] = f2bf(acc[i][j][r] + bias);
+  }
+  __syncthreads();
+  constexpr int CG = BN_ / 8, ROWS_PER_PASS = NT / CG;
+  const int cg = tid % CG;
+  float s[2][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[0][q] = s[1][q] = 0.f;
+#pragma unroll
+  for (int r0 = 0; r0 < BM; r0 += ROWS_PER_PASS) {
+    const int row = r0 + tid / CG;
+    int m;
+    if (out_m(row, m)) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + nBlock + cg * 8) = v;
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        s[0][q] += f[q];
+        s[1][q] += f[q] * f[q];
+      }
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      for (int o = CG; o < 64; o <<= 1) {
+        s[0][q] += __shfl_xor(s[0][q], o, 64);
+        s[1][q] += __shfl_xor(s[1][q], o, 64);
+      }
+    if (lane < CG) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        sred[0][wid][cg * 8 + q] = s[0][q];
+        sred[1][wid][cg * 8 + q] = s[1][q];
+      }
+    }
+    __syncthreads();
+    float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+    for (int e = tid; e < 2 * BN_; e += NT) {
+      const int st = e / BN_, cc = e - st * BN_;
+      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+    }
+  }
+}
+
+template <int TH, int TW, int BN_, int WM, int WN>
+int launch(const ConvParams& p, int splits, hipStream_t st) {
+  const int chunks = p.Cin / BK;
+  const int per = (chunks + splits - 1) / splits;
+  splits = (chunks + per - 1) / per;
+  const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
+  dim3 grid(tiles, p.N / BN_, splits);
+  hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? p.ws : nullptr);
+  return splits;
+}
+
+}  // namespace
+
+int conv3x3_splits(const ConvParams& p) {
+  const int tw = p.Wo >= 16 ? 16 : 8;
+  const int th = 128 / tw;
+  const int bn = p.N >= 128 ? 128 : p.N;
+  const int blocks = ((p.Ho + th - 1) / th) * ((p.Wo + tw - 1) / tw) * p.B * (p.N / bn);
+  const int chunks = p.Cin / BK;
+  if (blocks >= 192 || chunks < 2) return 1;
+  int s = (384 + blocks - 1) / blocks;
+  if (s > chunks) s = chunks;
+  const int per = (chunks + s - 1) / s;
+  return (chunks + per - 1) / per;
+}
+
+bool conv3x3_supported(const ConvParams& p) {
+  return p.ks == 3 && p.stride == 1 && p.pad_t == 1 && p.pad_l == 1 && p.Cin % BK == 0 && p.N % 32 == 0 &&
+         p.Wo >= 8 && p.Ho >= 8 && (p.N % 128 == 0 || p.N == 64 || p.N == 32);
+}
+
+int conv3x3(const ConvParams& p, hipStream_t st) {
+  if (!conv3x3_supported(p)) return 1;
+  int splits = conv3x3_splits(p);
+  if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
+  const bool w16 = p.Wo >= 16;
+  if (p.N % 128 == 0) {
+    if (w16) splits = launch<8, 16, 128, 2, 2>(p, splits, st);
+    else splits = launch<16, 8, 128, 2, 2>(p, splits, st);
+  } else if (p.N == 64) {
+    if (w16) splits = launch<8, 16, 64, 2, 2>(p, splits, st);
+    else splits = launch<16, 8, 64, 2, 2>(p, splits, st);
+  } else {
+    if (w16) splits = launch<8, 16, 32, 4, 1>(p, splits, st);
+    else splits = launch<16, 8, 32, 4, 1>(p, splits, st);
+  }
+  if (hipGetLastError() != hipSuccess) return 3;
+  return splits > 1 ? -splits : 0;   // negative: caller must run the split-K epilogue
+}

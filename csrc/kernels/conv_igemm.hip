@@ -318,7 +318,14 @@ void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
 
 }  // namespace
 
+bool conv3x3_supported(const ConvParams& p);
+int conv3x3_splits(const ConvParams& p);
+int conv3x3(const ConvParams& p, hipStream_t st);
+
+static bool use3x3(const ConvParams& p) { return p.algo != 1 && conv3x3_supported(p); }
+
 int conv_igemm_splits(const ConvParams& p) {
+  if (use3x3(p)) return conv3x3_splits(p);
   const int KT = p.K / BK;
   const int bm = (p.N <= 64 && p.M >= 256 * 512) ? 256 : 128;
   const int bn = p.N >= 128 ? 128 : p.N;
@@ -332,6 +339,18 @@ int conv_igemm_splits(const ConvParams& p) {
 
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
+  if (use3x3(p)) {                       // halo-tile kernel for every 3x3 / stride-1 conv (conv3x3.hip)
+    const int rc = conv3x3(p, st);
+    if (rc > 0) return rc;
+    if (rc < 0) {
+      const int G = p.N / 8, lanes = NT / G;
+      int blocks = (p.M + lanes - 1) / lanes;
+      if (blocks > 1024) blocks = 1024;
+      hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(NT), 0, st, p, p.ws, -rc);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
+  if (p.algo == 2) return 4;
   int splits = conv_igemm_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const bool big_m = p.M >= 256 * 512;

@@ -23,6 +23,7 @@ struct ConvParams {
   int M, K;
   float* ws;           // split-K fp32 workspace (nullptr: no split)
   int64_t ws_elems;
+  int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)

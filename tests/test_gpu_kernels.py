@@ -252,7 +252,10 @@ def test_engine_graph_replay_matches_eager_and_learns():
     eng.train_step(use_graph=True)
     torch.cuda.synchronize()
     after_graph = eng.get_flat()
-    assert np.allclose(after_eager, after_graph, atol=1e-5)
+    # float-atomic reductions (BN stats, wgrad split-M) are order-nondeterministic: the first Adam step moves each
+    # weight by ~lr * sign(g), so near-zero gradients may flip sign -> per-element differences up to ~2 lr
+    d = np.abs(after_eager - after_graph)
+    assert d.max() < 2.5e-3 and (d > 1e-4).mean() < 0.01
     eng.read_metrics("train")
     losses = []
     for i in range(40):
@@ -284,7 +287,7 @@ def test_conv_igemm_split_k_with_stats():
     """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue."""
     torch.manual_seed(9)
     B, H, Cin, N = 4, 8, 256, 256
-    assert hip().conv_splits(B * H * H, N, 9 * Cin, Cin) > 1
+    assert hip().conv_splits(B, H, H, N, 3, 1, 1, Cin) > 1
     xb, xf = bf(torch.randn(B, H, H, Cin))
     wk = torch.randn(3, 3, N, Cin) * 0.02
     wb = pack(PK_CONVT, wk, 3, Cin, N)
@@ -298,3 +301,36 @@ def test_conv_igemm_split_k_with_stats():
     assert rel(out, ref) < 1e-2
     st = stats.view(-1, 2, N).sum(0).cpu()
     assert torch.allclose(st[1], (out * out).sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [
+    (2, 16, 64, 32, 0, True),     # 128^2-level decoder conv (BN 32, TW 16)
+    (2, 8, 32, 64, 1, False),     # upsampled input, 16x16 output
+    (4, 8, 256, 256, 0, True),    # deep layer: split-K over input chunks, TW 8
+    (2, 12, 128, 128, 0, True),   # ragged tiles (12 not a multiple of 8/16)
+])
+def test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab):
+    torch.manual_seed(11)
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    wk = torch.randn(3, 3, N, Cin) * 0.03
+    wb = pack(PK_CONVT, wk, 3, Cin, N)
+    ab, a, b = ab_for(Cin, 12)
+    Ho = Hs * (2 if up else 1)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    outs = []
+    for algo in (1, 2):
+        y = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
+        stats = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
+        ws = torch.zeros(16 * B * Ho * Ho * N, device=DEV)
+        hip().conv_igemm(xb, wb, bias, y, stats, ab.to(DEV) if use_ab else None, 1, B, Hs, Hs, Cin, up, Ho, Ho, N,
+                         3, 1, 1, 1, ws, algo)
+        outs.append((from_bits(y), stats.view(-1, 2, N).sum(0).cpu()))
+    (yg, sg), (yt, st) = outs
+    assert rel(yt, yg) < 5e-3
+    assert torch.allclose(st, sg, rtol=2e-3, atol=5e-2)
+    t = xf * a + b if use_ab else xf
+    xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    ref = R.convt_same(xin, wk.to(torch.bfloat16).float(), bias.cpu()).permute(0, 2, 3, 1)
+    assert rel(yt, ref) < 1e-2
