@@ -124,7 +124,8 @@ def save_weight_file(path: str, arrays: Sequence[np.ndarray]) -> None:
     d = os.path.dirname(path)
     if d:
         os.makedirs(d, exist_ok=True)   # reference never creates it
-    tmp = path + ".tmp"
+    import threading
+    tmp = f"{path}.{os.getpid()}.{threading.get_ident()}.tmp"   # unique per writer (processes and threads)
     with open(tmp, "wb") as f:
         f.write(encode_pickle(arrays))
     os.replace(tmp, path)

@@ -36,8 +36,11 @@ def main(argv: Optional[List[str]] = None) -> int:
     procs = []
     for r in range(n):
         e = dict(env, LOCAL_RANK=str(r), FL_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "fl_client.py"), *argv,
-                                       "--port", str(port), "--host", "127.0.0.1"], env=e))
+        extra = ["--port", str(port), "--host", "127.0.0.1"]
+        if cfg.client_weight_file and n > 1:     # one trainer->driver hand-off file per client process
+            root, ext = os.path.splitext(cfg.client_weight_file)
+            extra += ["--client-weight-file", f"{root}.rank{r}{ext}"]
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "fl_client.py"), *argv, *extra], env=e))
     rc = 0
     try:
         while any(p.poll() is None for p in procs):

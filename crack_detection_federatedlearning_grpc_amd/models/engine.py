@@ -130,15 +130,17 @@ class UNetEngine:
         bn_layers = [ly for ly in self.table.weighted_layers() if ly.kind == "bn"]
         self.bn_names = [ly.name for ly in bn_layers]
         tot_c = sum(ly.cout for ly in bn_layers)
+        RS = self.RS = self.C.SUM_REPLICAS
         self.stats_all = torch.zeros(R * 2 * tot_c, dtype=torch.float32, device=self.dev)
-        self.sums_all = torch.zeros(2 * tot_c, dtype=torch.float32, device=self.dev)
+        self.sums_all = torch.zeros(RS * 2 * tot_c, dtype=torch.float32, device=self.dev)
         self.ab_all = torch.zeros(4 * tot_c, dtype=torch.float32, device=self.dev)
         self.bn: Dict[str, Dict[str, torch.Tensor]] = {}
         so = 0
         for ly in bn_layers:
             c = ly.cout
             self.bn[ly.name] = dict(C=c, stats=self.stats_all[R * 2 * so:R * 2 * (so + c)],
-                                    sums=self.sums_all[2 * so:2 * (so + c)], ab=self.ab_all[4 * so:4 * (so + c)])
+                                    sums=self.sums_all[RS * 2 * so:RS * 2 * (so + c)],
+                                    ab=self.ab_all[4 * so:4 * (so + c)])
             so += c
         # forward activations (raw bf16) -------------------------------------------------------------
         A = self.act = {}
@@ -190,10 +192,72 @@ class UNetEngine:
             cin = F
         D["g0"] = t(B, r[0], r[0], ENTRY_FILTERS)
         D["dy0"] = t(B, r[0], r[0], ENTRY_FILTERS)
+        # replica rows for the small weight gradients every block adds into (depthwise kernels, entry conv):
+        # [R][n] slabs summed into the flat gradient by ONE grad_finish launch at the end of backward, which
+        # also applies the gradient copies (residual-conv bias grad == its BN's beta grad)
+        names = self.names
+        slabs = [(names[0], "kernel", 27 * ENTRY_FILTERS)]
+        cin = ENTRY_FILTERS
+        for k, F in enumerate(ENC_FILTERS):
+            s1, s2 = names[2 + 5 * k], names[2 + 5 * k + 2]
+            slabs += [(s1, "depthwise_kernel", 9 * cin), (s2, "depthwise_kernel", 9 * F)]
+            cin = F
+        tot = sum((n + 63) // 64 * 64 for _, _, n in slabs)
+        self.gws = torch.zeros(R * tot, dtype=torch.float32, device=self.dev)
+        self.gslab: Dict[Tuple[str, str], torch.Tensor] = {}
+        entries, off = [], 0
+        for ly, w, n in slabs:
+            sl = self.gws[off:off + R * n]
+            self.gslab[(ly, w)] = sl
+            entries.append((sl, self.G(ly, w), n, R, self.C.GF_REDUCE))
+            off += R * ((n + 63) // 64 * 64)
+        for k in range(len(ENC_FILTERS)):
+            entries.append((self.G(names[2 + 5 * k + 3], "beta"), self.G(names[2 + 5 * k + 4], "bias"),
+                            ENC_FILTERS[k], 1, self.C.GF_COPY))
+        for k in range(len(DEC_FILTERS)):
+            base = 17 + 5 * k
+            entries.append((self.G(names[base + 3], "beta"), self.G(names[base + 4], "bias"), DEC_FILTERS[k], 1,
+                            self.C.GF_COPY))
+        self._finish_static = entries
+        self._finish_dyn: List[tuple] = []
+        self._wslabs: Dict[str, torch.Tensor] = {}
+        self._build_finish()
+        # per-step zeroing of gradients / statistics in one launch
+        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:8]]
+        self.zero_table = self.C.make_zero_table(spans)
+        self.n_zero, self.max_zero = len(spans), max(t.numel() * t.element_size() for t in spans)
         # BN moving-stat table
         self.moving_table = self.C.make_bn_moving_table([
             (self.bn[n]["stats"], self.P(n, "moving_mean"), self.P(n, "moving_variance"), self.bn[n]["C"],
              float(self.bn_count(n))) for n in self.bn_names])
+
+    def _build_finish(self) -> None:
+        entries = self._finish_static + self._finish_dyn
+        self.finish_table, self.finish_work = self.C.make_grad_finish_table(entries)
+        self.n_finish = len(entries)
+        self._finish_dirty = False
+
+    def _wgrad(self, x, dy, layer, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l,
+               dst_mode) -> None:
+        """Weight gradient into a slab of partial rows (plain-stored pixel splits for the 3x3 halo kernel, atomic
+        replica rows otherwise) that grad_finish sums into the flat gradient at the end of backward. ``layer`` is
+        a layer name (weight "kernel") or a (layer, weight) pair. Slabs are allocated on the eager warm-up pass,
+        before graph capture."""
+        key = layer if isinstance(layer, tuple) else (layer, "kernel")
+        rows, plain = self.C.conv_wgrad_slabs(B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l)
+        n = ks * ks * Cin * N
+        slab = self._wslabs.get(key)
+        if slab is None or slab.numel() != rows * n:
+            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("weight-gradient slabs must be allocated before graph capture")
+            slab = torch.zeros(rows * n, dtype=torch.float32, device=self.dev)
+            self._wslabs[key] = slab
+            dst = self.G(*key)
+            self._finish_dyn = [e for e in self._finish_dyn if e[1].data_ptr() != dst.data_ptr()]
+            self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
+            self._finish_dirty = True
+        self.C.conv_wgrad(x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l,
+                          dst_mode, 0, 0, rows)
 
     def bn_count(self, name: str) -> int:
         """Pixels per channel in the batch statistics of a BN layer."""
@@ -310,32 +374,29 @@ class UNetEngine:
             bnB, bnA = self.bn[b2], self.bn[b1]
             # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU)
             C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, D[f"d{k}_g"], bnB["sums"],
-                       B, Rk, Rk, F)
+                       B, Rk, Rk, F, self.RS)
             C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
-                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F)
+                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
             if k == 0:
                 dq = dxlo
             else:
                 dq = D[f"d{k}_dq"]
                 C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
-            C.conv_wgrad(prev_t, dq, self.G(rc, "kernel"), None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
-                         F, 1, 1, 0, 0, 0, 0)
-            self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dq) == sum(g_B) (the BN_B node has no ReLU)
+            self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres, F, 1, 1, 0, 0, 0)
+            # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
             # convT2: input relu(BN_A(c1))
-            C.conv_wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], self.G(t2, "kernel"), bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
-                         F, 3, 1, 1, 1, 1, 0)
+            self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, 1)
             self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_dz"], None, None, 0, B, Rk, Rk, F,
                          0, Rk, Rk, F, 3, 1, 1, 1)
             C.node_bwd(D[f"d{k}_dz"], GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c1"], bnA["ab"], 1, D[f"d{k}_g"],
-                       bnA["sums"], B, Rk, Rk, F)
+                       bnA["sums"], B, Rk, Rk, F, self.RS)
             C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc"],
-                           self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F)
+                           self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
             # convT1: input relu(up?(prev))
-            C.conv_wgrad(prev_t, D[f"d{k}_dc"], self.G(t1, "kernel"), None, 1, B, prevres, prevres, cprev, up, Rk,
-                         Rk, F, 3, 1, 1, 1, 1, 0)
+            self._wgrad(prev_t, D[f"d{k}_dc"], t1, None, 1, B, prevres, prevres, cprev, up, Rk, Rk, F, 3, 1, 1, 1, 1)
             self._igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
                          F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
@@ -357,33 +418,34 @@ class UNetEngine:
             bnb, bna = self.bn[b2], self.bn[b1]
             # BN_b node: routed through the max-pool (no ReLU)
             C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
-                       bnb["sums"], B, H, H, F)
+                       bnb["sums"], B, H, H, F, self.RS)
             C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"], self.G(b2, "gamma"),
-                           self.G(b2, "beta"), B * H * H, F)
+                           self.G(b2, "beta"), B * H * H, F, self.RS)
             # pointwise 2
-            C.conv_wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], self.G(s2, "pointwise_kernel"), None, 0, B, H, H, F, 0, H, H,
-                         F, 1, 1, 0, 0, 0, 0)
+            self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H, F, 0, H, H, F, 1, 1,
+                        0, 0, 0)
             self._igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
                          H, H, F, 1, 1, 0, 0)
             # depthwise 2 on relu(BN_a(y1))
-            C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.G(s2, "depthwise_kernel"), bna["ab"], 1, B, H, H, F)
+            C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B, H, H, F,
+                       self.C.STAT_REPLICAS)
             C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_dz1"], B, H, H, F)
             C.node_bwd(D[f"e{k}_dz1"], GM_SAME, 0, None, 0, 0, None, A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_g"],
-                       bna["sums"], B, H, H, F)
+                       bna["sums"], B, H, H, F, self.RS)
             C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy"], self.G(b1, "gamma"),
-                           self.G(b1, "beta"), B * H * H, F)
+                           self.G(b1, "beta"), B * H * H, F, self.RS)
             # pointwise 1
-            C.conv_wgrad(A[f"e{k}_d1"], D[f"e{k}_dy"], self.G(s1, "pointwise_kernel"), None, 0, B, H, H, cin, 0, H,
-                         H, F, 1, 1, 0, 0, 0, 0)
+            self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy"], (s1, "pointwise_kernel"), None, 0, B, H, H, cin, 0, H, H, F, 1,
+                        1, 0, 0, 0)
             self._igemm(D[f"e{k}_dy"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
                          H, H, cin, 1, 1, 0, 0)
             # depthwise 1 on relu(x_in)
-            C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.G(s1, "depthwise_kernel"), xin.ab, 1, B, H, H, cin)
+            C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H, cin,
+                       self.C.STAT_REPLICAS)
             C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
-            C.conv_wgrad(xin.t, dx_out, self.G(rc, "kernel"), xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
-                         1, 2, 0, 0, 0, 0)
-            self.G(rc, "bias").copy_(self.G(b2, "beta"))     # sum(dx_out) == sum(g_b): max-pool routing keeps sums
+            self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F, 1, 2, 0, 0, 0)
+            # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                          H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
             if k > 0:
@@ -393,10 +455,16 @@ class UNetEngine:
             else:
                 bn0 = self.bn[names[1]]
                 C.node_bwd(D["e0_dz0"], GM_SAME, 0, D["e0_dres"], GM_SCATTER2, 0, None, A["y0"], bn0["ab"], 1,
-                           D["g0"], bn0["sums"], B, H, H, cin)
+                           D["g0"], bn0["sums"], B, H, H, cin, self.RS)
                 C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
-                               self.G(names[1], "beta"), B * H * H, cin)
-                C.entry_wgrad(self.images, self.idx, D["dy0"], self.G(names[0], "kernel"), B, self.S, ENTRY_FILTERS)
+                               self.G(names[1], "beta"), B * H * H, cin, self.RS)
+                C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
+                              ENTRY_FILTERS, self.C.STAT_REPLICAS)
+        if self._finish_dirty:
+            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("grad_finish table changed during graph capture")
+            self._build_finish()
+        C.grad_finish(self.finish_table, self.n_finish, self.finish_work)
 
     def optimizer_step(self) -> None:
         C = self.C
@@ -410,10 +478,7 @@ class UNetEngine:
         self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack)
 
     def _zero_step(self) -> None:
-        self.grad.zero_()
-        self.stats_all.zero_()
-        self.sums_all.zero_()
-        self.metrics[4:8].zero_()
+        self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
 
     def train_step_eager(self) -> None:
         self._zero_step()

@@ -73,7 +73,7 @@ int conv_splits_op(int B, int Ho, int Wo, int N, int ks, int stride, int pad, in
 
 void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win, int Cin,
                    int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t, int pad_l, int dst_mode,
-                   int m_chunk) {
+                   int m_chunk, int algo, int slabs) {
   WgradParams p{};
   p.x = ptr<const bf16_t>(x, "x");
   p.dy = ptr<const bf16_t>(dy, "dy");
@@ -85,10 +85,27 @@ void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu
   p.K = ks * ks * Cin;
   p.dst_mode = dst_mode;
   p.m_chunk = m_chunk;
+  p.algo = algo;
+  p.slabs = slabs;
+  TORCH_CHECK(slabs <= 0 || slabs == conv_wgrad_slabs(p), "conv_wgrad: slab rows != conv_wgrad_slabs()");
+  TORCH_CHECK(slabs <= 0 || !conv_wgrad_plain_slabs(p) || dw.numel() == (int64_t)slabs * p.K * N,
+              "conv_wgrad: a plain-stored slab must be exactly rows * K * N");
   TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv_wgrad: x size");
   TORCH_CHECK(dy.numel() == (int64_t)p.M * N, "conv_wgrad: dy size");
-  TORCH_CHECK(dw.numel() >= (int64_t)p.K * N, "conv_wgrad: dw size");
+  TORCH_CHECK(dw.numel() >= (int64_t)(slabs > 0 ? slabs : 1) * p.K * N, "conv_wgrad: dw size");
   ok(conv_wgrad(p, stream()), "conv_wgrad");
+}
+
+// (slab rows, rows are plain-stored (sum without re-zeroing) rather than atomic replicas)
+std::tuple<int, bool> conv_wgrad_slabs_op(int B, int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks,
+                                          int stride, int pad_t, int pad_l, int algo) {
+  WgradParams p{};
+  p.B = B; p.Hin = Hin; p.Win = Win; p.Cin = Cin; p.up_in = up_in;
+  p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
+  p.M = B * Ho * Wo;
+  p.K = ks * ks * Cin;
+  p.algo = algo;
+  return {conv_wgrad_slabs(p), conv_wgrad_plain_slabs(p)};
 }
 
 DwParams dwp(int B, int H, int W, int C) {
@@ -116,13 +133,16 @@ void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W
   ok(dw_dgrad(p, stream()), "dw_dgrad");
 }
 
-void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C) {
+void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C,
+                 int replicas) {
   DwParams p = dwp(B, H, W, C);
   p.x = ptr<const bf16_t>(x, "x");
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.dw = ptr<float>(dw, "dw");
   p.xf = xf(ab, C, relu);
-  TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && dy.numel() == x.numel() && dw.numel() == 9 * C, "dw_wgrad sizes");
+  p.replicas = replicas < 1 ? 1 : replicas;
+  TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && dy.numel() == x.numel() &&
+                  dw.numel() == (int64_t)p.replicas * 9 * C, "dw_wgrad sizes");
   ok(dw_wgrad(p, stream()), "dw_wgrad");
 }
 
@@ -140,14 +160,17 @@ void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bi
   ok(entry_fwd(p, stream()), "entry_fwd");
 }
 
-void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor dw, int B, int S, int Cout) {
+void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor dw, int B, int S, int Cout,
+                    int replicas) {
   EntryParams p{};
+  p.replicas = replicas < 1 ? 1 : replicas;
   p.images = ptr<const uint8_t>(images, "images");
   p.idx = ptr<const int32_t>(idx, "idx");
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.dw = ptr<float>(dw, "dw");
   p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
-  TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout && dw.numel() == 27 * Cout, "entry_wgrad sizes");
+  TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout && dw.numel() == (int64_t)p.replicas * 27 * Cout,
+              "entry_wgrad sizes");
   ok(entry_wgrad(p, stream()), "entry_wgrad");
 }
 
@@ -184,8 +207,9 @@ void bn_moving_update_op(at::Tensor table, int n_layers, double momentum) {
 }
 
 void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask1, OptT argmax, at::Tensor v, OptT ab,
-                 int relu_node, at::Tensor out, OptT sums, int B, int H, int W, int C) {
+                 int relu_node, at::Tensor out, OptT sums, int B, int H, int W, int C, int sum_reps) {
   NodeBwdParams p{};
+  p.sum_reps = sum_reps < 1 ? 1 : sum_reps;
   p.src[0] = GradSrc{optr<const bf16_t>(src0, "src0"), src0.has_value() ? mode0 : 0, mask0};
   p.src[1] = GradSrc{optr<const bf16_t>(src1, "src1"), src1.has_value() ? mode1 : 0, mask1};
   if (!p.src[0].p) p.src[0].mode = GM_NONE;
@@ -199,6 +223,7 @@ void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask
   p.B = B; p.H = H; p.W = W; p.C = C;
   const int64_t n = (int64_t)B * H * W * C;
   TORCH_CHECK(v.numel() == n && out.numel() == n, "node_bwd: v/out size");
+  if (sums) TORCH_CHECK(sums->numel() >= (int64_t)p.sum_reps * (ab ? 2 : 1) * C, "node_bwd: sums size");
   const int64_t half = (int64_t)B * ((H + 1) / 2) * ((W + 1) / 2) * C;
   for (int s = 0; s < 2; ++s) {
     const OptT& t = s ? src1 : src0;
@@ -212,8 +237,10 @@ void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask
 }
 
 void bn_bwd_apply_op(at::Tensor g, at::Tensor y, at::Tensor ab, at::Tensor sums, at::Tensor dy, OptT dgamma,
-                     OptT dbeta, int M, int C) {
+                     OptT dbeta, int M, int C, int sum_reps) {
   BnBwdApplyParams p{};
+  p.sum_reps = sum_reps < 1 ? 1 : sum_reps;
+  TORCH_CHECK(sums.numel() >= (int64_t)p.sum_reps * 2 * C, "bn_bwd_apply: sums size");
   p.g = ptr<const bf16_t>(g, "g");
   p.y = ptr<const bf16_t>(y, "y");
   p.ab = ptr<const float>(ab, "ab");
@@ -323,6 +350,53 @@ void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n
      "pack_weights");
 }
 
+// entries: list of (src, dst, n, replicas, mode) -> (device table, grid size)
+std::tuple<at::Tensor, int> make_grad_finish_table(std::vector<std::tuple<at::Tensor, at::Tensor, int, int, int>> entries) {
+  std::vector<GradFinish> h;
+  at::Device dev = std::get<0>(entries.at(0)).device();
+  for (auto& e : entries) {
+    GradFinish g{};
+    g.src = ptr<float>(std::get<0>(e), "src");
+    g.dst = ptr<float>(std::get<1>(e), "dst");
+    g.n = std::get<2>(e); g.replicas = std::get<3>(e); g.mode = std::get<4>(e);
+    TORCH_CHECK(g.n % 4 == 0 && (reinterpret_cast<uintptr_t>(g.src) & 15) == 0 &&
+                (reinterpret_cast<uintptr_t>(g.dst) & 15) == 0, "grad_finish: n % 4 and 16-byte alignment");
+    TORCH_CHECK(std::get<1>(e).numel() >= g.n, "grad_finish: dst size");
+    TORCH_CHECK(std::get<0>(e).numel() >= (int64_t)g.n * (g.mode == GF_COPY ? 1 : g.replicas), "grad_finish: src size");
+    h.push_back(g);
+  }
+  TORCH_CHECK(h.size() <= 256, "grad_finish: at most 256 entries");
+  const int work = grad_finish_work(h.data(), (int)h.size());
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(GradFinish))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(GradFinish));
+  return {cpu.to(dev), work};
+}
+
+void grad_finish_op(at::Tensor table, int n_entries, int total_work) {
+  TORCH_CHECK(table.numel() == (int64_t)n_entries * (int64_t)sizeof(GradFinish), "grad_finish: table size");
+  ok(grad_finish(ptr<const GradFinish>(table, "table"), n_entries, total_work, stream()), "grad_finish");
+}
+
+at::Tensor make_zero_table(std::vector<at::Tensor> spans) {
+  std::vector<ZeroSpan> h;
+  for (auto& t : spans) {
+    ZeroSpan z{};
+    z.p = t.data_ptr();
+    z.bytes = t.numel() * t.element_size();
+    TORCH_CHECK(t.is_contiguous() && (reinterpret_cast<uintptr_t>(z.p) & 15) == 0 && z.bytes % 16 == 0,
+                "zero_spans: spans must be contiguous, 16-byte aligned, multiple of 16 bytes");
+    h.push_back(z);
+  }
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(ZeroSpan))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(ZeroSpan));
+  return cpu.to(spans.at(0).device());
+}
+
+void zero_spans_op(at::Tensor table, int n, int64_t max_bytes) {
+  TORCH_CHECK(table.numel() == (int64_t)n * (int64_t)sizeof(ZeroSpan), "zero_spans: table size");
+  ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream()), "zero_spans");
+}
+
 void render_cracks_op(at::Tensor segs, at::Tensor params, at::Tensor images, at::Tensor masks, int n, int img,
                       int max_seg) {
   TORCH_CHECK(images.numel() == (int64_t)n * img * img * 3 && masks.numel() == (int64_t)n * img * img &&
@@ -349,17 +423,43 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"),
         py::arg("pad_l"), py::arg("ws") = py::none(), py::arg("algo") = 0);
   m.def("conv_splits", &conv_splits_op);
-  m.def("conv_wgrad", &conv_wgrad_op);
+  m.def("conv_wgrad", &conv_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
+        py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),
+        py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("dst_mode"),
+        py::arg("m_chunk") = 0, py::arg("algo") = 0, py::arg("slabs") = 0);
+  m.def("conv_wgrad_slabs", &conv_wgrad_slabs_op, py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"),
+        py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"),
+        py::arg("pad_t"), py::arg("pad_l"), py::arg("algo") = 0);
+  m.attr("GF_SUM") = (int)GF_SUM;
+  m.attr("TUNE_WGRAD3_BLOCKS") = (int)TUNE_WGRAD3_BLOCKS;
+  m.attr("TUNE_WGRAD3_MINTILES") = (int)TUNE_WGRAD3_MINTILES;
   m.def("dw_fwd", &dw_fwd_op);
   m.def("dw_dgrad", &dw_dgrad_op);
-  m.def("dw_wgrad", &dw_wgrad_op);
+  m.def("dw_wgrad", &dw_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
+        py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1);
   m.def("entry_fwd", &entry_fwd_op);
-  m.def("entry_wgrad", &entry_wgrad_op);
+  m.def("entry_wgrad", &entry_wgrad_op, py::arg("images"), py::arg("idx"), py::arg("dy"), py::arg("dw"), py::arg("B"),
+        py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1);
+  m.def("make_grad_finish_table", &make_grad_finish_table);
+  m.def("grad_finish", &grad_finish_op);
+  m.def("make_zero_table", &make_zero_table);
+  m.def("zero_spans", &zero_spans_op);
+  m.def("set_tune", &cfl_set_tune);
+  m.attr("GF_REDUCE") = (int)GF_REDUCE;
+  m.attr("GF_COPY") = (int)GF_COPY;
+  m.attr("TUNE_NODE_BWD_BLOCKS") = (int)TUNE_NODE_BWD_BLOCKS;
+  m.attr("TUNE_DW_WGRAD_BLOCKS") = (int)TUNE_DW_WGRAD_BLOCKS;
+  m.attr("TUNE_ENTRY_WGRAD_BLOCKS") = (int)TUNE_ENTRY_WGRAD_BLOCKS;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);
-  m.def("node_bwd", &node_bwd_op);
-  m.def("bn_bwd_apply", &bn_bwd_apply_op);
+  m.def("node_bwd", &node_bwd_op, py::arg("src0"), py::arg("mode0"), py::arg("mask0"), py::arg("src1"),
+        py::arg("mode1"), py::arg("mask1"), py::arg("argmax"), py::arg("v"), py::arg("ab"), py::arg("relu_node"),
+        py::arg("out"), py::arg("sums"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"),
+        py::arg("sum_reps") = 1);
+  m.def("bn_bwd_apply", &bn_bwd_apply_op, py::arg("g"), py::arg("y"), py::arg("ab"), py::arg("sums"), py::arg("dy"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("C"), py::arg("sum_reps") = 1);
+  m.attr("SUM_REPLICAS") = 16;
   m.def("pool_res_fwd", &pool_res_fwd_op);
   m.def("bn_add_fwd", &bn_add_fwd_op);
   m.def("head_fwd", &head_fwd_op);

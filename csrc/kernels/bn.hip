@@ -56,118 +56,149 @@ __global__ void bn_moving_kernel(const BnMoving* layers, float momentum) {
   }
 }
 
-__global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
-  __shared__ float red[2][4][256];
-  const int G = p.C >> 3, lg = ilog2(G);
-  const int cg = threadIdx.x & (G - 1), c0 = cg * 8;
+// Gather the incoming gradient of one item (pixel `w` of row (b, h), channels c0..c0+7): loads only, so the
+// caller can issue two items' gathers before any store (memory-level parallelism for a latency-bound walk).
+// M0 / M1: compile-time GradMode of the two sources (-1 = read from p at run time)
+template <int M0, int M1>
+CFL_DEVICE void node_gather(const NodeBwdParams& p, int b, int h, int w, int c0, const float* a, const float* bb,
+                            float* y, float* v, float* g) {
   const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
-  const int rows = p.B * p.H, items = p.W << lg;
-  float a[8], bb[8], mean[8], rstd[8];
-  if (p.ab) {
-    load_f8(p.ab + c0, a);
-    load_f8(p.ab + p.C + c0, bb);
-    load_f8(p.ab + 2 * p.C + c0, mean);
-    load_f8(p.ab + 3 * p.C + c0, rstd);
+  const size_t pix = ((size_t)b * p.H + h) * p.W + w;
+  load8(p.v + pix * p.C + c0, y);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = p.ab ? fmaf(a[j], y[j], bb[j]) : y[j];
+    g[j] = 0.f;
   }
-  float s[2][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    const int b = row / p.H, h = row - b * p.H;
-    for (int it = threadIdx.x; it < items; it += NT) {
-      const int w = it >> lg;
-      const int pix = row * p.W + w;
-      float y[8], v[8], g[8];
-      load8(p.v + (size_t)pix * p.C + c0, y);
+  for (int si = 0; si < 2; ++si) {
+    GradSrc src = p.src[si];
+    const int cm = si == 0 ? M0 : M1;
+    if (cm >= 0) src.mode = cm;
+    if (src.mode == GM_NONE) continue;
+    float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (src.mode == GM_SAME) {
+      load8(src.p + pix * p.C + c0, t);
+    } else if (src.mode == GM_SCATTER2) {
+      if (((h | w) & 1) == 0) load8(src.p + ((size_t)(b * Hh + (h >> 1)) * Wh + (w >> 1)) * p.C + c0, t);
+    } else if (src.mode == GM_SUM2X2) {
+      const int W2 = p.W * 2;
+      float u[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = p.ab ? fmaf(a[j], y[j], bb[j]) : y[j];
-        g[j] = 0.f;
-      }
+      for (int q = 0; q < 4; ++q)
+        load8(src.p + ((size_t)(b * 2 * p.H + 2 * h + (q >> 1)) * W2 + 2 * w + (q & 1)) * p.C + c0, u[q]);
 #pragma unroll
-      for (int si = 0; si < 2; ++si) {
-        const GradSrc src = p.src[si];
-        if (src.mode == GM_NONE) continue;
-        float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (src.mode == GM_SAME) {
-          load8(src.p + (size_t)pix * p.C + c0, t);
-        } else if (src.mode == GM_SCATTER2) {
-          if (((h | w) & 1) == 0) load8(src.p + ((size_t)(b * Hh + (h >> 1)) * Wh + (w >> 1)) * p.C + c0, t);
-        } else if (src.mode == GM_SUM2X2) {
-          const int W2 = p.W * 2;
+      for (int j = 0; j < 8; ++j) t[j] = (u[0][j] + u[1][j]) + (u[2][j] + u[3][j]);
+    } else if (src.mode == GM_MAXPOOL) {
+      // pooled outputs whose 3x3/s2 window contains (h, w): oh = h>>1 (ky = h&1) and, for even h >= 2,
+      // oh = h/2 - 1 (ky = 2); same for w
+      const int ohs[2] = {h >> 1, ((h & 1) == 0 && h >= 2) ? (h >> 1) - 1 : -1};
+      const int kys[2] = {h & 1, 2};
+      const int ows[2] = {w >> 1, ((w & 1) == 0 && w >= 2) ? (w >> 1) - 1 : -1};
+      const int kxs[2] = {w & 1, 2};
 #pragma unroll
-          for (int dy = 0; dy < 2; ++dy)
+      for (int i = 0; i < 2; ++i) {
+        if (ohs[i] < 0 || ohs[i] >= Hh) continue;
 #pragma unroll
-            for (int dx = 0; dx < 2; ++dx) {
-              float u[8];
-              load8(src.p + ((size_t)(b * 2 * p.H + 2 * h + dy) * W2 + 2 * w + dx) * p.C + c0, u);
+        for (int k = 0; k < 2; ++k) {
+          if (ows[k] < 0 || ows[k] >= Wh) continue;
+          const size_t o = ((size_t)(b * Hh + ohs[i]) * Wh + ows[k]) * p.C + c0;
+          const uint2 am = *reinterpret_cast<const uint2*>(p.argmax + o);
+          const int want = kys[i] * 3 + kxs[k];
+          float u[8];
+          load8(src.p + o, u);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) t[j] += u[j];
-            }
-        } else if (src.mode == GM_MAXPOOL) {
-          // pooled outputs whose 3x3/s2 window contains (h, w): oh = h>>1 (ky = h&1) and, for even h >= 2,
-          // oh = h/2 - 1 (ky = 2); same for w
-          const int ohs[2] = {h >> 1, ((h & 1) == 0 && h >= 2) ? (h >> 1) - 1 : -1};
-          const int kys[2] = {h & 1, 2};
-          const int ows[2] = {w >> 1, ((w & 1) == 0 && w >= 2) ? (w >> 1) - 1 : -1};
-          const int kxs[2] = {w & 1, 2};
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            if (ohs[i] < 0 || ohs[i] >= Hh) continue;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              if (ows[k] < 0 || ows[k] >= Wh) continue;
-              const size_t o = ((size_t)(b * Hh + ohs[i]) * Wh + ows[k]) * p.C + c0;
-              const uint2 am = *reinterpret_cast<const uint2*>(p.argmax + o);
-              const int want = kys[i] * 3 + kxs[k];
-              float u[8];
-              load8(src.p + o, u);
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const uint32_t word = j < 4 ? am.x : am.y;
-                if ((int)((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[j];
-              }
-            }
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? am.x : am.y;
+            if ((int)((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[j];
           }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] += src.mask ? (v[j] > 0.f ? t[j] : 0.f) : t[j];
-      }
-      if (p.relu_node) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = v[j] > 0.f ? g[j] : 0.f;
-      }
-      const uint4 gv = pack8(g);
-      *reinterpret_cast<uint4*>(p.out + (size_t)pix * p.C + c0) = gv;
-      if (p.sums) {
-        float gr[8];
-        unpack8(gv, gr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s[0][j] += gr[j];
-          if (p.ab) s[1][j] += gr[j] * (y[j] - mean[j]) * rstd[j];
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] += src.mask ? (v[j] > 0.f ? t[j] : 0.f) : t[j];
+  }
+}
+
+template <int M0, int M1>
+__global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
+  __shared__ float red[2][4][256];
+  const int G = p.C >> 3, lg = ilog2(G);
+  const int c0 = (threadIdx.x & (G - 1)) * 8;
+  const bool has_ab = p.ab != nullptr;
+  float a[8], bb[8], mean[8], rstd[8];
+  load_f8_or(p.ab + c0, has_ab, 1.f, a);
+  load_f8_or(p.ab + p.C + c0, has_ab, 0.f, bb);
+  load_f8_or(p.ab + 2 * p.C + c0, has_ab, 0.f, mean);
+  load_f8_or(p.ab + 3 * p.C + c0, has_ab, 0.f, rstd);
+  float s[2][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+  auto finish = [&](size_t pix, const float* y, const float* v, float* g) {
+    if (p.relu_node) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = v[j] > 0.f ? g[j] : 0.f;
+    }
+    const uint4 gv = pack8(g);
+    *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
+    if (p.sums) {
+      float gr[8];
+      unpack8(gv, gr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[0][j] += gr[j];
+        s[1][j] += gr[j] * (y[j] - mean[j]) * rstd[j];     // unused (and rstd = 0) for a plain node
+      }
+    }
+  };
+  // flat items (pixel, channel group), two per iteration; the grid stride is a multiple of G
+  const int total = (p.B * p.H * p.W) << lg;
+  const int HW = p.H * p.W;
+  const int stride = gridDim.x * NT;
+  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += 2 * stride) {
+    const int it2 = it + stride;
+    const bool two = it2 < total;
+    float y0[8], v0[8], g0[8], y1[8], v1[8], g1[8];
+    const int pix0 = it >> lg, b0 = pix0 / HW, r0 = pix0 - b0 * HW, h0 = r0 / p.W;
+    node_gather<M0, M1>(p, b0, h0, r0 - h0 * p.W, c0, a, bb, y0, v0, g0);
+    int pix1 = 0;
+    if (two) {
+      pix1 = it2 >> lg;
+      const int b1 = pix1 / HW, r1 = pix1 - b1 * HW, h1 = r1 / p.W;
+      node_gather<M0, M1>(p, b1, h1, r1 - h1 * p.W, c0, a, bb, y1, v1, g1);
+    }
+    finish((size_t)pix0, y0, v0, g0);
+    if (two) finish((size_t)pix1, y1, v1, g1);
   }
   if (!p.sums) return;
-  if (p.ab) block_channel_atomics<2>(s, G, p.C, p.sums, red);
+  // replica row of this block: every block adding into ONE row of sums serialises at the memory-side atomic units
+  const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
+  if (p.ab) block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * 2 * p.C, red);
   else {
     float s1[1][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[0][j] = s[0][j];
-    block_channel_atomics<1>(s1, G, p.C, p.sums, red);
+    block_channel_atomics<1>(s1, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * p.C, red);
   }
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
+  __shared__ float ssum[2 * 256];
   const int G = p.C >> 3, lg = ilog2(G);
   const float invM = 1.f / (float)p.M;
   const int total = p.M << lg;
+  // sum the node_bwd replica rows [reps][2][C] once per block (L2-resident, 2*C*reps floats)
+  // (all threads load in parallel: thread -> (element, replica subset), combined with LDS atomics)
+  const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
+  const int C2 = 2 * p.C;
+  for (int e = threadIdx.x; e < C2; e += NT) ssum[e] = 0.f;
+  __syncthreads();
+  for (int q = threadIdx.x; q < C2 * reps; q += NT) atomicAdd(&ssum[q % C2], p.sums[q]);
+  __syncthreads();
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < p.C; c += NT) {
-      if (p.dbeta) p.dbeta[c] = p.sums[c];
-      if (p.dgamma) p.dgamma[c] = p.sums[p.C + c];
+      if (p.dbeta) p.dbeta[c] = ssum[c];
+      if (p.dgamma) p.dgamma[c] = ssum[p.C + c];
     }
   }
   // grid stride is a multiple of G, so a thread's channel group never changes
@@ -178,8 +209,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
   load_f8(p.ab + 3 * p.C + c0, rstd);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    k1[j] = p.sums[c0 + j] * invM;
-    k2[j] = p.sums[p.C + c0 + j] * invM;
+    k1[j] = ssum[c0 + j] * invM;
+    k2[j] = ssum[p.C + c0 + j] * invM;
   }
   for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
     const int m = t >> lg;
@@ -214,16 +245,28 @@ int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float mo
 
 int node_bwd(const NodeBwdParams& p, hipStream_t st) {
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
-  int blocks = p.B * p.H;
-  if (blocks > 1024) blocks = 1024;   // bounded grid: one set of channel atomics per block
-  hipLaunchKernelGGL(node_bwd_kernel, dim3(blocks), dim3(NT), 0, st, p);
+  const int64_t items = (int64_t)p.B * p.H * p.W * (p.C / 8);
+  int blocks = (int)((items + 2 * NT - 1) / (2 * NT));
+  const int cap = cfl_tune(TUNE_NODE_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_NODE_BWD_BLOCKS) : 1024;
+  if (blocks > cap) blocks = cap;     // bounded grid: one set of channel atomics per block
+  if (blocks < 1) blocks = 1;
+  const int m0 = p.src[0].mode, m1 = p.src[1].mode;
+  // specialised instances for the engine's source combinations (fewer live registers, no mode branches)
+  if (m0 == GM_SAME && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SUM2X2 && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_MAXPOOL && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_MAXPOOL, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SAME && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SAME>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SUM2X2 && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_SAME>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SAME && m1 == GM_SCATTER2) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SCATTER2>), dim3(blocks), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL((node_bwd_kernel<-1, -1>), dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
   if (p.C % 8 || !pow2(p.C / 8)) return 1;
+  if (p.C > 256) return 1;
   int blocks = (int)(((int64_t)p.M * (p.C / 8) + NT - 1) / NT);
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -55,6 +55,18 @@ CFL_DEVICE void load_f8(const float* p, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+// 8 floats from p when cond, else 8 copies of dflt. Written with float4 values (not a branch over array stores) so
+// the two paths merge as register phis: a branch-dependent store into a private array makes the compiler keep the
+// array in scratch memory.
+CFL_DEVICE void load_f8_or(const float* p, bool cond, float dflt, float* f) {
+  float4 a = make_float4(dflt, dflt, dflt, dflt), b = a;
+  if (cond) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 CFL_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -9,8 +9,8 @@
 //
 // Output tile BKO(k) x BNO(n) (128x128 for the big K*N layers, down to 32x32), 4 waves 2x2, reduction step 32
 // pixels, register-staged double buffer. The M range is split over gridDim.z so the grid holds ~512 long-running
-// blocks; partial tiles are combined with fp32 atomics directly into the layer's slot of the flat gradient buffer,
-// writing Keras layouts (HWIO for Conv2D / pointwise; (kh,kw,out,in) with the spatial flip for Conv2DTranspose).
+// blocks; partial tiles are combined with fp32 atomics into the layer's slot of the flat gradient buffer (or into
+// WGRAD_REPLICAS replica rows summed by grad_finish), writing Keras layouts (HWIO for Conv2D / pointwise; (kh,kw,out,in) with the spatial flip for Conv2DTranspose).
 #include "common.h"
 #include "launch.h"
 
@@ -164,7 +164,9 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
     buf ^= 1;
   }
 
-  // epilogue: D[k][n], col n = lane&15, row k = (lane>>4)*4 + r
+  // epilogue: D[k][n], col n = lane&15, row k = (lane>>4)*4 + r; slab mode spreads the split blocks' atomics
+  // over replica rows (every block adding into ONE row serialises at the memory-side atomic units)
+  float* dwb = p.slabs > 0 ? p.dw + (size_t)(blockIdx.z % p.slabs) * p.K * p.N : p.dw;
 #pragma unroll
   for (int i = 0; i < FK; ++i)
 #pragma unroll
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
         } else {
           dst = (size_t)k * p.N + n;
         }
-        atomicAdd(&p.dw[dst], acc[i][j][r]);
+        atomicAdd(&dwb[dst], acc[i][j][r]);
       }
     }
 }
@@ -204,7 +206,20 @@ void launch(const WgradParams& p, hipStream_t st) {
 
 }  // namespace
 
+bool conv3x3_wgrad_supported(const WgradParams& p);
+int conv3x3_wgrad(const WgradParams& p, hipStream_t st);
+int conv3x3_wgrad_splits(const WgradParams& p);
+
+int conv_wgrad_slabs(const WgradParams& p) {
+  if (p.algo != 1 && conv3x3_wgrad_supported(p)) return conv3x3_wgrad_splits(p);
+  return WGRAD_REPLICAS;
+}
+
+bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x3_wgrad_supported(p); }
+
 int conv_wgrad(const WgradParams& p, hipStream_t st) {
+  if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
+  if (p.algo != 1 && conv3x3_wgrad_supported(p)) return conv3x3_wgrad(p, st);
   if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
   const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
   if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) launch<128, 128>(p, st);

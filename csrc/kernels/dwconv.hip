@@ -5,8 +5,9 @@
 // window (3 rows x SW+2 columns) is loaded once, the producer's BN-apply + ReLU (coefficients held in registers)
 // applied once per loaded element, and reused by the 3 horizontal taps of every output in the strip. Blocks walk
 // whole rows (32-bit indices, shifts). Keras depthwise kernel layout (3,3,C,1) = [tap][C].
-// wgrad keeps 72 fp32 partial sums per thread across its rows, reduces over the wave's pixel lanes with shuffles
-// and over the block's waves through LDS, then one atomic per (tap, channel) per block.
+// wgrad keeps 72 fp32 partial sums per thread across its items, reduces over the wave's pixel lanes with shuffles
+// and over the block's waves through LDS, then one atomic per (tap, channel) per block into one of `replicas`
+// copies of the gradient row (grad_finish in optim.hip sums the copies).
 #include "common.h"
 #include "launch.h"
 
@@ -19,16 +20,8 @@ struct Coef8 {
 };
 
 CFL_DEVICE void load_coef(const InXform& xf, int c0, Coef8& k) {
-  if (xf.ab) {
-    load_f8(xf.ab + c0, k.a);
-    load_f8(xf.ab + xf.C + c0, k.b);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      k.a[j] = 1.f;
-      k.b[j] = 0.f;
-    }
-  }
+  load_f8_or(xf.ab + c0, xf.ab != nullptr, 1.f, k.a);
+  load_f8_or(xf.ab + xf.C + c0, xf.ab != nullptr, 0.f, k.b);
 }
 
 CFL_DEVICE void load_x8(const bf16_t* p, const Coef8& k, bool has_ab, int relu, float* f) {
@@ -98,7 +91,7 @@ __global__ __launch_bounds__(NT) void dw_conv_kernel(const bf16_t* __restrict__ 
 }
 
 template <int SW>
-__global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p) {
+__global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) {
   __shared__ float red[4][9][256];
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
@@ -111,32 +104,34 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-  const int rows = p.B * p.H, items = (p.W / SW) << lg;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  // flat items (row, strip, channel group): every thread gets work whatever the row width
+  const int strips = p.W / SW;
+  const int total = (p.B * p.H * strips) << lg;
+  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += gridDim.x * NT) {
+    const int pix = it >> lg;                       // row * strips + strip
+    const int row = pix / strips;
+    const int w0 = (pix - row * strips) * SW;
     const int b = row / p.H, h = row - b * p.H;
-    for (int it = threadIdx.x; it < items; it += NT) {
-      const int w0 = (it >> lg) * SW;
-      float g[SW][8];
+    float g[SW][8];
 #pragma unroll
-      for (int i = 0; i < SW; ++i) load8(p.dy + ((size_t)row * p.W + w0 + i) * p.C + c0, g[i]);
+    for (int i = 0; i < SW; ++i) load8(p.dy + ((size_t)row * p.W + w0 + i) * p.C + c0, g[i]);
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int ih = h + ky - 1;
-        if (ih < 0 || ih >= p.H) continue;
-        const bf16_t* src = p.x + (size_t)(b * p.H + ih) * p.W * p.C + c0;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int ih = h + ky - 1;
+      if (ih < 0 || ih >= p.H) continue;
+      const bf16_t* src = p.x + (size_t)(b * p.H + ih) * p.W * p.C + c0;
 #pragma unroll
-        for (int cx = 0; cx < SW + 2; ++cx) {
-          const int iw = w0 + cx - 1;
-          if (iw < 0 || iw >= p.W) continue;
-          float f[8];
-          load_x8(src + (size_t)iw * p.C, k, has_ab, p.xf.relu, f);
+      for (int cx = 0; cx < SW + 2; ++cx) {
+        const int iw = w0 + cx - 1;
+        if (iw < 0 || iw >= p.W) continue;
+        float f[8];
+        load_x8(src + (size_t)iw * p.C, k, has_ab, p.xf.relu, f);
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int o = cx - kx;
-            if (o < 0 || o >= SW) continue;
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SW) continue;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[ky * 3 + kx][j] = fmaf(f[j], g[o][j], acc[ky * 3 + kx][j]);
-          }
+          for (int j = 0; j < 8; ++j) acc[ky * 3 + kx][j] = fmaf(f[j], g[o][j], acc[ky * 3 + kx][j]);
         }
       }
     }
@@ -156,9 +151,12 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p) {
       for (int j = 0; j < 8; ++j) red[wid][t][c0 + j] = acc[t][j];
   }
   __syncthreads();
+  // one contiguous 9*C row of atomics per block, spread over `replicas` rows (reduced later by grad_finish):
+  // every block adding into ONE row serialises at the memory-side atomic units
+  float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
   for (int e = threadIdx.x; e < 9 * p.C; e += NT) {
     const int t = e / p.C, c = e - t * p.C;
-    atomicAdd(&p.dw[t * p.C + c], red[0][t][c] + red[1][t][c] + red[2][t][c] + red[3][t][c]);
+    atomicAdd(&dst[t * p.C + c], red[0][t][c] + red[1][t][c] + red[2][t][c] + red[3][t][c]);
   }
 }
 
@@ -184,12 +182,13 @@ int dw_dgrad(const DwParams& p, hipStream_t st) {
 int dw_wgrad(const DwParams& p, hipStream_t st) {
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
   const int sw = (p.W % 4 == 0) ? 4 : 1;
-  // a few rows per block keeps the per-block reduction + 9*C atomics amortised
-  const int items_per_row = (p.W / sw) * (p.C / 8);
-  const int rows_per_block = items_per_row >= 4 * NT ? 1 : (4 * NT + items_per_row - 1) / items_per_row;
-  int blocks = (p.B * p.H + rows_per_block - 1) / rows_per_block;
-  if (blocks > 1024) blocks = 1024;
-  if (sw == 4) hipLaunchKernelGGL(dw_wgrad_kernel<4>, dim3(blocks), dim3(NT), 0, st, p);
-  else hipLaunchKernelGGL(dw_wgrad_kernel<1>, dim3(blocks), dim3(NT), 0, st, p);
+  const int64_t items = (int64_t)p.B * p.H * (p.W / sw) * (p.C / 8);
+  int blocks = (int)((items + 2 * NT - 1) / (2 * NT));          // >= 2 items per thread
+  const int cap = cfl_tune(TUNE_DW_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_WGRAD_BLOCKS) : 1024;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  const int reps = p.replicas > 1 ? p.replicas : 1;
+  if (sw == 4) hipLaunchKernelGGL(dw_wgrad_kernel<4>, dim3(blocks), dim3(NT), 0, st, p, reps);
+  else hipLaunchKernelGGL(dw_wgrad_kernel<1>, dim3(blocks), dim3(NT), 0, st, p, reps);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -39,8 +39,15 @@ struct WgradParams {
   int M, K;
   int dst_mode;        // 0: dw[k*N + n] (Keras HWIO / pointwise layout)   1: Conv2DTranspose (kh,kw,out,in) flip
   int m_chunk;         // pixels per block along M (multiple of 32), 0 = auto
+  int algo;            // 0 auto (3x3/s1 -> halo wgrad conv3x3_wgrad.hip, else generic), 1 generic only
+  int slabs;           // 0: accumulate into dw with atomics.  >0: dw is [slabs][K*N] (destination layout) and must
+                       //    hold exactly conv_wgrad_slabs(p) rows; the rows are summed later by grad_finish
+                       //    (halo kernel: one plain-stored row per pixel split; generic: atomic replica rows)
 };
 int conv_wgrad(const WgradParams& p, hipStream_t st);
+int conv_wgrad_slabs(const WgradParams& p);
+bool conv_wgrad_plain_slabs(const WgradParams& p);   // slab rows are plain-stored (else atomic replica rows)
+#define WGRAD_REPLICAS 16
 
 // ---------------------------------------------------------------- depthwise 3x3 (dwconv.hip)
 struct DwParams {
@@ -48,9 +55,10 @@ struct DwParams {
   const float* w;      // Keras depthwise kernel (3,3,C,1) fp32
   const bf16_t* dy;    // gradient of the dw output (dgrad / wgrad)
   bf16_t* y;           // fwd output / dgrad output
-  float* dw;           // wgrad destination (fp32, atomic accumulate)
+  float* dw;           // wgrad destination (fp32, atomic accumulate): [replicas][9][C]
   InXform xf;
   int B, H, W, C;
+  int replicas;        // wgrad: >1 = spread block atomics over that many copies of the row (summed by grad_finish)
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);
@@ -65,8 +73,9 @@ struct EntryParams {
   bf16_t* y;               // [B, Ho, Wo, Cout]
   float* stats;            // [STAT_REPLICAS][2][Cout]
   const bf16_t* dy;        // wgrad: [B,Ho,Wo,Cout]
-  float* dw;               // wgrad destination (3,3,3,Cout) fp32
+  float* dw;               // wgrad destination (3,3,3,Cout) fp32: [replicas][27*Cout]
   int B, S, Cout, Ho, Wo;
+  int replicas;            // wgrad: >1 = spread block atomics over that many row copies (summed by grad_finish)
 };
 int entry_fwd(const EntryParams& p, hipStream_t st);
 int entry_wgrad(const EntryParams& p, hipStream_t st);
@@ -99,8 +108,9 @@ struct NodeBwdParams {
   const float* ab;         // BN coefficients (4 rows) or nullptr for a plain node
   int relu_node;           // mask the total by [v > 0]
   bf16_t* out;             // gradient w.r.t. the BN output (BN node) or w.r.t. x (plain node)
-  float* sums;             // [2][C]: sum g, sum g*xhat (BN node) / [C] sum g (plain node) / nullptr
+  float* sums;             // [sum_reps][2][C]: sum g, sum g*xhat (BN node) / [sum_reps][C] sum g (plain) / nullptr
   int B, H, W, C;
+  int sum_reps;            // replica rows of sums (block b adds into row b % sum_reps); <= 1: one row
 };
 int node_bwd(const NodeBwdParams& p, hipStream_t st);
 
@@ -108,11 +118,12 @@ struct BnBwdApplyParams {
   const bf16_t* g;         // gradient w.r.t. BN output (masked)
   const bf16_t* y;         // raw BN input
   const float* ab;         // 4 rows: a, b, mean, rstd
-  const float* sums;       // [2][C]
+  const float* sums;       // [sum_reps][2][C] (node_bwd replica rows, summed here)
   bf16_t* dy;              // gradient w.r.t. y
   float* dgamma;           // flat-grad slots (written, not accumulated) or nullptr
   float* dbeta;
   int M, C;
+  int sum_reps;
 };
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st);
 
@@ -177,6 +188,37 @@ struct PackView {
 };
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
                  hipStream_t st);
+
+// ---------------------------------------------------------------- step bookkeeping (optim.hip)
+// grad_finish: ONE launch at the end of backward for every gradient that was accumulated into replica rows
+// (GF_REDUCE: dst[i] += sum_r src[r*n + i], then the replicas are re-zeroed for the next step; GF_SUM: the same
+// for rows that are fully overwritten every step, so no re-zeroing) or that equals
+// another gradient (GF_COPY: dst[i] = src[i], e.g. a residual conv's bias grad == its BN's beta grad).
+enum GradFinishMode { GF_REDUCE = 0, GF_COPY = 1, GF_SUM = 2 };   // GF_SUM: like GF_REDUCE, rows not re-zeroed
+struct GradFinish {
+  float* src;
+  float* dst;
+  int n, replicas, mode;   // n % 4 == 0, src / dst 16-byte aligned
+  int work_begin;          // first work item (set by grad_finish_work)
+};
+int grad_finish_work(GradFinish* h_entries, int n_entries);   // fills work_begin, returns the grid size
+int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipStream_t st);
+// zero_spans: ONE launch zeroing a list of 16-byte aligned spans (the per-step gradient / statistics buffers)
+struct ZeroSpan {
+  void* p;
+  int64_t bytes;           // multiple of 16
+};
+int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st);
+
+// launch-shape tuning knobs (0 = built-in heuristic), set from Python for micro-benchmark sweeps
+enum TuneKey {
+  TUNE_NODE_BWD_BLOCKS = 0, TUNE_DW_WGRAD_BLOCKS = 1, TUNE_ENTRY_WGRAD_BLOCKS = 2,
+  TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 384)
+  TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 4)
+  TUNE_N = 16
+};
+int cfl_tune(int key);
+void cfl_set_tune(int key, int value);
 
 // ---------------------------------------------------------------- misc (optim.hip / datagen.hip)
 int fill_f32(float* p, float v, int64_t n, hipStream_t st);

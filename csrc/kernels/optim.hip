@@ -92,7 +92,97 @@ __global__ void gather_rows_kernel(const uint8_t* src, const int32_t* idx, uint8
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < row_bytes; i += (int64_t)gridDim.x * NT) d[i] = s[i];
 }
 
+// One block per work item = (entry, 1024-float element tile, group of GF_ROWS rows): the rows are loaded as 16
+// independent float4 loads per thread (memory-level parallelism over a long row list), summed, and added to the
+// destination - plainly when the entry has a single row group, else with one atomic per element per group.
+constexpr int GF_ROWS = 16;
+
+__global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __restrict__ e, int n_entries) {
+  // entry of this block: entries are sorted by work_begin; count how many begin at or before blockIdx.x
+  const int wb = threadIdx.x < n_entries ? e[threadIdx.x].work_begin : 0x7fffffff;
+  const int k = __syncthreads_count(wb <= (int)blockIdx.x) - 1;
+  const GradFinish g = e[k];
+  const int rows = g.mode == GF_COPY ? 1 : g.replicas;
+  const int ngroups = (rows + GF_ROWS - 1) / GF_ROWS;
+  const int local = blockIdx.x - g.work_begin;
+  const int tile = local / ngroups, rg = local - tile * ngroups;
+  const int i4 = tile * NT + threadIdx.x;
+  const int n4 = g.n >> 2;
+  if (i4 >= n4) return;
+  float4* src = reinterpret_cast<float4*>(g.src);
+  float4* dst = reinterpret_cast<float4*>(g.dst);
+  if (g.mode == GF_COPY) {
+    dst[i4] = src[i4];
+    return;
+  }
+  const int r0 = rg * GF_ROWS;
+  float4 v[GF_ROWS];
+#pragma unroll
+  for (int r = 0; r < GF_ROWS; ++r)
+    v[r] = r0 + r < rows ? src[(size_t)(r0 + r) * n4 + i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < GF_ROWS; ++r) {
+    s.x += v[r].x; s.y += v[r].y; s.z += v[r].z; s.w += v[r].w;
+  }
+  if (g.mode == GF_REDUCE) {        // atomic replica rows: re-zero for the next step
+#pragma unroll
+    for (int r = 0; r < GF_ROWS; ++r)
+      if (r0 + r < rows) src[(size_t)(r0 + r) * n4 + i4] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (ngroups == 1) {
+    float4 d = dst[i4];
+    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
+    dst[i4] = d;
+  } else {
+    float* d = g.dst + 4 * (size_t)i4;
+    atomicAdd(d, s.x); atomicAdd(d + 1, s.y); atomicAdd(d + 2, s.z); atomicAdd(d + 3, s.w);
+  }
+}
+
+__global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans) {
+  const ZeroSpan z = spans[blockIdx.y];
+  uint4* p = reinterpret_cast<uint4*>(z.p);
+  const int64_t n = z.bytes >> 4;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    p[i] = make_uint4(0, 0, 0, 0);
+}
+
+int g_tune[TUNE_N] = {0};
+
 }  // namespace
+
+int cfl_tune(int key) { return key >= 0 && key < TUNE_N ? g_tune[key] : 0; }
+void cfl_set_tune(int key, int value) {
+  if (key >= 0 && key < TUNE_N) g_tune[key] = value;
+}
+
+int grad_finish_work(GradFinish* h_entries, int n_entries) {
+  int w = 0;
+  for (int i = 0; i < n_entries; ++i) {
+    GradFinish& g = h_entries[i];
+    const int rows = g.mode == GF_COPY ? 1 : g.replicas;
+    g.work_begin = w;
+    w += ((g.n / 4 + NT - 1) / NT) * ((rows + GF_ROWS - 1) / GF_ROWS);
+  }
+  return w;
+}
+
+int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipStream_t st) {
+  if (n_entries <= 0 || total_work <= 0) return 0;
+  if (n_entries > NT) return 1;
+  hipLaunchKernelGGL(grad_finish_kernel, dim3(total_work), dim3(NT), 0, st, d_entries, n_entries);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st) {
+  if (n_spans <= 0) return 0;
+  int64_t bx = (max_bytes / 16 + NT - 1) / NT;
+  if (bx > 1024) bx = 1024;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 int adam_update(const AdamParams& p, hipStream_t st) {
   if (p.n % 4) return 1;

@@ -164,6 +164,29 @@ def test_depthwise_fwd_dgrad_wgrad():
     dw = torch.zeros(9 * C, device=DEV)
     C_.dw_wgrad(xb, dyb, dw, ab.to(DEV), 1, B, H, H, C)
     assert rel(dw.view(3, 3, C, 1).cpu(), w.grad) < 1e-2
+    # replica rows + one grad_finish launch (reduce into dst, re-zero the replicas; plus a GF_COPY entry)
+    R = 4
+    slab = torch.zeros(R * 9 * C, device=DEV)
+    C_.dw_wgrad(xb, dyb, slab, ab.to(DEV), 1, B, H, H, C, R)
+    dst = torch.ones(9 * C, device=DEV)
+    src2, dst2 = torch.randn(C, device=DEV), torch.zeros(C, device=DEV)
+    table, work = C_.make_grad_finish_table([(slab, dst, 9 * C, R, C_.GF_REDUCE), (src2, dst2, C, 1, C_.GF_COPY)])
+    C_.grad_finish(table, 2, work)
+    assert rel((dst - 1).cpu(), dw.cpu()) < 1e-5
+    assert float(slab.abs().max()) == 0.0
+    assert torch.equal(dst2, src2)
+
+
+def test_zero_spans():
+    C_ = hip()
+    a = torch.randn(1000, device=DEV)
+    m = torch.ones(8, dtype=torch.float64, device=DEV)
+    b = torch.randn(4096 * 33, device=DEV)
+    table = C_.make_zero_table([a[:992], m[4:8], b])
+    C_.zero_spans(table, 3, b.numel() * 4)
+    assert float(a[:992].abs().max()) == 0.0 and float(a[992:].abs().min()) > 0.0
+    assert m.tolist() == [1, 1, 1, 1, 0, 0, 0, 0]
+    assert float(b.abs().max()) == 0.0
 
 
 def test_datagen_matches_numpy():
@@ -334,3 +357,88 @@ def test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab):
         xin = R.upsample2(xin)
     ref = R.convt_same(xin, wk.to(torch.bfloat16).float(), bias.cpu()).permute(0, 2, 3, 1)
     assert rel(yt, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,dst_mode", [
+    (2, 8, 64, 32, 0, True, 1),      # a decoder ConvT shape, N=32 tile
+    (3, 6, 32, 64, 1, True, 1),      # upsampled input, 12x12 output (ragged 8x16 tiles)
+    (2, 20, 96, 128, 0, False, 0),   # Keras HWIO layout, ragged rows and columns, 3 channel chunks
+])
+def test_conv3x3_halo_wgrad_matches_generic_and_autograd(B, Hs, Cin, N, up, use_ab, dst_mode):
+    torch.manual_seed(13)
+    Ho = Hs * (2 if up else 1)
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, N))
+    ab, a, b = ab_for(Cin, 14)
+    outs = []
+    for algo in (1, 0):
+        dw = torch.zeros(9 * Cin * N, device=DEV)
+        hip().conv_wgrad(xb, dyb, dw, ab.to(DEV) if use_ab else None, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1,
+                         dst_mode, 0, algo)
+        outs.append(dw.cpu())
+    assert rel(outs[1], outs[0]) < 2e-3
+    t = (xf * a + b) if use_ab else xf
+    xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    if dst_mode == 1:
+        w = torch.zeros(3, 3, N, Cin, requires_grad=True)
+        out = R.convt_same(xin, w, None)
+    else:
+        w = torch.zeros(3, 3, Cin, N, requires_grad=True)
+        out = R.conv2d_same(xin, w, None, 1)
+    (out.permute(0, 2, 3, 1) * dyf).sum().backward()
+    assert rel(outs[1].view(w.shape), w.grad) < 1e-2
+
+
+@pytest.mark.parametrize("ks,stride,up,Cin,N,H", [(3, 1, 0, 64, 64, 16), (3, 1, 1, 32, 32, 8), (1, 1, 0, 32, 64, 8),
+                                                  (1, 2, 0, 64, 32, 16), (3, 1, 0, 32, 32, 128)])
+def test_conv_wgrad_slab_rows_sum_to_direct(ks, stride, up, Cin, N, H):
+    """Slab mode (engine path): the rows grad_finish sums equal the direct atomic result."""
+    torch.manual_seed(17)
+    C_ = hip()
+    B = 2
+    pad = 1 if ks == 3 else 0
+    Ho = H // 2 if stride == 2 else H * (2 if up else 1)
+    xb, _ = bf(torch.randn(B, H, H, Cin))
+    dyb, _ = bf(torch.randn(B, Ho, Ho, N))
+    ab, _, _ = ab_for(Cin, 3)
+    K = ks * ks * Cin
+    dst_mode = 1 if ks == 3 else 0
+    direct = torch.zeros(K * N, device=DEV)
+    C_.conv_wgrad(xb, dyb, direct, ab.to(DEV), 1, B, H, H, Cin, up, Ho, Ho, N, ks, stride, pad, pad, dst_mode, 0)
+    rows, plain = C_.conv_wgrad_slabs(B, H, H, Cin, up, Ho, Ho, N, ks, stride, pad, pad)
+    assert plain == (ks == 3)
+    slab = torch.full((rows * K * N,), float("nan") if plain else 0.0, device=DEV)   # plain rows overwrite all
+    C_.conv_wgrad(xb, dyb, slab, ab.to(DEV), 1, B, H, H, Cin, up, Ho, Ho, N, ks, stride, pad, pad, dst_mode, 0, 0,
+                  rows)
+    dst = torch.zeros(K * N, device=DEV)
+    table, work = C_.make_grad_finish_table([(slab, dst, K * N, rows, C_.GF_SUM if plain else C_.GF_REDUCE)])
+    C_.grad_finish(table, 1, work)
+    assert rel(dst.cpu(), direct.cpu()) < 1e-5
+    with pytest.raises(RuntimeError):
+        C_.conv_wgrad(xb, dyb, slab, ab.to(DEV), 1, B, H, H, Cin, up, Ho, Ho, N, ks, stride, pad, pad, dst_mode, 0,
+                      0, rows + 1)
+
+
+def test_node_bwd_sum_replicas_feed_bn_bwd_apply():
+    torch.manual_seed(19)
+    C_ = hip()
+    B, H, C = 2, 16, 64
+    yb, _ = bf(torch.randn(B, H, H, C))
+    gb, _ = bf(torch.randn(B, H, H, C))
+    ab, _, _ = ab_for(C, 5)
+    ab[3 * C:] = torch.rand(C) + 0.5
+    ab[2 * C:3 * C] = torch.randn(C) * 0.1
+    outs = []
+    for reps in (1, 16):
+        g = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
+        sums = torch.zeros(reps * 2 * C, device=DEV)
+        C_.node_bwd(gb, 1, 0, None, 0, 0, None, yb, ab.to(DEV), 1, g, sums, B, H, H, C, reps)
+        dy = torch.zeros_like(g)
+        dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        C_.bn_bwd_apply(g, yb, ab.to(DEV), sums, dy, dgam, dbet, B * H * H, C, reps)
+        outs.append((from_bits(dy), dgam.cpu(), dbet.cpu()))
+    assert rel(outs[1][0], outs[0][0]) < 1e-3
+    assert torch.allclose(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-3)
+    assert torch.allclose(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)

@@ -1,0 +1,119 @@
+"""Per-op micro-benchmark of the HIP engine at the bench shapes.
+
+Records every extension call made by one eager training step (exact shapes and buffers), then replays each call in
+isolation N times between CUDA events. Replays only rewrite the op's own outputs (gradient atomics just keep
+accumulating), so the numbers are pure kernel time at the real shapes. Variants (e.g. the weight-gradient algo)
+are timed side by side.
+
+    python tools/kbench.py [--img 256] [--batch 16] [--reps 20] [--ops conv_wgrad,node_bwd] [--variants]
+"""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device  # noqa: E402
+from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine  # noqa: E402
+from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  # noqa: E402
+
+SKIP = {"conv_splits", "conv_wgrad_slabs", "make_pack_table", "make_bn_moving_table", "make_grad_finish_table",
+        "make_zero_table", "adam_step_done"}
+
+
+class Recorder:
+    def __init__(self, C):
+        self._C = C
+        self.calls = []
+
+    def __getattr__(self, name):
+        f = getattr(self._C, name)
+        if not callable(f) or name in SKIP:
+            return f
+
+        def wrap(*a, **k):
+            self.calls.append((name, a, k))
+            return f(*a, **k)
+        return wrap
+
+
+def shape_key(name, a, k):
+    ints = [x for x in a if isinstance(x, int) and not isinstance(x, bool)]
+    return f"{name}{tuple(ints)}"
+
+
+def time_call(C, name, a, k, reps):
+    f = getattr(C, name)
+    f(*a, **k)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        f(*a, **k)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--img", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ops", default="")
+    ap.add_argument("--variants", action="store_true", help="also time algo variants of conv_wgrad / conv_igemm")
+    ap.add_argument("--tune", default="", help="launch knobs, e.g. 3=256,4=2 (see TuneKey in launch.h)")
+    ap.add_argument("--quiet", action="store_true", help="totals only")
+    args = ap.parse_args()
+    from crack_detection_federatedlearning_grpc_amd._native_loader import hip
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        hip().set_tune(int(k), int(v))
+    table = ParamTable()
+    data = make_synthetic_device(64, args.img, seed=0)
+    eng = UNetEngine(table, args.batch, args.img)
+    eng.bind_data(data.images, data.masks)
+    eng.set_flat(table.init_flat(0))
+    eng.idx.copy_(torch.arange(args.batch, dtype=torch.int32, device=eng.dev))
+    eng.train_step_eager()
+    torch.cuda.synchronize()
+    rec = Recorder(eng.C)
+    C = eng.C
+    eng.C = rec
+    eng.train_step_eager()
+    eng.C = C
+    torch.cuda.synchronize()
+    want = set(args.ops.split(",")) if args.ops else None
+    tot = defaultdict(float)
+    n = defaultdict(int)
+    print(f"{'us':>8}  op(shape ints)")
+    for name, a, k in rec.calls:
+        if want and name not in want:
+            continue
+        t = time_call(C, name, a, k, args.reps)
+        tot[name] += t
+        n[name] += 1
+        line = f"{t:8.1f}  {shape_key(name, a, k)}"
+        if args.variants and name in ("conv_wgrad", "conv_igemm"):
+            for algo in (1, 0):
+                a2, kk = list(a), dict(k)
+                if name == "conv_wgrad":      # (..., dst_mode, m_chunk, algo, slabs): direct atomics variant
+                    a2[-2], a2[-1] = algo, 0
+                else:
+                    kk["algo"] = algo
+                try:
+                    line += f"  algo{algo}={time_call(C, name, a2, kk, args.reps):.1f}"
+                except Exception as ex:  # noqa: BLE001 - unsupported variant for this shape
+                    line += f"  algo{algo}=n/a({str(ex)[:30]})"
+        if not args.quiet:
+            print(line, flush=True)
+    print("\nper-op totals (us per step):")
+    for name in sorted(tot, key=lambda x: -tot[x]):
+        print(f"{tot[name]:9.1f}  {n[name]:3d} calls  {name}")
+    print(f"{sum(tot.values()):9.1f}  total")
+
+
+if __name__ == "__main__":
+    main()
