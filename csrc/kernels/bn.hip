@@ -188,12 +188,28 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
   const float invM = 1.f / (float)p.M;
   const int total = p.M << lg;
   // sum the node_bwd replica rows [reps][2][C] once per block (L2-resident, 2*C*reps floats)
-  // (all threads load in parallel: thread -> (element, replica subset), combined with LDS atomics)
+  // (all threads load in parallel: thread -> (element, replica subset), partials combined through LDS)
+  __shared__ float part[NT];
   const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
-  const int C2 = 2 * p.C;
-  for (int e = threadIdx.x; e < C2; e += NT) ssum[e] = 0.f;
-  __syncthreads();
-  for (int q = threadIdx.x; q < C2 * reps; q += NT) atomicAdd(&ssum[q % C2], p.sums[q]);
+  const int C2 = 2 * p.C;                                  // power of two (C / 8 is)
+  if (C2 <= NT) {
+    const int per = NT / C2, e = threadIdx.x & (C2 - 1), j = threadIdx.x / C2;
+    float v = 0.f;
+    for (int r = j; r < reps; r += per) v += p.sums[(size_t)r * C2 + e];
+    part[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x < C2) {
+      float t = 0.f;
+      for (int k = 0; k < per; ++k) t += part[k * C2 + threadIdx.x];
+      ssum[threadIdx.x] = t;
+    }
+  } else {
+    for (int e = threadIdx.x; e < C2; e += NT) {
+      float v = 0.f;
+      for (int r = 0; r < reps; ++r) v += p.sums[(size_t)r * C2 + e];
+      ssum[e] = v;
+    }
+  }
   __syncthreads();
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < p.C; c += NT) {

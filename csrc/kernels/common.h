@@ -67,6 +67,22 @@ CFL_DEVICE void load_f8_or(const float* p, bool cond, float dflt, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+// XCD-aware block order. Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), and each
+// XCD has its own L2: blocks that share input rows (halo tiles, neighbouring rows, the N-blocks of one M-tile)
+// should sit on the same XCD. This maps the dispatch index to a logical index such that every XCD receives one
+// contiguous range of logical indices (a bijection on [0, n)).
+CFL_DEVICE int xcd_swizzle(int b, int n) {
+  const int q = n >> 3, r = n & 7;
+  const int x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+// logical linear block index of a 3-D grid under xcd_swizzle
+CFL_DEVICE int xcd_block_linear() {
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  return xcd_swizzle(lin, gridDim.x * gridDim.y * gridDim.z);
+}
+
 CFL_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -44,13 +44,18 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_w = (p.Wo + TW - 1) / TW, tiles_h = (p.Ho + TH - 1) / TH;
-  int t = blockIdx.x;
+  // logical block (XCD-aware): the N-blocks and K-splits of one pixel tile, and neighbouring tiles, share an XCD
+  const int lin = xcd_block_linear();
+  const int bn_idx = lin % gridDim.y, rest = lin / gridDim.y;
+  const int bz = rest % gridDim.z;
+  int t = rest / gridDim.z;
+  const int tile_id = t;
   const int b = t / (tiles_w * tiles_h);
   t -= b * tiles_w * tiles_h;
   const int ty0 = (t / tiles_w) * TH, tx0 = (t % tiles_w) * TW;
-  const int nBlock = blockIdx.y * BN_;
+  const int nBlock = bn_idx * BN_;
   const int chunks = p.Cin / BK;
-  const int ch0 = blockIdx.z * chunks_per_split;
+  const int ch0 = bz * chunks_per_split;
   const int ch1 = imin(chunks, ch0 + chunks_per_split);
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
   const bool has_ab = p.xf.ab != nullptr;
@@ -62,10 +67,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
     const int cbase = chunk * BK;
     // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
     float a8[8], b8[8];
-    if (has_ab) {
-      load_f8(p.xf.ab + cbase + (tid & 3) * 8, a8);
-      load_f8(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, b8);
-    }
+    load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
+    load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
@@ -110,7 +113,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < B_CHUNKS) rb[i] = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (e >> 2)) * p.K + kofs + (e & 3) * 8);
+      uint4 v = make_uint4(0, 0, 0, 0);   // unconditional register write: a conditionally written array goes to scratch
+      if (B_CHUNKS % NT == 0 || e < B_CHUNKS)
+        v = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (e >> 2)) * p.K + kofs + (e & 3) * 8);
+      rb[i] = v;
     }
   };
   auto store_b = [&](int buf) {
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   };
 
   if (ws != nullptr) {                    // split-K partials
-    float* dst = ws + (size_t)blockIdx.z * p.M * p.N;
+    float* dst = ws + (size_t)bz * p.M * p.N;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
     }
     __syncthreads();
-    float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+    float* rep = p.stats + (size_t)(tile_id % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);

@@ -49,10 +49,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
   const bool has_ab = p.xf.ab != nullptr;
   float a8[8], b8[8];
-  if (has_ab) {
-    load_f8(p.xf.ab + cbase + (tid & 3) * 8, a8);
-    load_f8(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, b8);
-  }
+  load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
+  load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
 
   uint4 rh[H_PER_T], rd[D_PER_T];
   auto load = [&](int t) {
@@ -201,7 +199,7 @@ static void wgrad3_shape(const WgradParams& p, int& bno, int& tiles, int& splits
   bno = p.N % 64 == 0 ? 64 : 32;
   tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   const int xy = (p.Cin / CB) * (p.N / bno);
-  const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 384;
+  const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 512;
   const int min_tiles = cfl_tune(TUNE_WGRAD3_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_MINTILES) : 4;
   splits = (target + xy - 1) / xy;
   const int max_splits = (tiles + min_tiles - 1) / min_tiles;   // amortise each block's output write

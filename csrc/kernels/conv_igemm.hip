@@ -118,10 +118,12 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int ch = tid + i * NT;
-      if (ch < B_CHUNKS) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (B_CHUNKS % NT == 0 || ch < B_CHUNKS) {
         const int n = ch >> 2, q = ch & 3;
-        rb[i] = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + n) * p.K + kt * BK + q * 8);
+        v = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + n) * p.K + kt * BK + q * 8);
       }
+      rb[i] = v;
     }
     // advance (tap, channel) to the next K-step
     c += BK;
@@ -327,8 +329,9 @@ static bool use3x3(const ConvParams& p) { return p.algo != 1 && conv3x3_supporte
 int conv_igemm_splits(const ConvParams& p) {
   if (use3x3(p)) return conv3x3_splits(p);
   const int KT = p.K / BK;
-  const int bm = (p.N <= 64 && p.M >= 256 * 512) ? 256 : 128;
-  const int bn = p.N >= 128 ? 128 : p.N;
+  const bool t128 = p.N % 128 == 0 && p.M >= 65536;
+  const int bm = t128 ? 128 : p.N % 64 == 0 ? 64 : 128;
+  const int bn = t128 ? 128 : p.N % 64 == 0 ? 64 : 32;
   const int blocks = ((p.M + bm - 1) / bm) * (p.N / bn);
   if (blocks >= 192 || KT < 16) return 1;
   int s = (384 + blocks - 1) / blocks;
@@ -353,12 +356,22 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.algo == 2) return 4;
   int splits = conv_igemm_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
-  const bool big_m = p.M >= 256 * 512;
-  if (p.N % 128 == 0) launch<128, 128, 2, 2>(p, splits, p.ws, st);
-  else if (p.N == 64 && big_m) launch<256, 64, 4, 1>(p, splits, p.ws, st);
-  else if (p.N == 64) launch<128, 64, 2, 2>(p, splits, p.ws, st);
-  else if (p.N == 32 && big_m) launch<256, 32, 4, 1>(p, splits, p.ws, st);
-  else if (p.N == 32) launch<128, 32, 4, 1>(p, splits, p.ws, st);
+  const int cfg = cfl_tune(TUNE_IGEMM_CFG);
+  if (cfg > 0) {                           // forced tile (micro-benchmark sweeps); must divide N
+    const int bn = cfg == 1 || cfg == 6 ? 128 : cfg == 2 || cfg == 3 || cfg == 7 ? 64 : 32;
+    if (p.N % bn) return 2;
+    switch (cfg) {
+      case 1: launch<128, 128, 2, 2>(p, splits, p.ws, st); break;
+      case 2: launch<256, 64, 4, 1>(p, splits, p.ws, st); break;
+      case 3: launch<128, 64, 2, 2>(p, splits, p.ws, st); break;
+      case 4: launch<256, 32, 4, 1>(p, splits, p.ws, st); break;
+      case 5: launch<128, 32, 4, 1>(p, splits, p.ws, st); break;
+      case 6: launch<64, 128, 1, 4>(p, splits, p.ws, st); break;
+      default: launch<64, 64, 2, 2>(p, splits, p.ws, st); break;
+    }
+  } else if (p.N % 128 == 0 && p.M >= 65536) launch<128, 128, 2, 2>(p, splits, p.ws, st);
+  else if (p.N % 64 == 0) launch<64, 64, 2, 2>(p, splits, p.ws, st);     // (measured: tools/kbench.py sweeps)
+  else if (p.N % 32 == 0) launch<128, 32, 4, 1>(p, splits, p.ws, st);
   else return 2;
   if (splits > 1) {
     const int G = p.N / 8, lanes = NT / G;

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(NT) void dw_conv_kernel(const bf16_t* __restrict__ 
   float wt[9][8];
   load_w9(w, C, c0, wt, flip != 0);
   const int rows = B * H, items = (W / SW) << lg;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  for (int row = xcd_swizzle(blockIdx.x, gridDim.x); row < rows; row += gridDim.x) {   // halo rows on one XCD
     const int b = row / H, h = row - b * H;
     for (int it = threadIdx.x; it < items; it += NT) {
       const int w0 = (it >> lg) * SW;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) 
   // flat items (row, strip, channel group): every thread gets work whatever the row width
   const int strips = p.W / SW;
   const int total = (p.B * p.H * strips) << lg;
-  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += gridDim.x * NT) {
+  for (int it = xcd_swizzle(blockIdx.x, gridDim.x) * NT + threadIdx.x; it < total; it += gridDim.x * NT) {
     const int pix = it >> lg;                       // row * strips + strip
     const int row = pix / strips;
     const int w0 = (pix - row * strips) * SW;

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(NT) void pool_res_kernel(PoolResParams p) {
   load_f8(p.ab + c0, a);
   load_f8(p.ab + p.C + c0, bb);
   const int rows = p.B * p.Ho, items = p.Wo << lg;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  for (int row = xcd_swizzle(blockIdx.x, gridDim.x); row < rows; row += gridDim.x) {
     const int b = row / p.Ho, oh = row - b * p.Ho;
     for (int it = threadIdx.x; it < items; it += NT) {
       const int ow = it >> lg;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(BnAddParams p) {
   load_f8(p.ab + p.C + c0, bb);
   const int Hq = p.q_up ? p.H >> 1 : p.H, Wq = p.q_up ? p.W >> 1 : p.W;
   const int rows = p.B * p.H, items = p.W << lg;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  for (int row = xcd_swizzle(blockIdx.x, gridDim.x); row < rows; row += gridDim.x) {
     const int b = row / p.H, h = row - b * p.H;
     const int qrow = p.q_up ? b * Hq + (h >> 1) : row;
     for (int it = threadIdx.x; it < items; it += NT) {
