@@ -568,6 +568,10 @@ class HipBackend:
     def reset_optimizer(self):
         self.eng.reset_optimizer()
 
+    def optimizer_state(self):
+        e = self.eng
+        return int(e.step_t.item()), e.m.cpu().numpy().copy(), e.v.cpu().numpy().copy()
+
     def train_batches(self, batches: np.ndarray) -> Dict[str, float]:
         e = self.eng
         dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)

@@ -78,6 +78,10 @@ class RefBackend:
     def reset_optimizer(self):
         self.tr.reset_optimizer()
 
+    def optimizer_state(self):
+        o = self.tr.opt
+        return o.t, o.m.detach().cpu().numpy().copy(), o.v.detach().cpu().numpy().copy()
+
     def train_batches(self, batches):
         ls, acc = [], []
         for ids in batches:
