@@ -108,7 +108,8 @@ def unet_forward(flat: torch.Tensor, x_nhwc: torch.Tensor, table: Optional[Param
 
     def sep(x, s):
         c = x.shape[1]
-        d = r(F.conv2d(F.pad(x, (1, 1, 1, 1)), P(s, "depthwise_kernel").permute(2, 3, 0, 1), None, groups=c))
+        # the depthwise kernels stage the transformed (BN-apply + ReLU) input in LDS as bf16
+        d = r(F.conv2d(F.pad(r(x), (1, 1, 1, 1)), P(s, "depthwise_kernel").permute(2, 3, 0, 1), None, groups=c))
         return r(F.conv2d(d, r(P(s, "pointwise_kernel")).permute(3, 2, 0, 1), P(s, "bias")))
 
     names = iter([ly.name for ly in table.weighted_layers()])

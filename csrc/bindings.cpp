@@ -114,8 +114,9 @@ DwParams dwp(int B, int H, int W, int C) {
   return p;
 }
 
-void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int B, int H, int W, int C) {
+void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int B, int H, int W, int C, int algo) {
   DwParams p = dwp(B, H, W, C);
+  p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
   p.w = ptr<const float>(w, "w");
   p.y = ptr<bf16_t>(y, "y");
@@ -124,8 +125,9 @@ void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int 
   ok(dw_fwd(p, stream()), "dw_fwd");
 }
 
-void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W, int C) {
+void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W, int C, int algo) {
   DwParams p = dwp(B, H, W, C);
+  p.algo = algo;
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.w = ptr<const float>(w, "w");
   p.y = ptr<bf16_t>(dx, "dx");
@@ -134,8 +136,9 @@ void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W
 }
 
 void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C,
-                 int replicas) {
+                 int replicas, int algo) {
   DwParams p = dwp(B, H, W, C);
+  p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.dw = ptr<float>(dw, "dw");
@@ -433,10 +436,12 @@ PYBIND11_MODULE(_C, m) {
   m.attr("GF_SUM") = (int)GF_SUM;
   m.attr("TUNE_WGRAD3_BLOCKS") = (int)TUNE_WGRAD3_BLOCKS;
   m.attr("TUNE_WGRAD3_MINTILES") = (int)TUNE_WGRAD3_MINTILES;
-  m.def("dw_fwd", &dw_fwd_op);
-  m.def("dw_dgrad", &dw_dgrad_op);
+  m.def("dw_fwd", &dw_fwd_op, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("ab"), py::arg("relu"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("C"), py::arg("algo") = 0);
+  m.def("dw_dgrad", &dw_dgrad_op, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("B"), py::arg("H"),
+        py::arg("W"), py::arg("C"), py::arg("algo") = 0);
   m.def("dw_wgrad", &dw_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
-        py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1);
+        py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1, py::arg("algo") = 0);
   m.def("entry_fwd", &entry_fwd_op);
   m.def("entry_wgrad", &entry_wgrad_op, py::arg("images"), py::arg("idx"), py::arg("dy"), py::arg("dw"), py::arg("B"),
         py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1);

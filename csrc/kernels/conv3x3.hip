@@ -23,7 +23,10 @@ constexpr int BK = 32;          // channels per chunk (one K-step = one tap of o
 constexpr int LDH = BK + 8;     // halo pixel stride (bf16)
 constexpr int LDB = BK + 8;
 
-template <int TH, int TW, int BN_, int WM, int WN>
+// WB ("whole-chunk B"): the block stages all 9 taps' weight tiles of a chunk at once ([tap][n][LDB], single LDS
+// buffer, next chunk register-prefetched during the current chunk's 9 x FMxFN MFMAs): two barriers per CHUNK
+// instead of one per tap, and no per-tap global-load latency on the critical path. Used for BN <= 64.
+template <int TH, int TW, int BN_, int WM, int WN, bool WB>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
@@ -31,7 +34,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   constexpr int HALO_CHUNKS = HP * (BK / 8);                      // 16-byte pieces per halo tile
   constexpr int H_PER_T = (HALO_CHUNKS + NT - 1) / NT;
   constexpr int B_CHUNKS = BN_ * BK / 8, B_PER_T = (B_CHUNKS + NT - 1) / NT;
-  constexpr int SH = 2 * HP * LDH, SB = 2 * BN_ * LDB;
+  constexpr int BW_CHUNKS = 9 * B_CHUNKS, BW_PER_T = WB ? (BW_CHUNKS + NT - 1) / NT : 1;
+  constexpr int SH = (WB ? 1 : 2) * HP * LDH, SB = (WB ? 9 : 2) * BN_ * LDB;
   constexpr int LDC = BN_ + 8;
   static_assert(BM * LDC <= SH + SB, "C staging tile must fit");
   static_assert(WM * WN == 4 && TM % 16 == 0 && TN % 16 == 0, "wave tiling");
@@ -127,6 +131,32 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
     }
   };
 
+  // ---- whole-chunk weight tiles (WB): piece e -> tap e / B_CHUNKS, row n, 16-byte quarter q ----
+  uint4 rbw[BW_PER_T];
+  auto load_bw = [&](int chunk) {
+#pragma unroll
+    for (int i = 0; i < BW_PER_T; ++i) {
+      const int e = tid + i * NT;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (BW_CHUNKS % NT == 0 || e < BW_CHUNKS) {
+        const int tap = e / B_CHUNKS, w = e - tap * B_CHUNKS;
+        v = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (w >> 2)) * p.K + (size_t)tap * p.Cin +
+                                            chunk * BK + (w & 3) * 8);
+      }
+      rbw[i] = v;
+    }
+  };
+  auto store_bw = [&]() {
+#pragma unroll
+    for (int i = 0; i < BW_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (BW_CHUNKS % NT == 0 || e < BW_CHUNKS) {
+        const int tap = e / B_CHUNKS, w = e - tap * B_CHUNKS;
+        *reinterpret_cast<uint4*>(sB + ((size_t)tap * BN_ + (w >> 2)) * LDB + (w & 3) * 8) = rbw[i];
+      }
+    }
+  };
+
   // per-lane fragment pixel coordinates within the tile
   int fpy[FM], fpx[FM];
 #pragma unroll
@@ -143,6 +173,44 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (WB) {
+    if (ch0 < ch1) {
+      load_halo(ch0);
+      load_bw(ch0);
+      store_halo(0);
+      store_bw();
+    }
+    __syncthreads();
+    for (int ch = ch0; ch < ch1; ++ch) {
+      const bool next_chunk = ch + 1 < ch1;
+      if (next_chunk) {                                      // in flight during this chunk's 9 taps
+        load_halo(ch + 1);
+        load_bw(ch + 1);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        s8v af[FM], bfg[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = *reinterpret_cast<const s8v*>(sH + ((size_t)(fpy[i] + ky) * HW + fpx[i] + kx) * LDH + fk);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bfg[j] = *reinterpret_cast<const s8v*>(sB + ((size_t)tap * BN_ + wn * TN + j * 16 + (lane & 15)) * LDB + fk);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+      if (next_chunk) {
+        store_halo(0);
+        store_bw();
+        __syncthreads();
+      }
+    }
+  } else {
   if (ch0 < ch1) {
     load_halo(ch0);
     store_halo(0);
@@ -180,6 +248,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       __syncthreads();
       bbuf ^= 1;
     }
+  }
   }
 
   // pixel index of accumulator row r of fragment i -> (m valid?, global m)
@@ -261,23 +330,29 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   }
 }
 
-template <int TH, int TW, int BN_, int WM, int WN>
+template <int TH, int TW, int BN_, int WM, int WN, bool WB = false>
 int launch(const ConvParams& p, int splits, hipStream_t st) {
   const int chunks = p.Cin / BK;
   const int per = (chunks + splits - 1) / splits;
   splits = (chunks + per - 1) / per;
   const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   dim3 grid(tiles, p.N / BN_, splits);
-  hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? p.ws : nullptr);
+  hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, WB>), grid, dim3(NT), 0, st, p, per,
+                     splits > 1 ? p.ws : nullptr);
   return splits;
 }
 
 }  // namespace
 
+static bool use_wb(const ConvParams& p) {
+  const int v = cfl_tune(TUNE_CONV3_WB);
+  return v == 0 ? true : v == 1;           // 0 = default (whole-chunk B, BN <= 64), 2 = per-tap B (BN up to 128)
+}
+
 int conv3x3_splits(const ConvParams& p) {
   const int tw = p.Wo >= 16 ? 16 : 8;
   const int th = 128 / tw;
-  const int bn = p.N >= 128 ? 128 : p.N;
+  const int bn = use_wb(p) ? (p.N >= 64 ? 64 : p.N) : (p.N >= 128 ? 128 : p.N);
   const int blocks = ((p.Ho + th - 1) / th) * ((p.Wo + tw - 1) / tw) * p.B * (p.N / bn);
   const int chunks = p.Cin / BK;
   if (blocks >= 192 || chunks < 2) return 1;
@@ -297,7 +372,13 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   int splits = conv3x3_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const bool w16 = p.Wo >= 16;
-  if (p.N % 128 == 0) {
+  if (use_wb(p) && p.N % 64 == 0) {
+    if (w16) splits = launch<8, 16, 64, 2, 2, true>(p, splits, st);
+    else splits = launch<16, 8, 64, 2, 2, true>(p, splits, st);
+  } else if (use_wb(p)) {
+    if (w16) splits = launch<8, 16, 32, 4, 1, true>(p, splits, st);
+    else splits = launch<16, 8, 32, 4, 1, true>(p, splits, st);
+  } else if (p.N % 128 == 0) {
     if (w16) splits = launch<8, 16, 128, 2, 2>(p, splits, st);
     else splits = launch<16, 8, 128, 2, 2>(p, splits, st);
   } else if (p.N == 64) {

@@ -59,6 +59,7 @@ struct DwParams {
   InXform xf;
   int B, H, W, C;
   int replicas;        // wgrad: >1 = spread block atomics over that many copies of the row (summed by grad_finish)
+  int algo;            // 0 auto (C % 32 == 0 -> LDS halo tiles), 1 row-strip kernels
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);
@@ -216,6 +217,7 @@ enum TuneKey {
   TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 512)
   TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 4)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
+  TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
   TUNE_N = 16
 };
 int cfl_tune(int key);

@@ -143,31 +143,32 @@ def test_conv_wgrad_1x1_and_up(stride, up):
     assert rel(dw.view(1, 1, Cin, N).cpu(), w.grad) < 2e-2
 
 
-def test_depthwise_fwd_dgrad_wgrad():
+@pytest.mark.parametrize("B,H,C,algo", [(2, 10, 64, 0), (2, 10, 64, 1), (3, 37, 32, 0), (2, 18, 128, 0),
+                                        (1, 9, 256, 0)])
+def test_depthwise_fwd_dgrad_wgrad(B, H, C, algo):
     torch.manual_seed(6)
-    B, H, C = 2, 10, 64
     xb, xf = bf(torch.randn(B, H, H, C))
     dyb, dyf = bf(torch.randn(B, H, H, C))
     wk = torch.randn(3, 3, C, 1) * 0.2
     ab, a, b = ab_for(C, 7)
     C_ = hip()
     y = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
-    C_.dw_fwd(xb, wk.reshape(-1).to(DEV), y, ab.to(DEV), 1, B, H, H, C)
+    C_.dw_fwd(xb, wk.reshape(-1).to(DEV), y, ab.to(DEV), 1, B, H, H, C, algo)
     t = (xf * a + b).relu().requires_grad_(True)
     w = wk.clone().requires_grad_(True)
     out = F.conv2d(F.pad(t.permute(0, 3, 1, 2), (1, 1, 1, 1)), w.permute(2, 3, 0, 1), None, groups=C)
     assert rel(from_bits(y), out.permute(0, 2, 3, 1).detach()) < 1e-2
     (out.permute(0, 2, 3, 1) * dyf).sum().backward()
     dx = torch.zeros_like(y)
-    C_.dw_dgrad(dyb, wk.reshape(-1).to(DEV), dx, B, H, H, C)
+    C_.dw_dgrad(dyb, wk.reshape(-1).to(DEV), dx, B, H, H, C, algo)
     assert rel(from_bits(dx), t.grad) < 1e-2
     dw = torch.zeros(9 * C, device=DEV)
-    C_.dw_wgrad(xb, dyb, dw, ab.to(DEV), 1, B, H, H, C)
+    C_.dw_wgrad(xb, dyb, dw, ab.to(DEV), 1, B, H, H, C, 1, algo)
     assert rel(dw.view(3, 3, C, 1).cpu(), w.grad) < 1e-2
     # replica rows + one grad_finish launch (reduce into dst, re-zero the replicas; plus a GF_COPY entry)
     R = 4
     slab = torch.zeros(R * 9 * C, device=DEV)
-    C_.dw_wgrad(xb, dyb, slab, ab.to(DEV), 1, B, H, H, C, R)
+    C_.dw_wgrad(xb, dyb, slab, ab.to(DEV), 1, B, H, H, C, R, algo)
     dst = torch.ones(9 * C, device=DEV)
     src2, dst2 = torch.randn(C, device=DEV), torch.zeros(C, device=DEV)
     table, work = C_.make_grad_finish_table([(slab, dst, 9 * C, R, C_.GF_REDUCE), (src2, dst2, C, 1, C_.GF_COPY)])

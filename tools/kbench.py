@@ -100,7 +100,7 @@ def main():
         tot[name] += t
         n[name] += 1
         line = f"{t:8.1f}  {shape_key(name, a, k)}"
-        if args.variants and name in ("conv_wgrad", "conv_igemm"):
+        if args.variants and name in ("conv_wgrad", "conv_igemm", "dw_fwd", "dw_dgrad", "dw_wgrad"):
             for algo in (1, 0):
                 a2, kk = list(a), dict(k)
                 if name == "conv_wgrad":      # (..., dst_mode, m_chunk, algo, slabs): direct atomics variant
