@@ -2,10 +2,12 @@
 
 BASELINE.json metric: "images/sec/node per FL round + wall-clock/round, U-Net 256^2 at 8 clients".
 One benchmark *step* is one FL round, exactly as a client runs it (client_fit_model.py:152-174 + fl_server.py:92-105):
-  fresh Adam state -> ``local_steps`` full training iterations (fwd + bwd + Adam + BN moving stats, batch ``batch``
-  per client, hipGraph replay of the HIP-kernel engine) -> FedAvg: weighted RCCL all-reduce of the whole flat
-  model (all 112 Keras arrays incl. BN moving statistics) across the N clients -> repack weights.
-value = N * local_steps * batch / round_seconds (whole node, training images; weak scaling: per-client work fixed).
+  fresh Adam state -> ``epochs`` x (``local_steps`` full training iterations (fwd + bwd + Adam + BN moving stats,
+  batch ``batch`` per client, hipGraph replay of the HIP-kernel engine) + a validation pass over the held-out split
+  (inference-mode forward, its own hipGraph)) -> FedAvg: weighted RCCL all-reduce of the whole flat model (all 112
+  Keras arrays incl. BN moving statistics) across the N clients -> repack weights.
+value = N * epochs * local_steps * batch / round_seconds (whole node, training images per round wall-clock; the
+validation images are reported separately; weak scaling: per-client work fixed).
 Data: synthetic crack images/masks rendered on the device (per-client shard); weights: Keras-default random init.
 
 Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
@@ -30,7 +32,10 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1, help="untimed FL rounds")
     ap.add_argument("--img", type=int, default=256)
     ap.add_argument("--batch", type=int, default=16, help="per-client batch (reference: 16)")
-    ap.add_argument("--local-steps", type=int, default=388, help="iterations per round (reference epoch: 6213//16)")
+    ap.add_argument("--epochs", type=int, default=10, help="local epochs per FL round (client_fit_model.py:166)")
+    ap.add_argument("--local-steps", type=int, default=388, help="iterations per epoch (reference: 6213 // 16)")
+    ap.add_argument("--val-steps", type=int, default=-1,
+                    help="validation batches per epoch (-1: the whole held-out split, as Keras fit(validation_data))")
     ap.add_argument("--samples", type=int, default=8000, help="synthetic images per client")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
@@ -73,11 +78,19 @@ def main() -> int:
         print(json.dumps({"profile_steps": args.profile_steps, "metrics": eng.read_metrics("train")}))
         return 0
 
+    val_steps = len(data.val_idx) // args.batch if args.val_steps < 0 else args.val_steps
+    vbatches = torch.as_tensor(epoch_batches(data.val_idx, args.batch, 0, 0)[:val_steps], dtype=torch.int32,
+                               device=dev) if val_steps else None
+
     def fl_round() -> None:
         eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
-        for s in range(args.local_steps):
-            eng.idx.copy_(batches[s])
-            eng.train_step(use_graph)
+        for _ep in range(args.epochs):                     # model.fit(epochs=10, validation_data=val_gen)
+            for s in range(args.local_steps):
+                eng.idx.copy_(batches[s])
+                eng.train_step(use_graph)
+            for v in range(val_steps):
+                eng.idx.copy_(vbatches[v])
+                eng.eval_step(use_graph)
         if agg is not None:
             agg.average(float(n_local))                    # weighted FedAvg over RCCL/xGMI
         eng.pack()
@@ -103,7 +116,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     round_s = dt / args.steps
-    imgs_per_round = world * args.local_steps * args.batch
+    imgs_per_round = world * args.epochs * args.local_steps * args.batch
     value = imgs_per_round / round_s
     if rank == 0:
         out = {"metric": "images/sec/node per FL round", "value": round(value, 2), "unit": "images/s",
@@ -111,11 +124,14 @@ def main() -> int:
                "ms_per_step": round(round_s * 1000.0, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-rendered crack masks, random init)",
                "wall_clock_per_round_s": round(round_s, 4),
-               "ms_per_iteration": round(round_s * 1000.0 / args.local_steps, 4),
+               "ms_per_iteration": round(round_s * 1000.0 / (args.epochs * args.local_steps), 4),
+               "val_images_per_round": world * args.epochs * val_steps * args.batch,
+               "peak_hbm_gb_per_client": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",
                           "img_size": args.img, "global_batch": args.batch * world, "per_client_batch": args.batch,
-                          "seq_len": None, "local_steps_per_round": args.local_steps,
+                          "seq_len": None, "epochs_per_round": args.epochs,
+                          "local_steps_per_round": args.epochs * args.local_steps,
                           "parallelism": f"fedavg-dp{world} (1 FL client per GPU, RCCL weighted all-reduce)",
                           "graph": use_graph}}
         print(json.dumps(out), flush=True)

@@ -74,6 +74,8 @@ class UNetEngine:
         self._build_pack()
         self._alloc()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.eval_graph: Optional[torch.cuda.CUDAGraph] = None
+        self._retired: List[torch.Tensor] = []   # replaced workspaces a captured graph may still reference
         self.images: Optional[torch.Tensor] = None
         self.masks: Optional[torch.Tensor] = None
 
@@ -250,6 +252,8 @@ class UNetEngine:
         if slab is None or slab.numel() != rows * n:
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("weight-gradient slabs must be allocated before graph capture")
+            if key in self._wslabs:
+                self._retired.append(self._wslabs[key])
             slab = torch.zeros(rows * n, dtype=torch.float32, device=self.dev)
             self._wslabs[key] = slab
             dst = self.G(*key)
@@ -302,6 +306,7 @@ class UNetEngine:
         if need > 1 and need * B * Ho * Wo * N > self.ws.numel():
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")
+            self._retired.append(self.ws)
             self.ws = torch.empty(need * B * Ho * Wo * N, dtype=torch.float32, device=self.dev)
         self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                           pad_l, self.ws if need > 1 else None)
@@ -512,6 +517,27 @@ class UNetEngine:
         else:
             self.train_step_eager()
 
+    def eval_step(self, use_graph: bool = True) -> None:
+        """Inference-mode forward (moving BN statistics) of the batch in ``idx``; loss / accuracy accumulate into
+        ``eval_metrics``. Replayed from its own hipGraph (captured after an eager warm-up)."""
+        if not use_graph:
+            self.forward(False)
+            return
+        if self.eval_graph is None:
+            s = torch.cuda.Stream(device=self.dev)
+            s.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(s):
+                saved = self.eval_metrics.clone()
+                self.forward(False)
+                self.eval_metrics.copy_(saved)
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            torch.cuda.synchronize(self.dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.forward(False)
+            self.eval_graph = g
+        self.eval_graph.replay()
+
     # ------------------------------------------------------------------------------------------------ state
     def set_flat(self, flat: np.ndarray) -> None:
         self.flat.copy_(torch.as_tensor(np.asarray(flat, np.float32)).to(self.dev))
@@ -590,7 +616,7 @@ class HipBackend:
         e.eval_metrics.zero_()
         for s in range(dev_b.shape[0]):
             e.idx.copy_(dev_b[s])
-            e.forward(False)
+            e.eval_step(self.use_graph)
         return e.read_metrics("eval")
 
     def predict(self, idx: np.ndarray) -> np.ndarray:

@@ -289,6 +289,26 @@ def test_engine_graph_replay_matches_eager_and_learns():
     assert losses[-1] < losses[0]
 
 
+def test_engine_eval_graph_matches_eager_and_reference():
+    table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=4)
+    # give the BN moving statistics non-trivial values first (a few training steps)
+    for _ in range(3):
+        eng.train_step(use_graph=False)
+    eng.eval_metrics.zero_()
+    eng.eval_step(use_graph=False)
+    eager = eng.read_metrics("eval")
+    for _ in range(2):
+        eng.eval_step(use_graph=True)
+    graph = eng.read_metrics("eval")
+    assert abs(graph["loss"] - eager["loss"]) < 1e-6 * max(1.0, abs(eager["loss"]))
+    assert abs(graph["accuracy"] - eager["accuracy"]) < 1e-9
+    # inference-mode oracle (moving statistics) on the same weights
+    p = torch.as_tensor(eng.get_flat())
+    logits, _ = R.unet_forward(p, x, table, training=False, emulate_bf16=True)
+    ref = float(R.bce_with_logits_mean(logits, y))
+    assert abs(eager["loss"] - ref) < 2e-2 * max(1.0, ref)
+
+
 @pytest.mark.parametrize("N", [32, 64])
 def test_conv_igemm_big_m_tiles(N):
     """BM=256 tiles (M >= 131072) used by the 128^2 layers at 256^2 input."""
