@@ -10,6 +10,7 @@ loop { TRAIN_DONE -> RESP_ACY: poll VERSION until NOT_WAIT | RESP_ARY: TRAINING 
 """
 from __future__ import annotations
 
+import json
 import os
 import random
 import sys
@@ -50,6 +51,7 @@ class FLClient:
         self.aggregator = None
         self.trainer: Optional[LocalTrainer] = None
         self.history: List[Dict] = []
+        self.phases: List[Dict] = []
         self.info: Dict[str, object] = {}
         self.final_state = ""
 
@@ -77,6 +79,16 @@ class FLClient:
 
     def _params(self, stub) -> bytes:
         return self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="P"))).update_rep.buffer_chunk
+
+    def _log_phase(self, phase: Dict) -> None:
+        """Per-round phase wall-clock (aggregate = RCCL all-reduce in rccl mode, upload = TRAIN_DONE RPC incl. the
+        server-side FedAvg when this client closes the round, wait = VERSION long-poll until the new global)."""
+        rec = dict(phase, client=self.name, kind="phases")
+        self.phases.append(rec)
+        if self.cfg.metrics_file:
+            os.makedirs(os.path.dirname(os.path.abspath(self.cfg.metrics_file)), exist_ok=True)
+            with open(self.cfg.metrics_file, "a") as f:
+                f.write(json.dumps(rec) + "\n")
 
     def _training(self, stub) -> None:
         self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="T", cname=self.name, state=P.TRAINING)))
@@ -169,13 +181,21 @@ class FLClient:
                 print(f"### Deliver model state: TRAIN DONE to server ### round {cr}")
                 if self.cfg.fault_delay_s:
                     time.sleep(self.cfg.fault_delay_s)
-                rep = self._train_done(stub, cr, self._payload(), getattr(self.trainer, "n_samples", 0))
+                t0 = time.perf_counter()
+                payload = self._payload()                 # RCCL mode: the all-reduce runs here
+                t1 = time.perf_counter()
+                rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0))
+                t2 = time.perf_counter()
+                phase = {"round": cr, "aggregate_s": t1 - t0, "upload_s": t2 - t1, "wait_s": 0.0,
+                         "payload_bytes": len(payload)}
                 st = rep.config["state"].scstring
                 print(f"### Received from state {st} ###")
                 if st == "RESP_ACY":
                     while True:
                         vr = self._version(stub, mv, cr, self.cfg.long_poll_s)
                         if vr.state == P.NOT_WAIT:
+                            phase["wait_s"] = time.perf_counter() - t2
+                            self._log_phase(phase)
                             cr = vr.config["current_round"].scint32
                             mv = vr.config["model_version"].scint32
                             self._apply(vr.buffer_chunk)
@@ -183,6 +203,8 @@ class FLClient:
                             self._train(cr)
                             break
                         if vr.state == P.FIN:
+                            phase["wait_s"] = time.perf_counter() - t2
+                            self._log_phase(phase)
                             cr = vr.config["current_round"].scint32
                             mv = vr.config["model_version"].scint32
                             self.final_state = "FIN"
@@ -192,12 +214,14 @@ class FLClient:
                     if self.final_state == "FIN":
                         break
                 elif st == "RESP_ARY":
+                    self._log_phase(phase)
                     self._training(stub)
                     cr = rep.config["current_round"].scint32
                     mv = rep.config["model_version"].scint32
                     self._apply(rep.buffer_chunk)
                     self._train(cr)
                 elif st == "FIN":
+                    self._log_phase(phase)
                     cr = rep.config["current_round"].scint32
                     mv = rep.config["model_version"].scint32
                     self.final_state = "FIN"

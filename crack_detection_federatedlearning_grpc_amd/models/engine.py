@@ -175,7 +175,6 @@ class UNetEngine:
             prevres = Rk if k == 0 else Rk // 2
             D[f"d{k}_g"] = t(B, Rk, Rk, F)          # BN node grads (reused A / B)
             D[f"d{k}_dc"] = t(B, Rk, Rk, F)         # dy of a conv output
-            D[f"d{k}_dz"] = t(B, Rk, Rk, F)         # dgrad of convT2 (grad of relu(BN_A(c1)))
             D[f"d{k}_dxin"] = t(B, Rk, Rk, cprev)   # dgrad of convT1 at block resolution
             D[f"d{k}_dq"] = t(B, qres_of(k, Rk), qres_of(k, Rk), F)
             D[f"d{k}_dres"] = t(B, prevres, prevres, cprev)
@@ -186,7 +185,6 @@ class UNetEngine:
             D[f"e{k}_g"] = t(B, H, H, F)
             D[f"e{k}_dy"] = t(B, H, H, F)
             D[f"e{k}_dd2"] = t(B, H, H, F)
-            D[f"e{k}_dz1"] = t(B, H, H, F)
             D[f"e{k}_dd1"] = t(B, H, H, cin)
             D[f"e{k}_dz0"] = t(B, H, H, cin)
             D[f"e{k}_dres"] = t(B, H // 2, H // 2, cin)
@@ -300,16 +298,23 @@ class UNetEngine:
         return b["ab"]
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
-               pad_l) -> None:
-        """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture)."""
+               pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None) -> None:
+        """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
+
+        ``node`` = (y, bn, relu): the output is the incoming gradient of that BN node; the kernel's epilogue writes
+        the masked node gradient and accumulates the BN-backward sums (fused node_bwd)."""
         need = self.C.conv_splits(B, Ho, Wo, N, ks, stride, pad_t, Cin)
         if need > 1 and need * B * Ho * Wo * N > self.ws.numel():
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")
             self._retired.append(self.ws)
             self.ws = torch.empty(need * B * Ho * Wo * N, dtype=torch.float32, device=self.dev)
+        kw = {}
+        if node is not None:
+            ny, bn, nrelu = node
+            kw = dict(node_y=ny, node_ab=bn["ab"], node_sums=bn["sums"], node_reps=self.RS, node_relu=nrelu)
         self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
-                          pad_l, self.ws if need > 1 else None)
+                          pad_l, self.ws if need > 1 else None, **kw)
 
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
               Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor]) -> None:
@@ -377,10 +382,15 @@ class UNetEngine:
             prevres = Rk if k == 0 else Rk // 2
             up = 0 if k == 0 else 1
             bnB, bnA = self.bn[b2], self.bn[b1]
-            # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU)
-            C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, D[f"d{k}_g"], bnB["sums"],
-                       B, Rk, Rk, F, self.RS)
-            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
+            # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. For k < 3 the BN-backward sums
+            # were accumulated by the plain node pass of level k+1 that produced dxlo (node_bwd sy/sab).
+            if k == 3:
+                C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, D[f"d{k}_g"],
+                           bnB["sums"], B, Rk, Rk, F, self.RS)
+                gB = D[f"d{k}_g"]
+            else:
+                gB = dxlo
+            C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
                            self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
             if k == 0:
@@ -394,10 +404,9 @@ class UNetEngine:
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
             # convT2: input relu(BN_A(c1))
             self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, 1)
-            self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_dz"], None, None, 0, B, Rk, Rk, F,
-                         0, Rk, Rk, F, 3, 1, 1, 1)
-            C.node_bwd(D[f"d{k}_dz"], GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c1"], bnA["ab"], 1, D[f"d{k}_g"],
-                       bnA["sums"], B, Rk, Rk, F, self.RS)
+            # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
+            self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None, 0, B, Rk, Rk, F,
+                        0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1))
             C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc"],
                            self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
             # convT1: input relu(up?(prev))
@@ -405,8 +414,15 @@ class UNetEngine:
             self._igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
                          F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
-            C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None, prev_t,
-                       None, 0, D[f"d{k}_dprev"], None, B, prevres, prevres, cprev)
+            # for k > 0 this gradient is also BN_B(k-1)'s node gradient: accumulate that BN's backward sums here
+            if k > 0:
+                bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
+                C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
+                           prev_t, None, 0, D[f"d{k}_dprev"], bprev["sums"], B, prevres, prevres, cprev, self.RS,
+                           sy=A[f"d{k - 1}_c2"], sab=bprev["ab"])
+            else:
+                C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
+                           prev_t, None, 0, D[f"d{k}_dprev"], None, B, prevres, prevres, cprev)
             dxlo = D[f"d{k}_dprev"]
         # encoder
         dx_out = dxlo                                         # grad of x3
@@ -434,9 +450,10 @@ class UNetEngine:
             # depthwise 2 on relu(BN_a(y1))
             C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B, H, H, F,
                        self.C.STAT_REPLICAS)
-            C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_dz1"], B, H, H, F)
-            C.node_bwd(D[f"e{k}_dz1"], GM_SAME, 0, None, 0, 0, None, A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_g"],
-                       bna["sums"], B, H, H, F, self.RS)
+            # depthwise dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
+            C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
+                       node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
+                       node_relu=1)
             C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy"], self.G(b1, "gamma"),
                            self.G(b1, "beta"), B * H * H, F, self.RS)
             # pointwise 1
@@ -475,12 +492,12 @@ class UNetEngine:
         C = self.C
         C.adam_update(self.flat, self.grad, self.m, self.v, self.trainable, self.lr, self.b1, self.b2, self.adam_eps,
                       self.step_t)
-        C.adam_step_done(self.step_t)
         C.bn_moving_update(self.moving_table, len(self.bn_names), self.momentum)
-        self.pack()
+        self.pack(step=True)                               # also advances the Adam step counter
 
-    def pack(self) -> None:
-        self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack)
+    def pack(self, step: bool = False) -> None:
+        self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack,
+                            self.step_t if step else None)
 
     def _zero_step(self) -> None:
         self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)

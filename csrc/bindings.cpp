@@ -39,9 +39,26 @@ void ok(int rc, const char* what) {
 
 InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(ab, "ab"), C, relu}; }
 
+// fused BN-node gradient epilogue arguments (launch.h BnNodeEpi); node_y = None -> off
+BnNodeEpi node_epi_args(const OptT& node_y, const OptT& node_ab, const OptT& node_sums, int reps, int relu,
+                        int64_t out_numel, int C) {
+  BnNodeEpi e{};
+  if (!node_y) return e;
+  TORCH_CHECK(node_ab && node_sums, "node epilogue: node_ab and node_sums are required with node_y");
+  e.y = ptr<const bf16_t>(*node_y, "node_y");
+  e.ab = ptr<const float>(*node_ab, "node_ab");
+  e.sums = ptr<float>(*node_sums, "node_sums");
+  e.reps = reps < 1 ? 1 : reps;
+  e.relu = relu;
+  TORCH_CHECK(node_y->numel() == out_numel, "node epilogue: node_y must have the output's shape");
+  TORCH_CHECK(node_ab->numel() >= 4 * C && node_sums->numel() >= (int64_t)e.reps * 2 * C, "node epilogue sizes");
+  return e;
+}
+
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
-                   int pad_l, OptT ws, int algo) {
+                   int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
+                   int node_relu) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -60,6 +77,8 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   TORCH_CHECK(wt.numel() >= (int64_t)N * p.K, "conv_igemm: wt size");
   TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv_igemm: y size");
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
+  p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, y.numel(), N);
+  TORCH_CHECK(!p.node.y || (!p.stats && !p.bias), "conv_igemm: the node epilogue excludes stats and bias");
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
@@ -125,9 +144,11 @@ void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int 
   ok(dw_fwd(p, stream()), "dw_fwd");
 }
 
-void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W, int C, int algo) {
+void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W, int C, int algo, OptT node_y,
+                 OptT node_ab, OptT node_sums, int node_reps, int node_relu) {
   DwParams p = dwp(B, H, W, C);
   p.algo = algo;
+  p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, dx.numel(), C);
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.w = ptr<const float>(w, "w");
   p.y = ptr<bf16_t>(dx, "dx");
@@ -210,8 +231,12 @@ void bn_moving_update_op(at::Tensor table, int n_layers, double momentum) {
 }
 
 void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask1, OptT argmax, at::Tensor v, OptT ab,
-                 int relu_node, at::Tensor out, OptT sums, int B, int H, int W, int C, int sum_reps) {
+                 int relu_node, at::Tensor out, OptT sums, int B, int H, int W, int C, int sum_reps, OptT sy,
+                 OptT sab) {
   NodeBwdParams p{};
+  p.sy = optr<const bf16_t>(sy, "sy");
+  p.sab = optr<const float>(sab, "sab");
+  TORCH_CHECK(!p.sy || (p.sab && sy->numel() == out.numel() && sab->numel() >= 4 * C), "node_bwd: sy / sab");
   p.sum_reps = sum_reps < 1 ? 1 : sum_reps;
   p.src[0] = GradSrc{optr<const bf16_t>(src0, "src0"), src0.has_value() ? mode0 : 0, mask0};
   p.src[1] = GradSrc{optr<const bf16_t>(src1, "src1"), src1.has_value() ? mode1 : 0, mask1};
@@ -226,7 +251,7 @@ void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask
   p.B = B; p.H = H; p.W = W; p.C = C;
   const int64_t n = (int64_t)B * H * W * C;
   TORCH_CHECK(v.numel() == n && out.numel() == n, "node_bwd: v/out size");
-  if (sums) TORCH_CHECK(sums->numel() >= (int64_t)p.sum_reps * (ab ? 2 : 1) * C, "node_bwd: sums size");
+  if (sums) TORCH_CHECK(sums->numel() >= (int64_t)p.sum_reps * (ab || sab ? 2 : 1) * C, "node_bwd: sums size");
   const int64_t half = (int64_t)B * ((H + 1) / 2) * ((W + 1) / 2) * C;
   for (int s = 0; s < 2; ++s) {
     const OptT& t = s ? src1 : src0;
@@ -346,10 +371,10 @@ at::Tensor make_pack_table(std::vector<std::tuple<int, int64_t, int64_t, int, in
   return cpu.to(like.device());
 }
 
-void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n_views, int max_elems) {
+void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n_views, int max_elems, OptT step) {
   TORCH_CHECK(table.numel() == (int64_t)n_views * (int64_t)sizeof(PackView), "pack: table size");
   ok(pack_weights(ptr<const float>(flat, "flat"), ptr<bf16_t>(packed, "packed"), ptr<const PackView>(table, "table"),
-                  n_views, max_elems, stream()),
+                  n_views, max_elems, stream(), optr<int>(step, "step")),
      "pack_weights");
 }
 
@@ -424,7 +449,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_igemm", &conv_igemm_op, py::arg("x"), py::arg("wt"), py::arg("bias"), py::arg("y"), py::arg("stats"),
         py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"),
         py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"),
-        py::arg("pad_l"), py::arg("ws") = py::none(), py::arg("algo") = 0);
+        py::arg("pad_l"), py::arg("ws") = py::none(), py::arg("algo") = 0, py::arg("node_y") = py::none(),
+        py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,
+        py::arg("node_relu") = 1);
   m.def("conv_splits", &conv_splits_op);
   m.def("conv_wgrad", &conv_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),
@@ -439,7 +466,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("dw_fwd", &dw_fwd_op, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("ab"), py::arg("relu"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("C"), py::arg("algo") = 0);
   m.def("dw_dgrad", &dw_dgrad_op, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("B"), py::arg("H"),
-        py::arg("W"), py::arg("C"), py::arg("algo") = 0);
+        py::arg("W"), py::arg("C"), py::arg("algo") = 0, py::arg("node_y") = py::none(),
+        py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,
+        py::arg("node_relu") = 1);
   m.def("dw_wgrad", &dw_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1, py::arg("algo") = 0);
   m.def("entry_fwd", &entry_fwd_op);
@@ -461,7 +490,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("node_bwd", &node_bwd_op, py::arg("src0"), py::arg("mode0"), py::arg("mask0"), py::arg("src1"),
         py::arg("mode1"), py::arg("mask1"), py::arg("argmax"), py::arg("v"), py::arg("ab"), py::arg("relu_node"),
         py::arg("out"), py::arg("sums"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"),
-        py::arg("sum_reps") = 1);
+        py::arg("sum_reps") = 1, py::arg("sy") = py::none(), py::arg("sab") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply_op, py::arg("g"), py::arg("y"), py::arg("ab"), py::arg("sums"), py::arg("dy"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("C"), py::arg("sum_reps") = 1);
   m.attr("SUM_REPLICAS") = 16;
@@ -472,7 +501,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_update", &adam_update_op);
   m.def("adam_step_done", &adam_step_done_op);
   m.def("make_pack_table", &make_pack_table);
-  m.def("pack_weights", &pack_weights_op);
+  m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
+        py::arg("max_elems"), py::arg("step") = py::none());
   m.def("render_cracks", &render_cracks_op);
   m.def("gather_rows_u8", &gather_rows_u8_op);
 }

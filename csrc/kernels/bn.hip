@@ -126,11 +126,12 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
   const bool has_ab = p.ab != nullptr;
+  const float* sab = p.sab ? p.sab : p.ab;        // statistics of the BN whose sums this pass accumulates
   float a[8], bb[8], mean[8], rstd[8];
   load_f8_or(p.ab + c0, has_ab, 1.f, a);
   load_f8_or(p.ab + p.C + c0, has_ab, 0.f, bb);
-  load_f8_or(p.ab + 2 * p.C + c0, has_ab, 0.f, mean);
-  load_f8_or(p.ab + 3 * p.C + c0, has_ab, 0.f, rstd);
+  load_f8_or(sab + 2 * p.C + c0, sab != nullptr, 0.f, mean);
+  load_f8_or(sab + 3 * p.C + c0, sab != nullptr, 0.f, rstd);
   float s[2][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
@@ -142,12 +143,13 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
     const uint4 gv = pack8(g);
     *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
     if (p.sums) {
-      float gr[8];
+      float gr[8], ys[8];
       unpack8(gv, gr);
+      if (p.sy) load8(p.sy + pix * p.C + c0, ys);       // BN input of the node this gradient also feeds
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[0][j] += gr[j];
-        s[1][j] += gr[j] * (y[j] - mean[j]) * rstd[j];     // unused (and rstd = 0) for a plain node
+        s[1][j] += gr[j] * ((p.sy ? ys[j] : y[j]) - mean[j]) * rstd[j];   // rstd = 0 for a plain node
       }
     }
   };
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   if (!p.sums) return;
   // replica row of this block: every block adding into ONE row of sums serialises at the memory-side atomic units
   const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
-  if (p.ab) block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * 2 * p.C, red);
+  if (sab) block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * 2 * p.C, red);
   else {
     float s1[1][8];
 #pragma unroll

@@ -156,6 +156,34 @@ struct InXform {
   int relu;          // apply ReLU after the affine (or alone when ab == nullptr)
 };
 
+// Coefficients of a fused BN-node epilogue (launch.h BnNodeEpi) for 8 channels c0..c0+7 of C.
+struct NodeCoef {
+  float a[8], b[8], mean[8], rstd[8];
+};
+
+CFL_DEVICE void node_coef_load(const float* ab, int C, int c0, NodeCoef& k) {
+  load_f8(ab + c0, k.a);
+  load_f8(ab + C + c0, k.b);
+  load_f8(ab + 2 * C + c0, k.mean);
+  load_f8(ab + 3 * C + c0, k.rstd);
+}
+
+// g = mask * o for 8 bf16 values o (exact: o is already bf16, masked lanes become 0); accumulates the BN-backward
+// sums from the stored g. yp points at the node input y for the same pixel / channels.
+CFL_DEVICE uint4 node_epi(uint4 o_bits, const bf16_t* yp, const NodeCoef& k, int relu, float* s0, float* s1) {
+  float o[8], y[8];
+  unpack8(o_bits, o);
+  load8(yp, y);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float g = (!relu || fmaf(k.a[j], y[j], k.b[j]) > 0.f) ? o[j] : 0.f;
+    o[j] = g;
+    s0[j] += g;
+    s1[j] += g * (y[j] - k.mean[j]) * k.rstd[j];
+  }
+  return pack8(o);
+}
+
 CFL_DEVICE float xform1(float v, const InXform& t, int c) {
   if (t.ab) v = fmaf(t.ab[c], v, t.ab[t.C + c]);
   if (t.relu) v = fmaxf(v, 0.f);

@@ -288,6 +288,9 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   __syncthreads();
   constexpr int CG = BN_ / 8, ROWS_PER_PASS = NT / CG;
   const int cg = tid % CG;
+  const bool node = p.node.y != nullptr;           // fused BN-node gradient epilogue (dgrad of a BN node's input)
+  NodeCoef nk;
+  if (node) node_coef_load(p.node.ab, p.N, nBlock + cg * 8, nk);
   float s[2][8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) s[0][q] = s[1][q] = 0.f;
@@ -296,18 +299,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
     const int row = r0 + tid / CG;
     int m;
     if (out_m(row, m)) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
-      *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + nBlock + cg * 8) = v;
-      float f[8];
-      unpack8(v, f);
+      const size_t off = (size_t)m * p.N + nBlock + cg * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      if (node) {
+        v = node_epi(v, p.node.y + off, nk, p.node.relu, s[0], s[1]);
+      } else {
+        float f[8];
+        unpack8(v, f);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        s[0][q] += f[q];
-        s[1][q] += f[q] * f[q];
+        for (int q = 0; q < 8; ++q) {
+          s[0][q] += f[q];
+          s[1][q] += f[q] * f[q];
+        }
       }
+      *reinterpret_cast<uint4*>(p.y + off) = v;
     }
   }
-  if (p.stats) {
+  if (p.stats || node) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       for (int o = CG; o < 64; o <<= 1) {
@@ -322,7 +330,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
     }
     __syncthreads();
-    float* rep = p.stats + (size_t)(tile_id % STAT_REPLICAS) * 2 * p.N;
+    float* rep = node ? p.node.sums + (size_t)(tile_id % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+                      : p.stats + (size_t)(tile_id % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);

@@ -209,15 +209,20 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   constexpr int CG = BN_ / 8;                 // 16-byte column groups per row
   constexpr int ROWS_PER_PASS = NT / CG;
   const int cg = tid % CG;
+  const bool node = p.node.y != nullptr;      // fused BN-node gradient epilogue
+  NodeCoef nk;
+  if (node) node_coef_load(p.node.ab, p.N, nBlock + cg * 8, nk);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int r0 = 0; r0 < BM_; r0 += ROWS_PER_PASS) {
     const int row = r0 + tid / CG;
     const int m = mBlock + row;
     if (m < p.M) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
-      *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + nBlock + cg * 8) = v;
-      if (p.stats) {
+      const size_t off = (size_t)m * p.N + nBlock + cg * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      if (node) {
+        v = node_epi(v, p.node.y + off, nk, p.node.relu, s, s2);
+      } else if (p.stats) {
         float f[8];
         unpack8(v, f);
 #pragma unroll
@@ -226,9 +231,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
           s2[q] += f[q] * f[q];
         }
       }
+      *reinterpret_cast<uint4*>(p.y + off) = v;
     }
   }
-  if (p.stats) {
+  if (p.stats || node) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       for (int o = CG; o < 64; o <<= 1) {
@@ -243,7 +249,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       }
     }
     __syncthreads();
-    float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+    float* rep = node ? p.node.sums + (size_t)(blockIdx.x % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+                      : p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       float v = 0.f;
@@ -263,6 +270,9 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
   float bias[8], s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int q = 0; q < 8; ++q) bias[q] = p.bias ? p.bias[c0 + q] : 0.f;
+  const bool node = p.node.y != nullptr;
+  NodeCoef nk;
+  if (node) node_coef_load(p.node.ab, p.N, c0, nk);
   const size_t plane = (size_t)p.M * p.N;
   for (int m = blockIdx.x * lanes + threadIdx.x / G; m < p.M; m += gridDim.x * lanes) {
     float v[8];
@@ -275,17 +285,21 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
       v[0] += u0.x; v[1] += u0.y; v[2] += u0.z; v[3] += u0.w;
       v[4] += u1.x; v[5] += u1.y; v[6] += u1.z; v[7] += u1.w;
     }
-    const uint4 o = pack8(v);
-    *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + c0) = o;
-    float f[8];
-    unpack8(o, f);
+    uint4 o = pack8(v);
+    if (node) {
+      o = node_epi(o, p.node.y + (size_t)m * p.N + c0, nk, p.node.relu, s, s2);
+    } else {
+      float f[8];
+      unpack8(o, f);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      s[q] += f[q];
-      s2[q] += f[q] * f[q];
+      for (int q = 0; q < 8; ++q) {
+        s[q] += f[q];
+        s2[q] += f[q] * f[q];
+      }
     }
+    *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + c0) = o;
   }
-  if (!p.stats) return;
+  if (!p.stats && !node) return;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
     for (int o = G; o < 64; o <<= 1) {
@@ -300,7 +314,8 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
     }
   }
   __syncthreads();
-  float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+  float* rep = node ? p.node.sums + (size_t)(blockIdx.x % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+                    : p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
   for (int e = threadIdx.x; e < 2 * p.N; e += NT) {
     const int st = e / p.N, cc = e - st * p.N;
     float v = 0.f;

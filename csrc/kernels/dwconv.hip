@@ -250,11 +250,48 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(DwParams p, int replicas) {
         }
       }
     }
+    const bool node = MODE == 1 && p.node.y != nullptr;     // fused BN-node gradient epilogue (dgrad)
+    float s0[8], s1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
     if (row_ok) {
-      bf16_t* dst = p.y + (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+      NodeCoef nk;
+      if (node) node_coef_load(p.node.ab, p.C, c0, nk);
+      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
 #pragma unroll
       for (int i = 0; i < SL; ++i)
-        if (x0 + sc + i < p.W) *reinterpret_cast<uint4*>(dst + (size_t)i * p.C) = pack8(acc[i]);
+        if (x0 + sc + i < p.W) {
+          uint4 v = pack8(acc[i]);
+          if (node) v = node_epi(v, p.node.y + off0 + (size_t)i * p.C, nk, p.node.relu, s0, s1);
+          *reinterpret_cast<uint4*>(p.y + off0 + (size_t)i * p.C) = v;
+        }
+    }
+    if (node) {                                              // block-reduce the BN sums, one atomic per channel
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        for (int o = G; o < 64; o <<= 1) {
+          s0[j] += __shfl_xor(s0[j], o, 64);
+          s1[j] += __shfl_xor(s1[j], o, 64);
+        }
+      __syncthreads();                                       // halo reads done: reuse it for the partials
+      float* red = reinterpret_cast<float*>(sH);             // [4 waves][2][CT]
+      const int lane = tid & 63, wid = tid >> 6;
+      if (lane < G) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          red[(wid * 2 + 0) * CT + cg * 8 + j] = s0[j];
+          red[(wid * 2 + 1) * CT + cg * 8 + j] = s1[j];
+        }
+      }
+      __syncthreads();
+      const int reps = p.node.reps > 1 ? p.node.reps : 1;
+      float* dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * p.C;
+      for (int e = tid; e < 2 * CT; e += NT) {
+        const int k = e / CT, c = e % CT;
+        const float v = red[(0 * 2 + k) * CT + c] + red[(1 * 2 + k) * CT + c] + red[(2 * 2 + k) * CT + c] +
+                        red[(3 * 2 + k) * CT + c];
+        atomicAdd(&dst[k * p.C + cbase + c], v);
+      }
     }
   } else {
     float g[SL][8];
@@ -347,6 +384,7 @@ int dw_fwd(const DwParams& p, hipStream_t st) {
 
 int dw_dgrad(const DwParams& p, hipStream_t st) {
   if (tiled(p)) return launch_tile<1>(p, 1, st);
+  if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the halo-tile path only
   return launch_dw(p.dy, p.w, p.y, InXform{nullptr, p.C, 0}, p.B, p.H, p.W, p.C, 1, st);
 }
 

@@ -150,7 +150,8 @@ int entry_fwd(const EntryParams& p, hipStream_t st) {
   if (p.S % 4) return 1;
   const size_t lds = (size_t)3 * p.S * 3 * sizeof(float);
   if (lds > 48 * 1024) return 1;
-  hipLaunchKernelGGL(entry_fwd_kernel, dim3(rows < 1024 ? rows : 1024), dim3(NT), lds, st, p);
+  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 1024;
+  hipLaunchKernelGGL(entry_fwd_kernel, dim3(rows < cap ? rows : cap), dim3(NT), lds, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -11,6 +11,18 @@
 #define STAT_REPLICAS 32
 
 // ---------------------------------------------------------------- implicit-GEMM conv (conv_igemm.hip)
+// BN-node gradient epilogue (backward). The kernel's output o is the incoming gradient of a BatchNorm node whose
+// forward input was `y` (ab rows: a, b, mean, rstd). Instead of o the kernel writes the node gradient
+// g = (relu ? [a*y + b > 0] : 1) * o (bf16) and accumulates sum(g), sum(g * xhat), xhat = (y - mean) * rstd, into
+// replica rows sums[reps][2][C] - i.e. node_bwd fused into the producer's epilogue (one pass fewer).
+struct BnNodeEpi {
+  const bf16_t* y;     // nullptr = off
+  const float* ab;
+  float* sums;
+  int reps;
+  int relu;
+};
+
 struct ConvParams {
   const bf16_t* x;     // [B, Hin, Win, Cin] NHWC (physical; logical = upsample2 if up_in)
   const bf16_t* wt;    // [N][K] packed bf16 weights, K = ks*ks*Cin, k = (ky*ks + kx)*Cin + ci
@@ -24,6 +36,7 @@ struct ConvParams {
   float* ws;           // split-K fp32 workspace (nullptr: no split)
   int64_t ws_elems;
   int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
+  BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
@@ -60,6 +73,7 @@ struct DwParams {
   int B, H, W, C;
   int replicas;        // wgrad: >1 = spread block atomics over that many copies of the row (summed by grad_finish)
   int algo;            // 0 auto (C % 32 == 0 -> LDS halo tiles), 1 row-strip kernels
+  BnNodeEpi node;      // dgrad only (halo-tile path): fused BN-node gradient epilogue
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);
@@ -110,6 +124,8 @@ struct NodeBwdParams {
   int relu_node;           // mask the total by [v > 0]
   bf16_t* out;             // gradient w.r.t. the BN output (BN node) or w.r.t. x (plain node)
   float* sums;             // [sum_reps][2][C]: sum g, sum g*xhat (BN node) / [sum_reps][C] sum g (plain) / nullptr
+  const bf16_t* sy;        // optional: xhat for the sums from THIS tensor + sab (mean, rstd rows) instead of v / ab -
+  const float* sab;        //   the gradient of a plain node that is also the (unmasked) gradient of a BN node
   int B, H, W, C;
   int sum_reps;            // replica rows of sums (block b adds into row b % sum_reps); <= 1: one row
 };
@@ -187,8 +203,9 @@ struct PackView {
   int64_t dst;             // offset in the bf16 pack buffer
   int ks, cin, cout;       // layer geometry (Keras meaning)
 };
+// step != nullptr: also increments the Adam step counter (adam_step_done folded into this launch)
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
-                 hipStream_t st);
+                 hipStream_t st, int* step = nullptr);
 
 // ---------------------------------------------------------------- step bookkeeping (optim.hip)
 // grad_finish: ONE launch at the end of backward for every gradient that was accumulated into replica rows
@@ -218,6 +235,7 @@ enum TuneKey {
   TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 4)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
+  TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 1024)
   TUNE_N = 16
 };
 int cfl_tune(int key);

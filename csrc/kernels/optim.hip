@@ -43,7 +43,9 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
 
 __global__ void step_done_kernel(int* step) { *step += 1; }
 
-__global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* packed, const PackView* views) {
+__global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* packed, const PackView* views,
+                                                  int* step) {
+  if (step != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *step += 1;   // adam_step_done
   const PackView v = views[blockIdx.y];
   const int taps = v.ks * v.ks;
   int N, K;
@@ -55,27 +57,27 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
     case PK_PW: N = v.cout; K = v.cin; break;
     default: N = v.cin; K = v.cout; break;   // PK_PW_DGRAD
   }
-  const int64_t total = (int64_t)N * K;
+  const int total = N * K;                      // < 2^31 for every layer (32-bit index math, no 64-bit division)
   const float* src = flat + v.src;
   bf16_t* dst = packed + v.dst;
-  for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < total; e += (int64_t)gridDim.x * NT) {
-    const int n = (int)(e / K), k = (int)(e - (int64_t)n * K);
-    int64_t s;
+  for (int e = blockIdx.x * NT + threadIdx.x; e < total; e += gridDim.x * NT) {
+    const int n = e / K, k = e - n * K;
+    int s;
     switch (v.kind) {
-      case PK_CONV: s = (int64_t)k * v.cout + n; break;                          // HWIO [tap][ci][co]
-      case PK_CONV_DGRAD1x1: s = (int64_t)n * v.cout + k; break;                 // [ci][co] as [N=ci][K=co]
+      case PK_CONV: s = k * v.cout + n; break;                                   // HWIO [tap][ci][co]
+      case PK_CONV_DGRAD1x1: s = n * v.cout + k; break;                          // [ci][co] as [N=ci][K=co]
       case PK_CONVT: {                                                          // (3,3,out,in), flipped
         const int tap = k / v.cin, c = k - tap * v.cin;
-        s = ((int64_t)(8 - tap) * v.cout + n) * v.cin + c;
+        s = ((8 - tap) * v.cout + n) * v.cin + c;
         break;
       }
       case PK_CONVT_DGRAD: {                                                    // k = tap*cout + o, n = c
         const int tap = k / v.cout, o = k - tap * v.cout;
-        s = ((int64_t)tap * v.cout + o) * v.cin + n;
+        s = (tap * v.cout + o) * v.cin + n;
         break;
       }
-      case PK_PW: s = (int64_t)k * v.cout + n; break;                           // (1,1,C,F): [c][f]
-      default: s = (int64_t)n * v.cout + k; break;                              // pw dgrad: [N=c][K=f]
+      case PK_PW: s = k * v.cout + n; break;                                    // (1,1,C,F): [c][f]
+      default: s = n * v.cout + k; break;                                       // pw dgrad: [N=c][K=f]
     }
     dst[e] = f2bf(src[s]);
   }
@@ -198,10 +200,10 @@ int adam_step_done(int* step, hipStream_t st) {
 }
 
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
-                 hipStream_t st) {
+                 hipStream_t st, int* step) {
   int bx = (max_elems + NT - 1) / NT;
   if (bx > 256) bx = 256;
-  hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views);
+  hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views, step);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -463,3 +463,67 @@ def test_node_bwd_sum_replicas_feed_bn_bwd_apply():
     assert rel(outs[1][0], outs[0][0]) < 1e-3
     assert torch.allclose(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-3)
     assert torch.allclose(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)
+
+
+def _node_ref(C_, o_bits, yb, ab, relu, B, H, W, C):
+    """Unfused reference: node_bwd on a plain output."""
+    g = torch.zeros_like(o_bits)
+    sums = torch.zeros(2 * C, device=DEV)
+    C_.node_bwd(o_bits, 1, 0, None, 0, 0, None, yb, ab, relu, g, sums, B, H, W, C)
+    return g, sums
+
+
+@pytest.mark.parametrize("ks,Cin,N,H,B,split", [(3, 64, 64, 16, 2, False), (3, 32, 32, 24, 2, False),
+                                                 (3, 256, 64, 16, 2, True), (1, 64, 128, 16, 2, False)])
+def test_conv_node_epilogue_matches_node_bwd(ks, Cin, N, H, B, split):
+    torch.manual_seed(23)
+    C_ = hip()
+    xb, _ = bf(torch.randn(B, H, H, Cin))
+    wt, _ = bf(torch.randn(N, ks * ks * Cin) * 0.05)
+    yb, _ = bf(torch.randn(B, H, H, N))
+    ab, _, _ = ab_for(N, 9)
+    ab[2 * N:3 * N] = torch.randn(N) * 0.1
+    ab[3 * N:] = torch.rand(N) + 0.5
+    ab = ab.to(DEV)
+    pad = 1 if ks == 3 else 0
+    ws = torch.zeros(16 * B * H * H * N, device=DEV) if split else None
+    out = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+    C_.conv_igemm(xb, wt, None, out, None, None, 0, B, H, H, Cin, 0, H, H, N, ks, 1, pad, pad, ws)
+    g_ref, s_ref = _node_ref(C_, out, yb, ab, 1, B, H, H, N)
+    R_ = 4
+    g = torch.zeros_like(out)
+    sums = torch.zeros(R_ * 2 * N, device=DEV)
+    C_.conv_igemm(xb, wt, None, g, None, None, 0, B, H, H, Cin, 0, H, H, N, ks, 1, pad, pad, ws,
+                  node_y=yb, node_ab=ab, node_sums=sums, node_reps=R_, node_relu=1)
+    assert torch.equal(g, g_ref) or rel(from_bits(g), from_bits(g_ref)) < 1e-3
+    assert torch.allclose(sums.view(R_, 2 * N).sum(0), s_ref, rtol=1e-3, atol=1e-2)
+
+
+def test_dw_dgrad_node_epilogue_and_node_bwd_side_sums():
+    torch.manual_seed(29)
+    C_ = hip()
+    B, H, C = 2, 20, 64
+    dyb, _ = bf(torch.randn(B, H, H, C))
+    w = (torch.randn(9 * C) * 0.2).to(DEV)
+    yb, _ = bf(torch.randn(B, H, H, C))
+    ab, _, _ = ab_for(C, 3)
+    ab[3 * C:] = torch.rand(C) + 0.5
+    ab = ab.to(DEV)
+    dz = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
+    C_.dw_dgrad(dyb, w, dz, B, H, H, C)
+    g_ref, s_ref = _node_ref(C_, dz, yb, ab, 1, B, H, H, C)
+    g = torch.zeros_like(dz)
+    sums = torch.zeros(8 * 2 * C, device=DEV)
+    C_.dw_dgrad(dyb, w, g, B, H, H, C, 0, node_y=yb, node_ab=ab, node_sums=sums, node_reps=8, node_relu=1)
+    assert torch.equal(g, g_ref)
+    assert torch.allclose(sums.view(8, 2 * C).sum(0), s_ref, rtol=1e-3, atol=1e-2)
+    # plain node whose output also feeds an unmasked BN node: sums from sy / sab
+    vb, _ = bf(torch.randn(B, H, H, C))
+    out = torch.zeros_like(dz)
+    side = torch.zeros(2 * C, device=DEV)
+    C_.node_bwd(dz, 1, 1, None, 0, 0, None, vb, None, 0, out, side, B, H, H, C, 1, sy=yb, sab=ab)
+    out2 = torch.zeros_like(dz)
+    C_.node_bwd(dz, 1, 1, None, 0, 0, None, vb, None, 0, out2, None, B, H, H, C)
+    assert torch.equal(out, out2)
+    _, s2 = _node_ref(C_, out2, yb, ab, 0, B, H, H, C)
+    assert torch.allclose(side, s2, rtol=1e-3, atol=1e-2)
