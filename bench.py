@@ -92,8 +92,11 @@ def main() -> int:
                 eng.idx.copy_(vbatches[v])
                 eng.eval_step(use_graph)
         if agg is not None:
-            agg.average(float(n_local))                    # weighted FedAvg over RCCL/xGMI
-        eng.pack()
+            # weighted FedAvg over RCCL/xGMI, bucketed in layer order on a side stream; each bucket's layers are
+            # repacked to bf16 there and the next round waits per bucket (engine.defer_until)
+            eng.defer_until(agg.average_async(float(n_local), on_bucket=eng.pack_bucket))
+        else:
+            eng.pack()
 
     for _ in range(args.warmup):
         fl_round()

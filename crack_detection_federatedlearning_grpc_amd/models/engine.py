@@ -49,6 +49,7 @@ class UNetEngine:
         if img % 16:
             raise ValueError("image size must be a multiple of 16")
         self.C = hip()
+        self._pending: List[tuple] = []
         self.table = table
         self.B, self.S = batch, img
         self.dev = torch.device(device)
@@ -82,7 +83,38 @@ class UNetEngine:
     # ------------------------------------------------------------------------------------------------ params
     def P(self, layer: str, w: str) -> torch.Tensor:
         e = self.table.entry(layer, w)
+        if self._pending:
+            self._await_range(e.offset + e.size)
         return self.flat[e.offset:e.offset + e.size]
+
+    # ---- overlapped aggregation (parallel/rccl.py FedAvgAllReduce.average_async) ----
+    def defer_until(self, bucket_events) -> None:
+        """Register per-bucket completion events of an in-flight FedAvg all-reduce (+ bucket repack). The eager
+        step waits per layer - each parameter read waits only for the bucket holding it, so the first layers
+        start while later buckets are still reducing; a graph replay (no per-layer hooks) waits for all."""
+        self._pending = [(sl.start, sl.stop, ev) for sl, ev in bucket_events]
+
+    def _await_range(self, end: int) -> None:
+        cur = torch.cuda.current_stream(self.dev)
+        while self._pending and self._pending[0][0] < end:
+            _, _, ev = self._pending.pop(0)
+            cur.wait_event(ev)
+
+    def _await_all(self) -> None:
+        if self._pending:
+            self._await_range(self.table.total + 1)
+
+    def pack_bucket(self, sl: slice) -> None:
+        """bf16 repack of the views whose source range ENDS inside this bucket (buckets complete in order, so the
+        earlier part of a view that straddles a boundary is already reduced)."""
+        key = (sl.start, sl.stop)
+        if key not in self._bucket_packs:
+            sub = [v for v in self._views if sl.start < v[1] + v[3] * v[3] * v[4] * v[5] <= sl.stop]
+            self._bucket_packs[key] = (self.C.make_pack_table(sub, self.flat), len(sub),
+                                       max([v[3] * v[3] * v[4] * v[5] for v in sub], default=0)) if sub else None
+        t = self._bucket_packs[key]
+        if t is not None:
+            self.C.pack_weights(self.flat, self.packed, t[0], t[1], t[2])
 
     def G(self, layer: str, w: str) -> torch.Tensor:
         e = self.table.entry(layer, w)
@@ -113,10 +145,16 @@ class UNetEngine:
                 add(PK_CONV_DGRAD1x1, ly.name, "kernel", 1, ly.cin, ly.cout)
         self.packed = torch.zeros(off, dtype=torch.int16, device=self.dev)
         self.pack_table = self.C.make_pack_table(views, self.flat)
+        self._views = views
+        self._view_src = {(v[0], ly): v for ly, v in zip([k[0] for k in self.packed_at], views)}
+        self._bucket_packs: Dict[Tuple[int, int], object] = {}
         self.n_views, self.max_pack = len(views), max_el
 
     def W(self, layer: str, kind: int) -> torch.Tensor:
         off, n = self.packed_at[(layer, kind)]
+        if self._pending:
+            v = self._view_src[(kind, layer)]
+            self._await_range(v[1] + v[3] * v[3] * v[4] * v[5])
         return self.packed[off:off + n]
 
     # ------------------------------------------------------------------------------------------------ buffers
@@ -489,6 +527,7 @@ class UNetEngine:
         C.grad_finish(self.finish_table, self.n_finish, self.finish_work)
 
     def optimizer_step(self) -> None:
+        self._await_all()
         C = self.C
         C.adam_update(self.flat, self.grad, self.m, self.v, self.trainable, self.lr, self.b1, self.b2, self.adam_eps,
                       self.step_t)
@@ -510,6 +549,7 @@ class UNetEngine:
 
     # ------------------------------------------------------------------------------------------------ graph
     def capture(self) -> None:
+        self._await_all()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
@@ -530,6 +570,7 @@ class UNetEngine:
         if use_graph:
             if self.graph is None:
                 self.capture()
+            self._await_all()
             self.graph.replay()
         else:
             self.train_step_eager()
@@ -540,6 +581,7 @@ class UNetEngine:
         if not use_graph:
             self.forward(False)
             return
+        self._await_all()
         if self.eval_graph is None:
             s = torch.cuda.Stream(device=self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
@@ -557,10 +599,12 @@ class UNetEngine:
 
     # ------------------------------------------------------------------------------------------------ state
     def set_flat(self, flat: np.ndarray) -> None:
+        self._await_all()
         self.flat.copy_(torch.as_tensor(np.asarray(flat, np.float32)).to(self.dev))
         self.pack()
 
     def get_flat(self) -> np.ndarray:
+        self._await_all()
         return self.flat.detach().cpu().numpy().copy()
 
     def reset_optimizer(self) -> None:

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import os
 from datetime import timedelta
-from typing import Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -40,6 +40,7 @@ class FedAvgAllReduce:
         self.buckets = _buckets(flat.numel(), max(1024, int(bucket_mb * (1 << 20)) // 4))
         self._total_n: Optional[float] = None
         self._last_n: Optional[float] = None
+        self._side = None
 
     def total_samples(self, n_local: float) -> float:
         if self._total_n is None or self._last_n != n_local:
@@ -58,6 +59,37 @@ class FedAvgAllReduce:
             works.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         for wk in works:
             wk.wait()
+
+    def average_async(self, n_local: float, weighted: bool = True,
+                      on_bucket: Optional[Callable[[slice], None]] = None) -> List[Tuple[slice, object]]:
+        """Overlapped FedAvg: the buckets' all-reduces are issued in forward-layer order and each bucket's
+        completion is chained onto a side HIP stream, where ``on_bucket`` (e.g. the bf16 repack of the layers in
+        that bucket) runs and a per-bucket event is recorded. Returns [(bucket slice, event)] - the consumer waits
+        per layer (``UNetEngine.defer_until``) instead of on the whole model, so the next round's setup and early
+        layers overlap the late buckets. On CPU / gloo the reduction is synchronous and no events are returned."""
+        if self.flat.device.type != "cuda":
+            self.average(n_local, weighted)
+            if on_bucket is not None:
+                for sl in self.buckets:
+                    on_bucket(sl)
+            return []
+        tot = self.total_samples(n_local) if weighted else float(self.world)
+        w = (float(n_local) if weighted else 1.0) / max(tot, 1e-12)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.flat.device)
+        out = []
+        for sl in self.buckets:
+            b = self.flat[sl]
+            b.mul_(w)
+            work = dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            with torch.cuda.stream(self._side):
+                work.wait()                                   # side stream <- this bucket's collective
+                if on_bucket is not None:
+                    on_bucket(sl)
+                ev = torch.cuda.Event()
+                ev.record(self._side)
+            out.append((sl, ev))
+        return out
 
 
 class RcclAggregator:

@@ -159,7 +159,7 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
-  const int cap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 512;
+  const int cap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 256;   // measured
   const int reps = p.replicas > 1 ? p.replicas : 1;
   hipLaunchKernelGGL(entry_wgrad_kernel, dim3(rows < cap ? rows : cap, 3), dim3(NT), (size_t)p.S * 3 * sizeof(float),
                      st, p, reps);

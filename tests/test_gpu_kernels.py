@@ -527,3 +527,43 @@ def test_dw_dgrad_node_epilogue_and_node_bwd_side_sums():
     assert torch.equal(out, out2)
     _, s2 = _node_ref(C_, out2, yb, ab, 0, B, H, H, C)
     assert torch.allclose(side, s2, rtol=1e-3, atol=1e-2)
+
+
+def test_overlapped_fedavg_bucket_repack_and_per_layer_waits():
+    """average_async on a 1-rank RCCL group: per-bucket repack equals a full repack, and an eager step that waits
+    per layer on the bucket events matches the synchronous path."""
+    import socket
+    import torch.distributed as dist
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import FedAvgAllReduce
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=6)
+        eng.train_step(use_graph=False)
+        f1 = eng.get_flat()
+        agg = FedAvgAllReduce(eng.flat, table, world=1, bucket_mb=0.5)       # several buckets
+        assert len(agg.buckets) > 2
+        eng.packed.zero_()
+        eng.defer_until(agg.average_async(10.0, on_bucket=eng.pack_bucket))
+        torch.cuda.synchronize()
+        packed_async = eng.packed.clone()
+        eng.pack()
+        assert torch.equal(packed_async, eng.packed)                          # every view repacked exactly once
+        assert np.array_equal(eng.get_flat(), f1)                             # 1 rank: average == identity
+        opt = [t.clone() for t in (eng.m, eng.v, eng.step_t)]
+        eng.defer_until(agg.average_async(10.0, on_bucket=eng.pack_bucket))
+        eng.train_step(use_graph=False)                                       # per-layer waits inside
+        f2 = eng.get_flat()
+        eng.set_flat(f1)
+        for t, c in zip((eng.m, eng.v, eng.step_t), opt):
+            t.copy_(c)
+        eng.train_step(use_graph=False)
+        f3 = eng.get_flat()
+        d = np.abs(f2 - f3)
+        assert d.max() < 2.5e-3 and (d > 1e-4).mean() < 0.01
+    finally:
+        dist.destroy_process_group()
