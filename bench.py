@@ -38,6 +38,7 @@ def main() -> int:
                     help="validation batches per epoch (-1: the whole held-out split, as Keras fit(validation_data))")
     ap.add_argument("--samples", type=int, default=8000, help="synthetic images per client")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="decoder Conv2DTranspose forward in fp8 e4m3 (config 5)")
     ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
     args = ap.parse_args()
 
@@ -61,7 +62,7 @@ def main() -> int:
 
     table = ParamTable()
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank, split=min(6213, args.samples))
-    eng = UNetEngine(table, args.batch, args.img, dev)
+    eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
     agg = FedAvgAllReduce(eng.flat, table, world) if world > 1 else None
@@ -125,7 +126,7 @@ def main() -> int:
         out = {"metric": "images/sec/node per FL round", "value": round(value, 2), "unit": "images/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(round_s * 1000.0, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-rendered crack masks, random init)",
+               "vs_baseline": None, "dtype": "bf16+fp8-convT-fwd" if args.fp8 else "bf16", "data": "synthetic (device-rendered crack masks, random init)",
                "wall_clock_per_round_s": round(round_s, 4),
                "ms_per_iteration": round(round_s * 1000.0 / (args.epochs * args.local_steps), 4),
                "val_images_per_round": world * args.epochs * val_steps * args.batch,

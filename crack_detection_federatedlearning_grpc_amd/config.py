@@ -69,6 +69,7 @@ class FLConfig:
     predict_round: int = 5               # client_fit_model.py:235 (cr == 5)
     device: str = "auto"                 # auto | cpu | cuda
     dtype: str = "bf16"                  # activation dtype on the GPU path (fp32 master weights)
+    conv_dtype: str = "bf16"             # bf16 | fp8: decoder Conv2DTranspose forward in fp8 e4m3 MFMA (config 5)
     use_graph: bool = True               # capture the train step in a hipGraph
 
     # --- data ------------------------------------------------------------------------------------
@@ -111,6 +112,10 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # config 3: 8 clients, RCCL weighted all-reduce.
     "gpu8-256": dict(device="cuda", img_size=256, batch_size=16, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, long_poll_s=20.0),
+    # config 5: fp8 (e4m3) Conv2DTranspose forward MFMA path + overlapped RCCL aggregation, 8 clients.
+    "gpu8-fp8": dict(device="cuda", img_size=256, batch_size=16, ready_stall_s=0.0, num_clients=8,
+                     register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, long_poll_s=20.0,
+                     conv_dtype="fp8"),
     # config 4: 512x512 large batch, activation memory sized for 288 GB HBM.
     "gpu8-512": dict(device="cuda", img_size=512, batch_size=64, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5),

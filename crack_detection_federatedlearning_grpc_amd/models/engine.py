@@ -45,7 +45,9 @@ class Lazy:
 class UNetEngine:
     def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
                  lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
-                 bn_momentum: float = 0.99, bn_eps: float = 1e-3):
+                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, fp8: bool = False):
+        self.fp8 = fp8                     # decoder Conv2DTranspose forward in fp8 e4m3 (conv3x3_fp8.hip)
+        self._fp8_calibrated = False
         if img % 16:
             raise ValueError("image size must be a multiple of 16")
         self.C = hip()
@@ -145,6 +147,24 @@ class UNetEngine:
                 add(PK_CONV_DGRAD1x1, ly.name, "kernel", 1, ly.cin, ly.cout)
         self.packed = torch.zeros(off, dtype=torch.int16, device=self.dev)
         self.pack_table = self.C.make_pack_table(views, self.flat)
+        if self.fp8:   # fp8 copies of the forward ConvT weights + per-output-channel scales + delayed amax slots
+            v8, off8, soff, self.p8_at = [], 0, 0, {}
+            for kind, src, _dst, ks, cin, cout in views:
+                if kind != PK_CONVT:
+                    continue
+                layer = next(ly for (ly, kd) in self.packed_at if kd == kind and
+                             self.table.entry(ly, "kernel").offset == src)
+                n = 9 * cin * cout
+                v8.append((kind, src, off8, ks, cin, cout, soff))
+                self.p8_at[layer] = (off8, n, soff, cout, len(v8) - 1)
+                off8 += (n + 15) // 16 * 16
+                soff += cout
+            self.packed8 = torch.zeros(off8, dtype=torch.uint8, device=self.dev)
+            self.scales8 = torch.ones(soff, dtype=torch.float32, device=self.dev)
+            self.amax8 = torch.zeros(len(v8), 2, dtype=torch.float32, device=self.dev)
+            self.amax8[:, 0] = 1.0                            # seed; replaced by the calibration forward
+            self.pack8_table = self.C.make_pack8_table(v8, self.flat)
+            self.n_views8, self.max_rows8 = len(v8), max(v[5] for v in v8)
         self._views = views
         self._view_src = {(v[0], ly): v for ly, v in zip([k[0] for k in self.packed_at], views)}
         self._bucket_packs: Dict[Tuple[int, int], object] = {}
@@ -389,11 +409,11 @@ class UNetEngine:
             t1, b1, t2, b2, rc = (next(n) for _ in range(5))
             Rk = r[3] << k
             up = 0 if k == 0 else 1
-            self._conv(Lazy(prev.t, None, 1, prev.H, prev.C), t1, PK_CONVT, A[f"d{k}_c1"], F, 3, 1, up, Rk,
-                       self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
+            self._convt(Lazy(prev.t, None, 1, prev.H, prev.C), t1, A[f"d{k}_c1"], F, up, Rk,
+                        self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
             abA = self._bn_final(b1, train)
-            self._conv(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, PK_CONVT, A[f"d{k}_c2"], F, 3, 1, 0, Rk,
-                       self.P(t2, "bias"), self.bn[b2]["stats"] if train else None)
+            self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
+                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None)
             abB = self._bn_final(b2, train)
             self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
             C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
@@ -537,11 +557,50 @@ class UNetEngine:
     def pack(self, step: bool = False) -> None:
         self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack,
                             self.step_t if step else None)
+        if self.fp8:   # after an optimizer step also fold the recorded activation amax (delayed scaling)
+            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
+                            self.amax8 if step else None, self.n_views8)
+
+    def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
+               bias: torch.Tensor, stats: Optional[torch.Tensor]) -> None:
+        """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled, else the bf16 halo kernel."""
+        if not self.fp8:
+            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats)
+            return
+        B = self.B
+        need = self.C.conv_splits(B, Ho, Ho, N, 3, 1, 1, x.C)
+        if need > 1 and need * B * Ho * Ho * N > self.ws.numel():
+            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("split-K workspace must be sized before graph capture")
+            self._retired.append(self.ws)
+            self.ws = torch.empty(need * B * Ho * Ho * N, dtype=torch.float32, device=self.dev)
+        off8, n8, soff, cout, i = self.p8_at[layer]
+        if self._pending:
+            self.P(layer, "kernel")                           # wait for this layer's FedAvg bucket
+        self.C.conv3x3_fp8(x.t, self.packed8[off8:off8 + n8], self.scales8[soff:soff + cout], self.amax8[i],
+                           bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho, N,
+                           self.ws if need > 1 else None)
+
+    def _fp8_calibrate(self) -> None:
+        """Seed the delayed activation scales: one training-mode forward records every fp8 conv input's amax,
+        which the fold then installs (weights, BN state and metrics untouched)."""
+        if not self.fp8 or self._fp8_calibrated:
+            return
+        self._fp8_calibrated = True
+        saved = self.metrics.clone()
+        self._zero_step()
+        self.amax8[:, 0] = 1e30                               # no saturation while measuring
+        self.forward(True)
+        self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
+                        self.amax8, self.n_views8)
+        self._zero_step()
+        self.metrics.copy_(saved)
 
     def _zero_step(self) -> None:
         self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
 
     def train_step_eager(self) -> None:
+        self._fp8_calibrate()
         self._zero_step()
         self.forward(True)
         self.backward()
@@ -578,6 +637,7 @@ class UNetEngine:
     def eval_step(self, use_graph: bool = True) -> None:
         """Inference-mode forward (moving BN statistics) of the batch in ``idx``; loss / accuracy accumulate into
         ``eval_metrics``. Replayed from its own hipGraph (captured after an eager warm-up)."""
+        self._fp8_calibrate()
         if not use_graph:
             self.forward(False)
             return
@@ -639,7 +699,7 @@ class HipBackend:
         self.cfg = cfg
         self.table = table
         self.eng = UNetEngine(table, cfg.batch_size, data.img_size, "cuda", cfg.loss, cfg.lr, cfg.beta1, cfg.beta2,
-                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps)
+                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps, fp8=getattr(cfg, "conv_dtype", "") == "fp8")
         images = data.images if isinstance(data.images, torch.Tensor) else torch.as_tensor(data.images)
         masks = data.masks if isinstance(data.masks, torch.Tensor) else torch.as_tensor(data.masks)
         self.eng.bind_data(images.to(self.eng.dev), masks.to(self.eng.dev))

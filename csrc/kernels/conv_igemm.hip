@@ -336,10 +336,17 @@ void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
 }  // namespace
 
 bool conv3x3_supported(const ConvParams& p);
-int conv3x3_splits(const ConvParams& p);
 int conv3x3(const ConvParams& p, hipStream_t st);
 
 static bool use3x3(const ConvParams& p) { return p.algo != 1 && conv3x3_supported(p); }
+
+int splitk_epilogue(const ConvParams& p, int splits, hipStream_t st) {
+  const int G = p.N / 8, lanes = NT / G;
+  int blocks = (p.M + lanes - 1) / lanes;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(NT), 0, st, p, p.ws, splits);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 int conv_igemm_splits(const ConvParams& p) {
   if (use3x3(p)) return conv3x3_splits(p);

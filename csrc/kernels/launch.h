@@ -40,6 +40,20 @@ struct ConvParams {
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
+int conv3x3_splits(const ConvParams& p);
+int splitk_epilogue(const ConvParams& p, int splits, hipStream_t st);   // sum partials + bias/stats/node epilogue
+
+// fp8 (e4m3) forward 3x3 conv (conv3x3_fp8.hip): c.wt unused; per-output-channel weight scales, delayed
+// per-tensor activation scaling through amax[2] (scale from amax[0], this call's amax max-ed into amax[1])
+struct Conv8Params {
+  ConvParams c;
+  const uint8_t* wt8;      // [N][K] fp8 weights (pack_fp8)
+  const float* wscale;     // [N]
+  float* amax;             // [2]
+};
+int conv3x3_fp8(const Conv8Params& p, hipStream_t st);
+bool conv3x3_fp8_supported(const ConvParams& c);
+
 
 // ---------------------------------------------------------------- weight gradient (conv_wgrad.hip)
 struct WgradParams {
@@ -200,9 +214,14 @@ enum PackKind { PK_CONV = 0, PK_CONV_DGRAD1x1 = 1, PK_CONVT = 2, PK_CONVT_DGRAD 
 struct PackView {
   int kind;
   int64_t src;             // offset in the flat fp32 buffer
-  int64_t dst;             // offset in the bf16 pack buffer
+  int64_t dst;             // offset in the bf16 pack buffer (fp8 pack: byte offset)
   int ks, cin, cout;       // layer geometry (Keras meaning)
+  int64_t dst_scale;       // fp8 pack: offset of the per-output-channel scales
 };
+// fp8 weight pack of PK_CONVT views (dst = byte offset into packed8, dst_scale = offset into scales); if amax is
+// given, also folds every conv's recorded amax[i][1] into its scale slot amax[i][0] (delayed scaling)
+int pack_fp8(const float* flat, uint8_t* packed8, float* scales, const PackView* d_views, int n_views, int max_rows,
+             hipStream_t st, float* amax = nullptr, int n_amax = 0);
 // step != nullptr: also increments the Adam step counter (adam_step_done folded into this launch)
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
                  hipStream_t st, int* step = nullptr);
