@@ -621,3 +621,46 @@ def test_engine_fp8_trains_close_to_bf16():
         losses[fp8] = ls
         assert ls[-1] < ls[0] and all(np.isfinite(ls))
     assert abs(losses[True][0] - losses[False][0]) < 0.1 * losses[False][0]
+
+
+def test_ops_autograd_layers_match_torch():
+    """ops/: Conv2D 3x3 / 1x1, Conv2DTranspose 3x3 and depthwise 3x3 as autograd functions vs fp32 torch."""
+    from crack_detection_federatedlearning_grpc_amd import ops
+    torch.manual_seed(37)
+    B, H, Cin, N = 2, 12, 32, 64
+    x32 = torch.randn(B, H, H, Cin)
+    xb = x32.to(torch.bfloat16).to(DEV).requires_grad_(True)
+    xr = x32.to(torch.bfloat16).float().requires_grad_(True)
+    cases = [("conv3", torch.randn(3, 3, Cin, N) * 0.05), ("conv1", torch.randn(1, 1, Cin, N) * 0.1),
+             ("convT", torch.randn(3, 3, N, Cin) * 0.05)]
+    for name, wk in cases:
+        w = wk.clone().to(DEV).requires_grad_(True)
+        b = (torch.randn(N) * 0.1).to(DEV).requires_grad_(True)
+        wr = wk.to(torch.bfloat16).float().requires_grad_(True)
+        br = b.detach().cpu().clone().requires_grad_(True)
+        if name == "convT":
+            y = ops.conv2d_transpose(xb, w, b)
+            yr = R.convt_same(xr.permute(0, 3, 1, 2), wr, br).permute(0, 2, 3, 1)
+        else:
+            y = ops.conv2d(xb, w, b)
+            yr = R.conv2d_same(xr.permute(0, 3, 1, 2), wr, br, 1).permute(0, 2, 3, 1)
+        gy = torch.randn_like(yr)
+        (y.float() * gy.to(DEV)).sum().backward()
+        (yr * gy).sum().backward()
+        assert rel(y.float().cpu(), yr.detach()) < 1e-2, name
+        assert rel(xb.grad.float().cpu(), xr.grad) < 2e-2, name
+        assert rel(w.grad.cpu(), wr.grad) < 2e-2, name
+        assert rel(b.grad.cpu(), br.grad) < 1e-3, name
+        xb.grad = None
+        xr.grad = None
+    wd = (torch.randn(3, 3, Cin, 1) * 0.2)
+    w = wd.clone().to(DEV).requires_grad_(True)
+    wr = wd.clone().requires_grad_(True)
+    y = ops.depthwise3x3(xb, w)
+    yr = F.conv2d(F.pad(xr.permute(0, 3, 1, 2), (1, 1, 1, 1)), wr.permute(2, 3, 0, 1), None, groups=Cin)
+    yr = yr.permute(0, 2, 3, 1)
+    gy = torch.randn_like(yr)
+    (y.float() * gy.to(DEV)).sum().backward()
+    (yr * gy).sum().backward()
+    assert rel(y.float().cpu(), yr.detach()) < 1e-2
+    assert rel(xb.grad.float().cpu(), xr.grad) < 2e-2 and rel(w.grad.cpu(), wr.grad) < 2e-2
