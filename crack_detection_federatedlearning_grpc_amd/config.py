@@ -86,6 +86,8 @@ class FLConfig:
     server_weight_file: str = "./server_weights/weights.pickle"
     log_dir: str = "send_logs/logs"
     metrics_file: str = ""               # JSONL metrics sink ("" = stdout only)
+    tensorboard: bool = False            # Keras-style tfevents per round under log_dir (client_fit_model.py:153-154)
+    histogram_freq: int = 1              # weight histograms every N epochs (the reference's histogram_freq=1)
     upload_logs: bool = False
     log_chunk_mb: int = 100
     snapshot_dir: str = ""               # server per-round snapshot (.h5 + state json) for --resume

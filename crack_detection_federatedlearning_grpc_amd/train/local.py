@@ -135,6 +135,10 @@ class LocalFit:
         print(f"### Model Training - Round: {current_round} ###")
         self.backend.reset_optimizer()
         out: Dict[str, float] = {}
+        tb = None
+        if cfg.tensorboard:
+            from ..utils.tfevents import KerasTensorBoard
+            tb = KerasTensorBoard(cfg.log_dir, current_round, cfg.histogram_freq)
         for ep in range(cfg.epochs):
             seed = (cfg.data_seed * 1000003 + current_round * 1009 + ep) & 0x7FFFFFFF
             batches = epoch_batches(self.data.train_idx, cfg.batch_size, self.steps, seed)
@@ -149,7 +153,15 @@ class LocalFit:
                 v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
                 rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
             self._log(rec)
+            if tb is not None:
+                ws = None
+                if cfg.histogram_freq and ep % cfg.histogram_freq == 0:
+                    flat = self.backend.get_flat()
+                    ws = [(e.keras_name, flat[e.offset:e.offset + e.size]) for e in self.table.entries]
+                tb.on_epoch_end(ep, rec, ws)
             out = rec
+        if tb is not None:
+            tb.close()
         if current_round == cfg.predict_round and len(self.data.val_idx):
             out["predict"] = self.predict_and_analyze(self.data.val_idx[:min(4, len(self.data.val_idx))])
         self.last = out

@@ -69,9 +69,12 @@ py::array_t<uint8_t> resize(py::array_t<uint8_t, py::array::c_style | py::array:
 }
 }  // namespace imgproc
 
+void register_tfrecord(py::module_& m);
+
 PYBIND11_MODULE(_native, m) {
-  m.doc() = "host-side native components (HDF5, contours, image resize)";
+  m.doc() = "host-side native components (HDF5, contours, image resize, TFRecord framing)";
   register_h5lite(m);
   register_contour(m);
+  register_tfrecord(m);
   m.def("resize_bilinear", &imgproc::resize, py::arg("img"), py::arg("height"), py::arg("width"), py::arg("threads") = 4);
 }
