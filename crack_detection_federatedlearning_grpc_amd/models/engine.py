@@ -563,8 +563,9 @@ class UNetEngine:
 
     def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
                bias: torch.Tensor, stats: Optional[torch.Tensor]) -> None:
-        """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled, else the bf16 halo kernel."""
-        if not self.fp8:
+        """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled (maps of at least 8x8; smaller ones - only
+        at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel."""
+        if not self.fp8 or Ho < 8:
             self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats)
             return
         B = self.B

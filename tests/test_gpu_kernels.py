@@ -650,7 +650,7 @@ def test_ops_autograd_layers_match_torch():
         assert rel(y.float().cpu(), yr.detach()) < 1e-2, name
         assert rel(xb.grad.float().cpu(), xr.grad) < 2e-2, name
         assert rel(w.grad.cpu(), wr.grad) < 2e-2, name
-        assert rel(b.grad.cpu(), br.grad) < 1e-3, name
+        assert rel(b.grad.cpu(), br.grad) < 5e-3, name          # dy reaches the op as bf16
         xb.grad = None
         xr.grad = None
     wd = (torch.randn(3, 3, Cin, 1) * 0.2)
