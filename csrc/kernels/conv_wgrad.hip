@@ -16,7 +16,6 @@
 
 namespace {
 
-constexpr int RM = 32;     // reduction step (pixels)
 constexpr int NT = 256;
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
@@ -25,7 +24,9 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(p));
 }
 
-template <int BKO, int BNO>
+// RM: pixels per pipeline stage (32 = one MFMA k-step; 128 = four k-steps per barrier and 4x the bytes in flight
+// per stage for the small K x N tiles, which are latency-bound at 32)
+template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
   constexpr int TK = BKO / 2, TN = BNO / 2;
   constexpr int FK = TK / 16, FN = TN / 16;
@@ -139,26 +140,30 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
   for (int m0 = m_begin; m0 < m_end; m0 += RM) {
     const bool more = m0 + RM < m_end;
     if (more) load(m0 + RM);
-    s8v af[FK], bfg[FN];
 #pragma unroll
-    for (int i = 0; i < FK; ++i) {
-      const int kc = wk * TK + i * 16 + 4 * pq;
-      const s4v lo = tr_read(&sX[buf][8 * g + q][kc]);
-      const s4v hi = tr_read(&sX[buf][8 * g + 4 + q][kc]);
-      af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int ks = 0; ks < RM / 32; ++ks) {
+      const int r0 = 32 * ks + 8 * g + q;
+      s8v af[FK], bfg[FN];
+#pragma unroll
+      for (int i = 0; i < FK; ++i) {
+        const int kc = wk * TK + i * 16 + 4 * pq;
+        const s4v lo = tr_read(&sX[buf][r0][kc]);
+        const s4v hi = tr_read(&sX[buf][r0 + 4][kc]);
+        af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int nc = wn * TN + j * 16 + 4 * pq;
+        const s4v lo = tr_read(&sG[buf][r0][nc]);
+        const s4v hi = tr_read(&sG[buf][r0 + 4][nc]);
+        bfg[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < FK; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int nc = wn * TN + j * 16 + 4 * pq;
-      const s4v lo = tr_read(&sG[buf][8 * g + q][nc]);
-      const s4v hi = tr_read(&sG[buf][8 * g + 4 + q][nc]);
-      bfg[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < FK; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
     }
 }
 
-template <int BKO, int BNO>
+template <int BKO, int BNO, int RM = 32>
 void launch(const WgradParams& p, hipStream_t st) {
   const int tiles = (p.K / BKO) * (p.N / BNO);
   int chunk = p.m_chunk;
@@ -201,7 +206,7 @@ void launch(const WgradParams& p, hipStream_t st) {
   chunk = (chunk + RM - 1) / RM * RM;
   const int zs = (p.M + chunk - 1) / chunk;
   dim3 grid(p.K / BKO, p.N / BNO, zs);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BKO, BNO>), grid, dim3(NT), 0, st, p, chunk);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BKO, BNO, RM>), grid, dim3(NT), 0, st, p, chunk);
 }
 
 }  // namespace
@@ -223,9 +228,9 @@ int conv_wgrad(const WgradParams& p, hipStream_t st) {
   if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
   const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
   if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) launch<128, 128>(p, st);
-  else if (p.K % 64 == 0 && p.N % 64 == 0) launch<64, 64>(p, st);
-  else if (p.K % 64 == 0) launch<64, 32>(p, st);
-  else if (p.N % 64 == 0) launch<32, 64>(p, st);
-  else launch<32, 32>(p, st);
+  else if (p.K % 64 == 0 && p.N % 64 == 0) launch<64, 64, 128>(p, st);
+  else if (p.K % 64 == 0) launch<64, 32, 128>(p, st);
+  else if (p.N % 64 == 0) launch<32, 64, 128>(p, st);
+  else launch<32, 32, 128>(p, st);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
