@@ -92,26 +92,28 @@ CFL_DEVICE void node_gather(const NodeBwdParams& p, int b, int h, int w, int c0,
     } else if (src.mode == GM_MAXPOOL) {
       // pooled outputs whose 3x3/s2 window contains (h, w): oh = h>>1 (ky = h&1) and, for even h >= 2,
       // oh = h/2 - 1 (ky = 2); same for w
-      const int ohs[2] = {h >> 1, ((h & 1) == 0 && h >= 2) ? (h >> 1) - 1 : -1};
-      const int kys[2] = {h & 1, 2};
-      const int ows[2] = {w >> 1, ((w & 1) == 0 && w >= 2) ? (w >> 1) - 1 : -1};
-      const int kxs[2] = {w & 1, 2};
+      // branch-free: the second candidate of each axis may not exist (clamped to a valid address, its tap id set
+      // to one no argmax holds), so all four gathers issue back to back instead of one latency each
+      const bool h2 = (h & 1) == 0 && h >= 2, w2 = (w & 1) == 0 && w >= 2;
+      const int ohs[2] = {h >> 1, h2 ? (h >> 1) - 1 : 0};
+      const int ows[2] = {w >> 1, w2 ? (w >> 1) - 1 : 0};
+      const int kys[2] = {(h & 1) * 3, h2 ? 6 : 64};
+      const int kxs[2] = {w & 1, w2 ? 2 : 64};
+      uint2 am[4];
+      float u[4][8];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (ohs[i] < 0 || ohs[i] >= Hh) continue;
+      for (int q = 0; q < 4; ++q) {
+        const size_t o = ((size_t)(b * Hh + ohs[q >> 1]) * Wh + ows[q & 1]) * p.C + c0;
+        am[q] = *reinterpret_cast<const uint2*>(p.argmax + o);
+        load8(src.p + o, u[q]);
+      }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          if (ows[k] < 0 || ows[k] >= Wh) continue;
-          const size_t o = ((size_t)(b * Hh + ohs[i]) * Wh + ows[k]) * p.C + c0;
-          const uint2 am = *reinterpret_cast<const uint2*>(p.argmax + o);
-          const int want = kys[i] * 3 + kxs[k];
-          float u[8];
-          load8(src.p + o, u);
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t want = (uint32_t)(kys[q >> 1] + kxs[q & 1]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t word = j < 4 ? am.x : am.y;
-            if ((int)((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[j];
-          }
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? am[q].x : am[q].y;
+          if (((word >> (8 * (j & 3))) & 0xffu) == want) t[j] += u[q][j];
         }
       }
     }
@@ -184,6 +186,8 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   }
 }
 
+constexpr int BBA_IPT = 4;
+
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
   __shared__ float ssum[2 * 256];
   const int G = p.C >> 3, lg = ilog2(G);
@@ -230,17 +234,29 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
     k1[j] = ssum[c0 + j] * invM;
     k2[j] = ssum[p.C + c0 + j] * invM;
   }
-  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
-    const int m = t >> lg;
-    float g[8], y[8], o[8];
-    load8(p.g + (size_t)m * p.C + c0, g);
-    load8(p.y + (size_t)m * p.C + c0, y);
+  // BBA_IPT items per thread per iteration, all loads issued before any math (memory-level parallelism: the small
+  // layers launch few blocks, so one item in flight per thread would leave HBM latency-bound)
+  const int S = gridDim.x * NT;
+  for (int t0 = blockIdx.x * NT + threadIdx.x; t0 < total; t0 += BBA_IPT * S) {
+    float g[BBA_IPT][8], y[BBA_IPT][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xhat = (y[j] - mean[j]) * rstd[j];
-      o[j] = a[j] * (g[j] - k1[j] - xhat * k2[j]);
+    for (int u = 0; u < BBA_IPT; ++u) {
+      const int t = t0 + u * S;
+      const size_t m = (size_t)(t < total ? t : t0) >> lg;   // clamped: loads stay unconditional
+      load8(p.g + m * p.C + c0, g[u]);
+      load8(p.y + m * p.C + c0, y[u]);
     }
-    *reinterpret_cast<uint4*>(p.dy + (size_t)m * p.C + c0) = pack8(o);
+#pragma unroll
+    for (int u = 0; u < BBA_IPT; ++u) {
+      const int t = t0 + u * S;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xhat = (y[u][j] - mean[j]) * rstd[j];
+        o[j] = a[j] * (g[u][j] - k1[j] - xhat * k2[j]);
+      }
+      if (t < total) *reinterpret_cast<uint4*>(p.dy + (size_t)(t >> lg) * p.C + c0) = pack8(o);
+    }
   }
 }
 
@@ -283,8 +299,8 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
   if (p.C % 8 || !pow2(p.C / 8)) return 1;
   if (p.C > 256) return 1;
-  int blocks = (int)(((int64_t)p.M * (p.C / 8) + NT - 1) / NT);
-  if (blocks > 2048) blocks = 2048;
+  int blocks = (int)(((int64_t)p.M * (p.C / 8) + BBA_IPT * NT - 1) / (BBA_IPT * NT));
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -199,27 +199,42 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(DwParams p, int replicas) {
   const bool has_ab = tx && p.xf.ab != nullptr;
   const int relu = tx ? p.xf.relu : 0;
   const bf16_t* src = MODE == 1 ? p.dy : p.x;
-  for (int e = tid; e < HALO_CH; e += NT) {
-    const int hp = e / G, q = e % G;
+  // all of this thread's halo loads issue back to back (unconditional register staging), then transform + LDS
+  // writes; NT is a multiple of G, so the thread's channel group (and its BN coefficients) is fixed
+  constexpr int NIT = (HALO_CH + NT - 1) / NT;
+  const int q = tid % G;
+  float a8[8], b8[8];
+  load_f8_or(p.xf.ab + cbase + q * 8, has_ab, 1.f, a8);
+  load_f8_or(p.xf.ab + p.xf.C + cbase + q * 8, has_ab, 0.f, b8);
+  uint4 hv[NIT];
+  uint32_t okm = 0;
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = tid + k * NT, hp = e / G;
     const int hy = hp / HWp, hx = hp - hy * HWp;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    const bool ok = e < HALO_CH && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) {
-      v = *reinterpret_cast<const uint4*>(src + (((size_t)b * p.H + iy) * p.W + ix) * p.C + cbase + q * 8);
-      if (has_ab || relu) {
-        float a8[8], b8[8], f[8];
-        load_f8_or(p.xf.ab + cbase + q * 8, has_ab, 1.f, a8);
-        load_f8_or(p.xf.ab + p.xf.C + cbase + q * 8, has_ab, 0.f, b8);
-        unpack8(v, f);
+    if (ok) v = *reinterpret_cast<const uint4*>(src + (((size_t)b * p.H + iy) * p.W + ix) * p.C + cbase + q * 8);
+    hv[k] = v;
+    okm |= (uint32_t)ok << k;
+  }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f[j] = fmaf(a8[j], f[j], b8[j]);
-          if (relu) f[j] = fmaxf(f[j], 0.f);
-        }
-        v = pack8(f);
+  for (int k = 0; k < NIT; ++k) {
+    const int e = tid + k * NT;
+    if (e >= HALO_CH) break;
+    uint4 v = hv[k];
+    if ((has_ab || relu) && ((okm >> k) & 1u)) {              // padding stays zero (TF SAME pads the input)
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = fmaf(a8[j], f[j], b8[j]);
+        if (relu) f[j] = fmaxf(f[j], 0.f);
       }
+      v = pack8(f);
     }
-    *reinterpret_cast<uint4*>(&sH[hp * LDP + q * 8]) = v;
+    *reinterpret_cast<uint4*>(&sH[(e / G) * LDP + q * 8]) = v;
   }
   __syncthreads();
 
