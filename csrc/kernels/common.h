@@ -23,12 +23,18 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 CFL_DEVICE float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-CFL_DEVICE bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)0x7fc0;   // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// fp32 -> bf16 round-to-nearest-even with gfx950's v_cvt_pk_bf16_f32 (one instruction per pair, NaN stays NaN)
+// instead of the ~5-op integer rounding sequence: bf16 packing is a large share of the VALU work of every
+// memory-bound epilogue / elementwise kernel.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+CFL_DEVICE uint32_t pack2bf(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
+
+CFL_DEVICE bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 // 8 bf16 <-> 8 float through one 16-byte vector
 CFL_DEVICE void unpack8(const uint4& v, float* f) {
@@ -41,10 +47,7 @@ CFL_DEVICE void unpack8(const uint4& v, float* f) {
 }
 
 CFL_DEVICE uint4 pack8(const float* f) {
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
 }
 
 CFL_DEVICE void load8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }

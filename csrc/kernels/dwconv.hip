@@ -367,6 +367,320 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(DwParams p, int replicas) {
   }
 }
 
+// ---- row-streaming variant (default) ----
+// A block owns a 32-pixel column strip x 32 channels x a segment of rows and walks down it 4 output rows per step.
+// Input rows live in an LDS ring of 10 rows: each input row is fetched once per segment (halo overhead
+// (SEG+2)/SEG x 34/32 instead of 6/4 x 34/32 for independent tiles), and the next step's 4 new rows are in flight in
+// registers while the current step computes. One barrier per step: the rows written after step s's compute and the
+// rows step s reads are 10 consecutive rows, i.e. distinct ring slots.
+// Thread = 4 channels x a strip of 4 pixels (8-byte vectors): 36 fp32 weights / tap sums per thread instead of 72
+// keeps the kernel at 3 waves per SIMD without spilling.
+namespace dws {
+constexpr int CT = 32, CPT = 4, G = CT / CPT, P = NT / G, SL = 4, TW = 32, SR = P / (TW / SL);
+constexpr int HWp = TW + 2, NRING = 2 * SR + 2, LDP = CT + 8;
+static_assert(TW * G == NT, "staging map: one thread per (column, channel group) of a row");
+
+CFL_DEVICE void unpack4(const uint2& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+CFL_DEVICE uint2 pack4(const float* f) {
+  return make_uint2(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]));
+}
+CFL_DEVICE void load_f4(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+}
+CFL_DEVICE void load_f4_or(const float* p, bool cond, float dflt, float* f) {
+  float4 a = make_float4(dflt, dflt, dflt, dflt);
+  if (cond) a = *reinterpret_cast<const float4*>(p);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+}
+
+// Row-major staging map: thread t owns column t / G (0..31) of every staged row, and the first 2*G*NR threads also
+// one element of the two right-halo columns 32, 33 (row t / (2G)); q = t % G in both cases. Addresses are then a
+// per-thread constant plus a per-row stride, so staging NR rows costs NR + 1 loads and almost no address registers.
+// src_b: image b's base + this thread's channel offset; offsets are 32-bit (every tensor < 2^31 elements).
+template <int NR>
+CFL_DEVICE void fetch(const bf16_t* src_b, const DwParams& p, int x0, int row0, bool on, uint2 (&v)[NR + 1],
+                      uint32_t& okm) {
+  const int tid = threadIdx.x;
+  const int ix = x0 + tid / G - 1;
+  const bool colok = on && (unsigned)ix < (unsigned)p.W;
+  okm = 0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int iy = row0 + r;
+    const bool ok = colok && (unsigned)iy < (unsigned)p.H;
+    uint2 t = make_uint2(0, 0);
+    if (ok) t = *reinterpret_cast<const uint2*>(src_b + (iy * p.W + ix) * p.C);
+    v[r] = t;
+    okm |= (uint32_t)ok << r;
+  }
+  const int iye = row0 + tid / (2 * G), ixe = x0 + TW - 1 + (tid % (2 * G)) / G;
+  const bool ok = on && tid < 2 * G * NR && (unsigned)iye < (unsigned)p.H && (unsigned)ixe < (unsigned)p.W;
+  uint2 t = make_uint2(0, 0);
+  if (ok) t = *reinterpret_cast<const uint2*>(src_b + (iye * p.W + ixe) * p.C);
+  v[NR] = t;
+  okm |= (uint32_t)ok << NR;
+}
+
+CFL_DEVICE uint2 xform4(uint2 t, bool on, const float* a4, const float* b4, int relu) {
+  if (!on) return t;                                         // padding stays zero (TF SAME pads the input)
+  float f[4];
+  unpack4(t, f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = fmaf(a4[j], f[j], b4[j]);
+    if (relu) f[j] = fmaxf(f[j], 0.f);
+  }
+  return pack4(f);
+}
+
+template <int NR>
+CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0, bool xform, const float* a4,
+                    const float* b4, int relu) {
+  const int tid = threadIdx.x, q = tid % G;
+  const int slot0 = (row0 + NRING) % NRING;                  // row0 >= -1
+  bf16_t* col = sH + (tid / G) * LDP + q * CPT;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int slot = slot0 + r >= NRING ? slot0 + r - NRING : slot0 + r;
+    *reinterpret_cast<uint2*>(col + slot * HWp * LDP) = xform4(v[r], xform && ((okm >> r) & 1u), a4, b4, relu);
+  }
+  if (tid < 2 * G * NR) {
+    const int re = tid / (2 * G), hxe = TW + (tid % (2 * G)) / G;
+    const int slot = slot0 + re >= NRING ? slot0 + re - NRING : slot0 + re;
+    *reinterpret_cast<uint2*>(sH + (slot * HWp + hxe) * LDP + q * CPT) =
+        xform4(v[NR], xform && ((okm >> NR) & 1u), a4, b4, relu);
+  }
+}
+}  // namespace dws
+
+template <int MODE>
+__global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replicas, int seg_rows) {
+  using namespace dws;
+  __shared__ __attribute__((aligned(16))) bf16_t sH[NRING * HWp * LDP];
+  __shared__ __attribute__((aligned(16))) float sNode[MODE == 1 ? 4 * CT : 4];   // dgrad node coefficients
+
+  const int tid = threadIdx.x, cg = tid % G, pt = tid / G;
+  const int sr = pt / (TW / SL), sc = (pt % (TW / SL)) * SL;
+  const int nslices = p.C / CT, tiles_w = (p.W + TW - 1) / TW, nseg = (p.H + seg_rows - 1) / seg_rows;
+  int lin = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int cs = lin % nslices;
+  lin /= nslices;
+  const int tw = lin % tiles_w;
+  lin /= tiles_w;
+  const int sg = lin % nseg;
+  const int b = lin / nseg;
+  const int x0 = tw * TW, cbase = cs * CT, c0 = cbase + cg * CPT;
+  const int ybeg = sg * seg_rows, yend = min(p.H, ybeg + seg_rows);
+  const int nsteps = (yend - ybeg + SR - 1) / SR;
+
+  const bool tx = MODE != 1;
+  const bool has_ab = tx && p.xf.ab != nullptr;
+  const int relu = tx ? p.xf.relu : 0;
+  const bf16_t* src_b = (MODE == 1 ? p.dy : p.x) + (size_t)b * p.H * p.W * p.C + c0;
+  float a4[4], b4[4];
+  load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
+  load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+  // fwd / dgrad taps live in LDS (re-read per input row: 36 fewer live registers than holding all 9 taps)
+  __shared__ __attribute__((aligned(16))) float sW[MODE == 2 ? 4 : 9 * CT];
+  if (MODE != 2) {
+    for (int e = tid; e < 9 * CT; e += NT) {
+      const int t = e / CT, c = e - t * CT;
+      sW[MODE == 2 ? 0 : e] = p.w[(MODE == 1 ? 8 - t : t) * p.C + cbase + c];
+    }
+  }
+  {
+    uint2 v[SR + 3];
+    uint32_t okm;
+    fetch<SR + 2>(src_b, p, x0, ybeg - 1, true, v, okm);
+    put<SR + 2>(sH, v, okm, ybeg - 1, has_ab || relu, a4, b4, relu);
+  }
+  // wgrad: this thread's dy strip of the current step (prefetched one step ahead like the halo rows)
+  constexpr int NG = MODE == 2 ? SL : 1;
+  uint2 gq[NG];
+  auto fetch_dy = [&](int a, uint2* dst) {
+    const int oy = a + sr;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const bool ok = oy < yend && x0 + sc + i < p.W;
+      uint2 t = make_uint2(0, 0);
+      if (ok) t = *reinterpret_cast<const uint2*>(p.dy + (((size_t)b * p.H + oy) * p.W + x0 + sc + i) * p.C + c0);
+      dst[i] = t;
+    }
+  };
+  if (MODE == 2) fetch_dy(ybeg, gq);
+  if (MODE == 1 && p.node.y != nullptr && tid < 4 * CT)
+    sNode[MODE == 1 ? tid : 0] = p.node.ab[(tid / CT) * p.C + cbase + tid % CT];
+  __syncthreads();
+
+  constexpr int NA = MODE == 2 ? 9 : SL;
+  float acc[NA][4];
+#pragma unroll
+  for (int t = 0; t < NA; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+  const bool node = MODE == 1 && p.node.y != nullptr;       // fused BN-node gradient epilogue (dgrad)
+  float s0[4], s1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s0[j] = s1[j] = 0.f;
+
+  // halo rows are prefetched two steps ahead (register sets ra / rb alternate): one step's rows in flight per block
+  // are too few bytes to cover HBM latency at 3 blocks per CU
+  // (wgrad keeps one step: its dy strips and 36 tap sums leave no registers for a second set)
+  constexpr bool D2 = MODE != 2;
+  uint2 ra[SR + 1], rb[SR + 1];
+  uint32_t oka = 0, okb = 0;
+  if (D2) fetch<SR>(src_b, p, x0, ybeg + SR + 1, nsteps > 1, ra, oka);
+  auto step = [&](int s, uint2 (&cur)[SR + 1], uint32_t& curok, uint2 (&nxt)[SR + 1], uint32_t& nxtok) {
+    const int a = ybeg + s * SR;
+    const bool more = s + 1 < nsteps;
+    if (D2) fetch<SR>(src_b, p, x0, a + 2 * SR + 1, s + 2 < nsteps, nxt, nxtok);
+    else fetch<SR>(src_b, p, x0, a + SR + 1, more, cur, curok);
+    uint2 gn[NG];
+    if (MODE == 2) fetch_dy(more ? a + SR : yend, gn);
+    const int oy = a + sr;
+    if (MODE != 2) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    }
+    float g[NG][4];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) unpack4(gq[i], g[i]);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int slot = (oy - 1 + ky + NRING) % NRING;
+      const bf16_t* hrow = &sH[(slot * HWp + sc) * LDP + cg * CPT];
+      float wt[MODE == 2 ? 1 : 3][4];
+      if (MODE != 2) {
+#pragma unroll
+        for (int kx = 0; kx < (MODE == 2 ? 1 : 3); ++kx) load_f4(&sW[(ky * 3 + kx) * CT + cg * CPT], wt[kx]);
+      }
+#pragma unroll
+      for (int cx = 0; cx < SL + 2; ++cx) {
+        float f[4];
+        unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SL) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (MODE == 2) acc[ky * 3 + kx][j] = fmaf(f[j], g[MODE == 2 ? o : 0][j], acc[ky * 3 + kx][j]);
+            else acc[MODE == 2 ? 0 : o][j] = fmaf(f[j], wt[MODE == 2 ? 0 : kx][j], acc[MODE == 2 ? 0 : o][j]);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one input row's 6 LDS reads in flight at a time (register pressure)
+    }
+    if (MODE != 2 && oy < yend) {
+      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+#pragma unroll
+      for (int i = 0; i < SL; ++i)
+        if (x0 + sc + i < p.W) {
+          uint2 v = pack4(acc[MODE == 2 ? 0 : i]);
+          if (node) {                                        // g = mask * o (o already bf16) + BN-backward sums
+            float o[4], y[4], na[4], nb[4], nmean[4], nrstd[4];   // coefficients re-read from LDS (registers)
+            const float* nc = &sNode[cg * CPT];
+            load_f4(nc, na);
+            load_f4(nc + CT, nb);
+            load_f4(nc + 2 * CT, nmean);
+            load_f4(nc + 3 * CT, nrstd);
+            unpack4(v, o);
+            unpack4(*reinterpret_cast<const uint2*>(p.node.y + off0 + (size_t)i * p.C), y);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float gg = (!p.node.relu || fmaf(na[j], y[j], nb[j]) > 0.f) ? o[j] : 0.f;
+              o[j] = gg;
+              s0[j] += gg;
+              s1[j] += gg * (y[j] - nmean[j]) * nrstd[j];
+            }
+            v = pack4(o);
+          }
+          *reinterpret_cast<uint2*>(p.y + off0 + (size_t)i * p.C) = v;
+        }
+    }
+    if (more) put<SR>(sH, cur, curok, a + SR + 1, has_ab || relu, a4, b4, relu);
+    if (MODE == 2) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) gq[i] = gn[i];
+    }
+    __syncthreads();
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, ra, oka, rb, okb);
+    if (s + 1 < nsteps) step(s + 1, rb, okb, ra, oka);
+  }
+
+  const int lane = tid & 63, wid = tid >> 6;
+  float* red = reinterpret_cast<float*>(sH);                 // ring no longer needed (loop ended on a barrier)
+  constexpr int NS = MODE == 2 ? 9 : 2;                      // rows of per-channel partials
+  float part[NS][4];
+  if (MODE == 2) {
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) part[t][j] = acc[MODE == 2 ? t : 0][j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      part[0][j] = s0[j];
+      part[MODE == 2 ? 0 : 1][j] = s1[j];
+    }
+  }
+  if (MODE == 2 || node) {                                   // block reduction, one atomic per (row, channel)
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = part[t][j];
+        for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+        part[t][j] = v;
+      }
+    if (lane < G) {
+#pragma unroll
+      for (int t = 0; t < NS; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(wid * NS + t) * CT + cg * CPT + j] = part[t][j];
+    }
+    __syncthreads();
+    float* dst;
+    int rstride;
+    if (MODE == 2) {
+      dst = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
+      rstride = p.C;
+    } else {
+      const int reps = p.node.reps > 1 ? p.node.reps : 1;
+      dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * p.C;
+      rstride = p.C;
+    }
+    for (int e = tid; e < NS * CT; e += NT) {
+      const int t = e / CT, c = e % CT;
+      atomicAdd(&dst[t * rstride + cbase + c], red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] +
+                                                   red[(2 * NS + t) * CT + c] + red[(3 * NS + t) * CT + c]);
+    }
+  }
+}
+
+template <int MODE>
+int launch_stream(const DwParams& p, int replicas, hipStream_t st) {
+  const int steps = (p.H + dws::SR - 1) / dws::SR;
+  const int strips = p.B * ((p.W + 31) / 32) * (p.C / dws::CT);
+  const int target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 1024;
+  int nseg = (target + strips - 1) / strips;
+  nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
+  const int seg_rows = ((steps + nseg - 1) / nseg) * dws::SR;
+  nseg = (p.H + seg_rows - 1) / seg_rows;
+  hipLaunchKernelGGL((dw_stream_kernel<MODE>), dim3(strips * nseg), dim3(NT), 0, st, p, replicas, seg_rows);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 template <int MODE>
 int launch_tile(const DwParams& p, int replicas, hipStream_t st) {
   const int ct = p.C % 64 == 0 ? 64 : 32;
@@ -391,19 +705,23 @@ int launch_dw(const bf16_t* x, const float* w, bf16_t* y, InXform xf, int B, int
 }  // namespace
 
 static bool tiled(const DwParams& p) { return p.C % 32 == 0 && p.algo != 1; }
+static bool streamed(const DwParams& p) { return tiled(p) && p.algo != 2; }
 
 int dw_fwd(const DwParams& p, hipStream_t st) {
+  if (streamed(p)) return launch_stream<0>(p, 1, st);
   if (tiled(p)) return launch_tile<0>(p, 1, st);
   return launch_dw(p.x, p.w, p.y, p.xf, p.B, p.H, p.W, p.C, 0, st);
 }
 
 int dw_dgrad(const DwParams& p, hipStream_t st) {
+  if (streamed(p)) return launch_stream<1>(p, 1, st);
   if (tiled(p)) return launch_tile<1>(p, 1, st);
   if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the halo-tile path only
   return launch_dw(p.dy, p.w, p.y, InXform{nullptr, p.C, 0}, p.B, p.H, p.W, p.C, 1, st);
 }
 
 int dw_wgrad(const DwParams& p, hipStream_t st) {
+  if (streamed(p)) return launch_stream<2>(p, p.replicas > 1 ? p.replicas : 1, st);
   if (tiled(p)) return launch_tile<2>(p, p.replicas > 1 ? p.replicas : 1, st);
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
   const int sw = (p.W % 4 == 0) ? 4 : 1;

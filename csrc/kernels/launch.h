@@ -86,7 +86,7 @@ struct DwParams {
   InXform xf;
   int B, H, W, C;
   int replicas;        // wgrad: >1 = spread block atomics over that many copies of the row (summed by grad_finish)
-  int algo;            // 0 auto (C % 32 == 0 -> LDS halo tiles), 1 row-strip kernels
+  int algo;            // 0 auto (C % 32 == 0 -> row-streaming LDS ring), 1 row-strip kernels, 2 LDS halo tiles
   BnNodeEpi node;      // dgrad only (halo-tile path): fused BN-node gradient epilogue
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
@@ -255,6 +255,7 @@ enum TuneKey {
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
   TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 1024)
+  TUNE_DW_STREAM_BLOCKS = 8,   // depthwise row-streaming kernels: target grid size (default 1024)
   TUNE_N = 16
 };
 int cfl_tune(int key);

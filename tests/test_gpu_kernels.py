@@ -143,9 +143,20 @@ def test_conv_wgrad_1x1_and_up(stride, up):
     assert rel(dw.view(1, 1, Cin, N).cpu(), w.grad) < 2e-2
 
 
-@pytest.mark.parametrize("B,H,C,algo", [(2, 10, 64, 0), (2, 10, 64, 1), (3, 37, 32, 0), (2, 18, 128, 0),
-                                        (1, 9, 256, 0)])
-def test_depthwise_fwd_dgrad_wgrad(B, H, C, algo):
+# algo 0 = row-streaming LDS ring (stream_blocks = grid target: 1 -> one segment per column strip, so a block walks
+# every row step of the image), 1 = row strips, 2 = independent halo tiles
+@pytest.mark.parametrize("B,H,C,algo,stream_blocks", [(2, 10, 64, 0, 0), (2, 10, 64, 1, 0), (3, 37, 32, 0, 0),
+                                                      (2, 18, 128, 0, 0), (1, 9, 256, 0, 0), (3, 37, 32, 2, 0),
+                                                      (2, 18, 128, 2, 0), (2, 45, 64, 0, 1), (1, 70, 32, 0, 3)])
+def test_depthwise_fwd_dgrad_wgrad(B, H, C, algo, stream_blocks):
+    hip().set_tune(hip().TUNE_DW_STREAM_BLOCKS, stream_blocks)
+    try:
+        _depthwise_case(B, H, C, algo)
+    finally:
+        hip().set_tune(hip().TUNE_DW_STREAM_BLOCKS, 0)
+
+
+def _depthwise_case(B, H, C, algo):
     torch.manual_seed(6)
     xb, xf = bf(torch.randn(B, H, H, C))
     dyb, dyf = bf(torch.randn(B, H, H, C))

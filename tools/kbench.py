@@ -101,10 +101,12 @@ def main():
         n[name] += 1
         line = f"{t:8.1f}  {shape_key(name, a, k)}"
         if args.variants and name in ("conv_wgrad", "conv_igemm", "dw_fwd", "dw_dgrad", "dw_wgrad"):
-            for algo in (1, 0):
+            for algo in ((1, 2, 0) if name.startswith("dw_") else (1, 0)):
                 a2, kk = list(a), dict(k)
                 if name == "conv_wgrad":      # (..., dst_mode, m_chunk, algo, slabs): direct atomics variant
                     a2[-2], a2[-1] = algo, 0
+                elif name == "dw_dgrad" and len(a2) > 7:      # algo passed positionally (node epilogue call)
+                    a2[7] = algo
                 else:
                     kk["algo"] = algo
                 try:
