@@ -13,3 +13,16 @@ for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:22]:
     t = float(r["TotalDurationNs"])
     print(f"{t / 1e6 / steps:8.3f} ms/step {100 * t / tot:6.2f}%  calls/step {int(r['Calls']) / steps:6.1f}  "
           f"avg {float(r['AverageNs']) / 1e3:8.1f} us  {r['Name'][:80]}")
+
+# busy vs wall over the graph-replayed steps (kernel trace): the gap share is launch/dependency overhead
+import os  # noqa: E402
+tp = f"{d}/run_kernel_trace.csv"
+if os.path.exists(tp):
+    tr = [r for r in csv.DictReader(open(tp)) if not any(s in r["Kernel_Name"] for s in skip)]
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    n = len(tr)
+    tail = tr[n // 2:]                       # second half: steady-state replays
+    wall = int(tail[-1]["End_Timestamp"]) - int(tail[0]["Start_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tail)
+    print(f"steady state (last {len(tail)} kernels): wall {wall / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms, "
+          f"idle {100 * (1 - busy / max(wall, 1)):.1f}%  (avg gap {(wall - busy) / 1e3 / max(len(tail) - 1, 1):.2f} us)")
