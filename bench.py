@@ -31,7 +31,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=3, help="timed FL rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed FL rounds")
     ap.add_argument("--img", type=int, default=256)
-    ap.add_argument("--batch", type=int, default=16, help="per-client batch (reference: 16)")
+    ap.add_argument("--batch", type=int, default=16,
+                    help="per-client batch (reference: 16; 0 = HBM planner, models/memplan.py)")
+    ap.add_argument("--hbm-fraction", type=float, default=0.85, help="HBM share the batch planner may fill")
     ap.add_argument("--epochs", type=int, default=10, help="local epochs per FL round (client_fit_model.py:166)")
     ap.add_argument("--local-steps", type=int, default=388, help="iterations per epoch (reference: 6213 // 16)")
     ap.add_argument("--val-steps", type=int, default=-1,
@@ -61,6 +63,13 @@ def main() -> int:
     from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
 
     table = ParamTable()
+    plan = None
+    if args.batch <= 0:
+        from crack_detection_federatedlearning_grpc_amd.models.memplan import plan_batch
+        plan = plan_batch(args.img, None, args.hbm_fraction, args.samples)
+        args.batch = plan.batch
+        if args.local_steps == 388:                        # reference epoch = 6213 // batch iterations
+            args.local_steps = max(1, min(6213, args.samples) // args.batch)
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank, split=min(6213, args.samples))
     eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
     eng.bind_data(data.images, data.masks)
@@ -137,7 +146,7 @@ def main() -> int:
                           "seq_len": None, "epochs_per_round": args.epochs,
                           "local_steps_per_round": args.epochs * args.local_steps,
                           "parallelism": f"fedavg-dp{world} (1 FL client per GPU, RCCL weighted all-reduce)",
-                          "graph": use_graph}}
+                          "graph": use_graph, "memplan": plan.as_dict() if plan else None}}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -54,7 +54,8 @@ class FLConfig:
     # --- local training ------------------------------------------------------------------------
     epochs: int = 10
     steps_per_epoch: int = 0             # 0 = len(train)//batch (reference Sequence.__len__)
-    batch_size: int = 16
+    batch_size: int = 16                 # 0 = planned: largest batch that fits hbm_fraction of HBM (models/memplan.py)
+    hbm_fraction: float = 0.85           # HBM share the batch planner may fill (engine + resident dataset shard)
     img_size: int = 128
     val_samples: int = 6213              # reference: FIRST 6213 are train (client_fit_model.py:79)
     shuffle_seed: int = 1337
@@ -119,7 +120,7 @@ PRESETS: Dict[str, Dict[str, Any]] = {
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, long_poll_s=20.0,
                      conv_dtype="fp8"),
     # config 4: 512x512 large batch, activation memory sized for 288 GB HBM.
-    "gpu8-512": dict(device="cuda", img_size=512, batch_size=64, ready_stall_s=0.0, num_clients=8,
+    "gpu8-512": dict(device="cuda", img_size=512, batch_size=0, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5),
 }
 

@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from .._native_loader import hip
+from .memplan import buffer_shapes
 from .spec import DEC_FILTERS, ENC_FILTERS, ENTRY_FILTERS, ParamTable
 
 PK_CONV, PK_CONV_DGRAD1x1, PK_CONVT, PK_CONVT_DGRAD, PK_PW, PK_PW_DGRAD = range(6)
@@ -202,54 +203,13 @@ class UNetEngine:
                                     sums=self.sums_all[RS * 2 * so:RS * 2 * (so + c)],
                                     ab=self.ab_all[4 * so:4 * (so + c)])
             so += c
-        # forward activations (raw bf16) -------------------------------------------------------------
-        A = self.act = {}
-        A["y0"] = t(B, r[0], r[0], ENTRY_FILTERS)
-        cin = ENTRY_FILTERS
-        for k, F in enumerate(ENC_FILTERS):
-            H = r[k]
-            A[f"e{k}_d1"] = t(B, H, H, cin)
-            A[f"e{k}_y1"] = t(B, H, H, F)
-            A[f"e{k}_d2"] = t(B, H, H, F)
-            A[f"e{k}_y2"] = t(B, H, H, F)
-            A[f"e{k}_res"] = t(B, H // 2, H // 2, F)
-            A[f"e{k}_x"] = t(B, H // 2, H // 2, F)
-            A[f"e{k}_am"] = torch.zeros(B, H // 2, H // 2, F, dtype=torch.uint8, device=self.dev)
-            cin = F
-        for k, F in enumerate(DEC_FILTERS):
-            Rk = r[3] << k
-            A[f"d{k}_c1"] = t(B, Rk, Rk, F)
-            A[f"d{k}_c2"] = t(B, Rk, Rk, F)
-            qres = Rk if k == 0 else Rk // 2
-            A[f"d{k}_q"] = t(B, qres, qres, F)
-            A[f"d{k}_xlo"] = t(B, Rk, Rk, F)
-        self.h = torch.zeros(B, r[0], r[0], dtype=torch.float32, device=self.dev)
-        # backward buffers ----------------------------------------------------------------------------------
-        D = self.dg = {}
-        D["dxlo3"] = t(B, r[0], r[0], DEC_FILTERS[-1])
-        for k, F in enumerate(DEC_FILTERS):
-            Rk = r[3] << k
-            cprev = ENC_FILTERS[-1] if k == 0 else DEC_FILTERS[k - 1]
-            prevres = Rk if k == 0 else Rk // 2
-            D[f"d{k}_g"] = t(B, Rk, Rk, F)          # BN node grads (reused A / B)
-            D[f"d{k}_dc"] = t(B, Rk, Rk, F)         # dy of a conv output
-            D[f"d{k}_dxin"] = t(B, Rk, Rk, cprev)   # dgrad of convT1 at block resolution
-            D[f"d{k}_dq"] = t(B, qres_of(k, Rk), qres_of(k, Rk), F)
-            D[f"d{k}_dres"] = t(B, prevres, prevres, cprev)
-            D[f"d{k}_dprev"] = t(B, prevres, prevres, cprev)
-        cin = ENTRY_FILTERS
-        for k, F in enumerate(ENC_FILTERS):
-            H = r[k]
-            D[f"e{k}_g"] = t(B, H, H, F)
-            D[f"e{k}_dy"] = t(B, H, H, F)
-            D[f"e{k}_dd2"] = t(B, H, H, F)
-            D[f"e{k}_dd1"] = t(B, H, H, cin)
-            D[f"e{k}_dz0"] = t(B, H, H, cin)
-            D[f"e{k}_dres"] = t(B, H // 2, H // 2, cin)
-            D[f"e{k}_dx"] = t(B, H, H, cin) if k > 0 else None
-            cin = F
-        D["g0"] = t(B, r[0], r[0], ENTRY_FILTERS)
-        D["dy0"] = t(B, r[0], r[0], ENTRY_FILTERS)
+        # forward activations (raw bf16) and backward buffers: shapes from models/memplan.py (the HBM planner
+        # prices exactly these)
+        shapes_a, shapes_d = buffer_shapes(B, S)
+        dt = {2: torch.int16, 1: torch.uint8, 4: torch.float32}
+        self.act = {n: t(*shp, dtype=dt[isz]) for n, (shp, isz) in shapes_a.items() if n != "h"}
+        self.h = t(*shapes_a["h"][0], dtype=torch.float32)
+        self.dg = {n: (t(*v[0], dtype=dt[v[1]]) if v else None) for n, v in shapes_d.items()}
         # replica rows for the small weight gradients every block adds into (depthwise kernels, entry conv):
         # [R][n] slabs summed into the flat gradient by ONE grad_finish launch at the end of backward, which
         # also applies the gradient copies (residual-conv bias grad == its BN's beta grad)
@@ -687,10 +647,6 @@ class UNetEngine:
         self.forward(False)
         p = torch.sigmoid(self.h)
         return p.repeat_interleave(2, 1).repeat_interleave(2, 2)
-
-
-def qres_of(k: int, Rk: int) -> int:
-    return Rk if k == 0 else Rk // 2
 
 
 class HipBackend:

@@ -22,6 +22,15 @@ def resolve_device(cfg: FLConfig) -> str:
     return "cuda" if torch.cuda.is_available() else "cpu"
 
 
+def planned_batch(cfg: FLConfig, device: str) -> int:
+    """batch_size=0: the HBM planner's batch for this image size (config 4, 512^2 large batch)."""
+    from ..models.memplan import plan_batch
+    hbm = None if device == "cuda" else 288 * 10**9
+    plan = plan_batch(cfg.img_size, hbm, cfg.hbm_fraction, cfg.synthetic_samples if cfg.data == "synthetic" else 0)
+    print(f"[memplan] {plan.as_dict()}", flush=True)
+    return plan.batch
+
+
 def make_dataset(cfg: FLConfig, rank: int = 0, device: str = "cpu") -> CrackDataset:
     if cfg.data == "folder":
         from ..data.folder import load_folder_dataset
@@ -38,6 +47,8 @@ def make_trainer(cfg: FLConfig, client: str = "client", rank: int = 0, table: Op
                  device: Optional[str] = None) -> LocalFit:
     table = table or ParamTable()
     device = device or resolve_device(cfg)
+    if cfg.batch_size <= 0:
+        cfg.batch_size = planned_batch(cfg, device)
     data = make_dataset(cfg, rank, device)
     if device == "cuda":
         from ..models.engine import HipBackend

@@ -229,6 +229,37 @@ def _engine_and_ref(S=64, B=2, seed=0):
     return table, eng, flat, x, y
 
 
+def test_memplan_matches_engine_allocation():
+    """models/memplan.py prices the engine: measured HBM after an eager 512^2 train step (activations, backward
+    buffers, slabs, split-K workspace) stays under the plan, and the per-batch growth matches the planned planes."""
+    import gc
+    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
+    from crack_detection_federatedlearning_grpc_amd.models import memplan as M
+    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table, S = ParamTable(), 512
+    data = make_synthetic_device(32, S, seed=5)
+    used = {}
+    for B in (8, 32):
+        gc.collect()
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        eng = UNetEngine(table, B, S)
+        eng.bind_data(data.images, data.masks)
+        eng.set_flat(table.init_flat(0))
+        eng.idx.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
+        eng.train_step(use_graph=False)
+        torch.cuda.synchronize()
+        used[B] = torch.cuda.memory_allocated() - base
+        m = eng.read_metrics("train")
+        assert 0 < m["loss"] < 10, m
+        assert used[B] <= M.engine_bytes(B, S), (B, used[B], M.engine_bytes(B, S))
+        del eng
+    grow = used[32] - used[8]
+    plan = M.activation_bytes(32, S) - M.activation_bytes(8, S)
+    assert 0.9 * plan <= grow <= 1.15 * plan, (grow, plan)
+
+
 def test_engine_gradients_match_fp32_reference():
     table, eng, flat, x, y = _engine_and_ref(S=128, B=4)
     eng._zero_step()
