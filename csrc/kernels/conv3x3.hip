@@ -10,7 +10,11 @@
 // The packed weights [N][K] (K = tap*Cin + c) stream through a register-staged double buffer per (chunk, tap)
 // K-step; the next chunk's halo is prefetched into registers during the current chunk's taps and written to the
 // second halo buffer before the chunk boundary, so each K-step costs one barrier.
-// Halo pixel stride is 40 bf16 (80 B): the 16 rows of a fragment read hit 16 distinct bank slots.
+// LDS images are dense (64 B per halo pixel / weight row) with an XOR swizzle of the four 16-byte channel quarters,
+// quarter q of row r stored at slot q ^ swz(r), swz(r) = (r >> 1) & 2: every ds_read_b128 lane group (16 lanes =
+// 16 consecutive rows, mixed quarters) then covers all 64 banks for ANY starting row - the tap shifts move the
+// start - and every ds_write_b128 group of 8 lanes (2 rows x 4 quarters) covers 32 banks. (A 40-bf16 padded
+// stride left 3-way conflicts on the shifted taps: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 45 %.)
 // Epilogue (bias, bf16, LDS-staged 16-byte stores, BN statistics) and split-K over input chunks (fp32 workspace
 // + splitk epilogue) are shared with conv_igemm.
 #include "common.h"
@@ -20,8 +24,11 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int BK = 32;          // channels per chunk (one K-step = one tap of one chunk)
-constexpr int LDH = BK + 8;     // halo pixel stride (bf16)
-constexpr int LDB = BK + 8;
+constexpr int LDH = BK;         // halo pixel stride (bf16), swizzled
+constexpr int LDB = BK;
+
+// bf16 offset of 16-byte quarter q of LDS row r in a swizzled dense image
+__device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r >> 1) & 2)) << 3); }
 
 // WB ("whole-chunk B"): the block stages all 9 taps' weight tiles of a chunk at once ([tap][n][LDB], single LDS
 // buffer, next chunk register-prefetched during the current chunk's 9 x FMxFN MFMAs): two barriers per CHUNK
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < HALO_CHUNKS) *reinterpret_cast<uint4*>(sH + ((size_t)buf * HP + (e >> 2)) * LDH + (e & 3) * 8) = rh[i];
+      if (e < HALO_CHUNKS) *reinterpret_cast<uint4*>(sH + buf * HP * LDH + swz_off(e >> 2, e & 3)) = rh[i];
     }
   };
   // ---- weight tile of K-step (chunk, tap): wt[n][tap*Cin + chunk*32 .. +32) ----
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < B_CHUNKS) *reinterpret_cast<uint4*>(sB + ((size_t)buf * BN_ + (e >> 2)) * LDB + (e & 3) * 8) = rb[i];
+      if (e < B_CHUNKS) *reinterpret_cast<uint4*>(sB + buf * BN_ * LDB + swz_off(e >> 2, e & 3)) = rb[i];
     }
   };
 
@@ -152,20 +159,20 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       const int e = tid + i * NT;
       if (BW_CHUNKS % NT == 0 || e < BW_CHUNKS) {
         const int tap = e / B_CHUNKS, w = e - tap * B_CHUNKS;
-        *reinterpret_cast<uint4*>(sB + ((size_t)tap * BN_ + (w >> 2)) * LDB + (w & 3) * 8) = rbw[i];
+        *reinterpret_cast<uint4*>(sB + swz_off(tap * BN_ + (w >> 2), w & 3)) = rbw[i];
       }
     }
   };
 
-  // per-lane fragment pixel coordinates within the tile
-  int fpy[FM], fpx[FM];
+  // per-lane fragment: halo row of tap (0,0) for each A fragment, B row, channel quarter
+  int fhp[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int pp = wm * TM + i * 16 + (lane & 15);
-    fpy[i] = pp / TW;
-    fpx[i] = pp % TW;
+    fhp[i] = (pp / TW) * HW + pp % TW;
   }
-  const int fk = (lane >> 4) * 8;
+  const int fq = lane >> 4;
+  const int brow = wn * TN + (lane & 15);
 
   f4v acc[FM][FN];
 #pragma unroll
@@ -193,10 +200,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
         s8v af[FM], bfg[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          af[i] = *reinterpret_cast<const s8v*>(sH + ((size_t)(fpy[i] + ky) * HW + fpx[i] + kx) * LDH + fk);
+          af[i] = *reinterpret_cast<const s8v*>(sH + swz_off(fhp[i] + ky * HW + kx, fq));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          bfg[j] = *reinterpret_cast<const s8v*>(sB + ((size_t)tap * BN_ + wn * TN + j * 16 + (lane & 15)) * LDB + fk);
+          bfg[j] = *reinterpret_cast<const s8v*>(sB + swz_off(tap * BN_ + brow + j * 16, fq));
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -234,10 +241,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       s8v af[FM], bfg[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const s8v*>(sH + ((size_t)hbuf * HP + (fpy[i] + ky) * HW + fpx[i] + kx) * LDH + fk);
+        af[i] = *reinterpret_cast<const s8v*>(sH + hbuf * HP * LDH + swz_off(fhp[i] + ky * HW + kx, fq));
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfg[j] = *reinterpret_cast<const s8v*>(sB + ((size_t)bbuf * BN_ + wn * TN + j * 16 + (lane & 15)) * LDB + fk);
+        bfg[j] = *reinterpret_cast<const s8v*>(sB + bbuf * BN_ * LDB + swz_off(brow + j * 16, fq));
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

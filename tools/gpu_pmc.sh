@@ -5,6 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out/pmc
+timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || echo "counter list failed"
 cd /tmp
 i=0
 while read -r counters; do

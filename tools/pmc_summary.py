@@ -20,7 +20,7 @@ dur = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     seen = set()
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         if "render_kernel" in k:
             continue
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
