@@ -48,6 +48,8 @@ class FLConfig:
     model_type: str = "unet"             # advertised in READY reply; client ignores it (as reference)
     aggregation: str = "weighted"        # weighted (n_k) | uniform (reference mean)
     data_plane: str = "grpc"             # grpc | rccl
+    rccl_timeout_s: float = 300.0        # collective timeout; on expiry / peer loss the client aborts the
+                                         # communicator and falls back to the gRPC data plane
     codec: str = "flat"                  # flat (safe, default) | pickle (reference wire format)
     wire_dtype: str = "fp32"             # fp32 | bf16 for the flat codec
 

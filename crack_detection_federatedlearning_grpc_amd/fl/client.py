@@ -7,6 +7,9 @@ loop { TRAIN_DONE -> RESP_ACY: poll VERSION until NOT_WAIT | RESP_ARY: TRAINING 
 * RPC deadlines + retry with backoff (reference has none, §5.3);
 * optional RCCL data plane: the weighted all-reduce runs between the clients on their GPUs
   (``parallel/rccl.py``); gRPC carries control only and rank 0 uploads the averaged model for the server's copy.
+  If a collective fails (a peer died, or ``rccl_timeout_s`` expired) every survivor aborts the communicator and
+  sends its local weights over gRPC instead; the server's round deadline + quorum then averages the survivors
+  (SURVEY §5.3).
 """
 from __future__ import annotations
 
@@ -54,6 +57,7 @@ class FLClient:
         self.phases: List[Dict] = []
         self.info: Dict[str, object] = {}
         self.final_state = ""
+        self.fallbacks = 0                      # RCCL -> gRPC data-plane fallbacks (peer loss)
 
     # -- transport helpers ---------------------------------------------------------------------------
     def _call(self, stub, req) -> "P.transportResponse":
@@ -143,10 +147,19 @@ class FLClient:
         arrays = self.trainer.get_weights()
         n = getattr(self.trainer, "n_samples", 0)
         if self.aggregator is not None:
-            arrays = self.aggregator.average(arrays, n)          # weighted all-reduce over RCCL
-            self.trainer.set_weights(arrays)                     # local model <- global average
-            if self.aggregator.rank != 0:
-                return b""
+            try:
+                avg = self.aggregator.average(arrays, n)         # weighted all-reduce over RCCL
+            except Exception as e:                               # peer lost / collective timed out
+                print(f"[{self.name}] RCCL aggregation failed ({type(e).__name__}: {e}); aborting the "
+                      f"communicator, falling back to the gRPC data plane")
+                self.aggregator.abort()
+                self.aggregator = None
+                self.fallbacks += 1
+            else:
+                self.trainer.set_weights(avg)                    # local model <- global average
+                if self.aggregator.rank != 0:
+                    return b""
+                arrays = avg
         if self.cfg.fault_corrupt:
             return b"\x80corrupt" + os.urandom(64)
         return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype)

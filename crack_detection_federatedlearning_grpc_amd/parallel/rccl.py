@@ -100,6 +100,9 @@ class RcclAggregator:
         self.rank, self.world = rank, world
         cuda = device is not None and device.type == "cuda"
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # blocking waits: a collective that cannot complete (dead peer) raises on the host after ``timeout_s``
+        # instead of the watchdog tearing the process down, so the client can fall back to gRPC (fl/client.py)
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
         if not dist.is_initialized():
             dist.init_process_group("nccl" if cuda else "gloo", init_method=f"tcp://{addr}:{port}", rank=rank,
                                     world_size=world, timeout=timedelta(seconds=timeout_s),
@@ -112,7 +115,7 @@ class RcclAggregator:
         if torch.cuda.is_available() and (cfg is None or cfg.device != "cpu"):
             dev = torch.device("cuda", torch.cuda.current_device())
         return cls(int(info.get("rank", 0)), int(info["world_size"]), str(info.get("dist_addr") or "127.0.0.1"),
-                   int(info["dist_port"]), dev)
+                   int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)))
 
     def average(self, arrays: Sequence[np.ndarray], n_local: float) -> List[np.ndarray]:
         shapes = [np.shape(a) for a in arrays]
@@ -125,6 +128,21 @@ class RcclAggregator:
             out.append(host[off:off + n].reshape(s).copy())
             off += n
         return out
+
+    def abort(self) -> None:
+        """A peer died or a collective timed out: tear the communicator down without a collective shutdown
+        (``ncclCommAbort`` under RCCL), so the surviving clients can carry on over gRPC."""
+        if not dist.is_initialized():
+            return
+        try:
+            from torch.distributed.distributed_c10d import _abort_process_group
+            _abort_process_group()
+        except Exception:
+            pass
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
 
     def close(self) -> None:
         if dist.is_initialized():

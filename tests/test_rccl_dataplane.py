@@ -51,3 +51,56 @@ def test_rccl_mode_two_processes(tmp_path):
     assert np.isclose(vals["c0"], 8.0) and np.isclose(vals["c1"], 8.0)
     e = table.entries[0]
     assert np.isclose(srv.state.global_flat[e.offset], 8.0)     # rank 0 uploaded the all-reduced model
+
+
+def _client_proc_faulty(port, name, delta, drop_round, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.client import FLClient
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+    from fakes import FakeTrainer
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=3, register_window_s=20, ready_stall_s=0,
+                   poll_period_s=0.05, long_poll_s=1.0, max_rounds=3, client_weight_file="", rpc_timeout_s=60,
+                   rccl_timeout_s=15.0, fault_drop_round=drop_round)
+    table = ParamTable()
+    tr = FakeTrainer(table, delta, n_samples=10)
+    c = FLClient(cfg, lambda: tr, name=name, target=f"127.0.0.1:{port}",
+                 aggregator_factory=lambda info: RcclAggregator.from_ready_info(info, cfg))
+    st = c.run()
+    q.put((name, st, c.fallbacks))
+
+
+def test_rccl_peer_loss_falls_back_to_grpc(tmp_path):
+    """a client dies after round 1; the survivors' round-2 collective fails, they abort the
+    communicator and send their local weights over gRPC; the round deadline + quorum averages the survivors."""
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=3, register_window_s=20, ready_stall_s=0,
+                   max_rounds=3, work_dir=str(tmp_path), server_weight_file="", long_poll_s=1.0,
+                   round_deadline_s=3.0, quorum=0.6)
+    srv = FLServer(cfg, global_flat=np.zeros(table.total, np.float32), table=table)
+    port = srv.start(0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    spec = [("c0", 1.0, 0), ("c1", 2.0, 0), ("c2", 4.0, 2)]
+    ps = [ctx.Process(target=_client_proc_faulty, args=(port, n, d, r, q)) for n, d, r in spec]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(30)
+    srv.stop()
+    assert sorted(n for n, _, _ in res) == ["c0", "c1"]
+    assert all(st == "FIN" and fb == 1 for _, st, fb in res), res
+    # round 1 over RCCL: (1+2+4)/3; round 2 over gRPC (survivors): mean of +1 / +2; round 3 likewise
+    r1 = 7.0 / 3.0
+    r2 = r1 + 1.5
+    r3 = r2 + 1.5
+    e = table.entries[0]
+    assert np.isclose(srv.state.global_flat[e.offset], r3, atol=1e-5)
+    assert [h.dropped for h in srv.state.history] == [[], ["c2"], ["c2"]]
