@@ -19,6 +19,7 @@ Layouts: activations NHWC bf16; master weights, grads, Adam moments fp32 in one 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -75,6 +76,8 @@ class UNetEngine:
         self.eval_metrics = torch.zeros(8, dtype=torch.float64, device=dev)
         self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
+        # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
+        self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
         self._build_pack()
         self._alloc()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -316,7 +319,8 @@ class UNetEngine:
         return b["ab"]
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
-               pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None) -> None:
+               pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
+               join: Optional[Dict[str, object]] = None) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
 
         ``node`` = (y, bn, relu): the output is the incoming gradient of that BN node; the kernel's epilogue writes
@@ -331,15 +335,18 @@ class UNetEngine:
         if node is not None:
             ny, bn, nrelu = node
             kw = dict(node_y=ny, node_ab=bn["ab"], node_sums=bn["sums"], node_reps=self.RS, node_relu=nrelu)
+        if join:
+            kw.update(join)
         self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                           pad_l, self.ws if need > 1 else None, **kw)
 
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
-              Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor]) -> None:
+              Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor],
+              join: Optional[Dict[str, object]] = None) -> None:
         pad = (ks - 1) // 2 if stride == 1 else 0
         B = self.B
         self._igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
-                          N, ks, stride, pad, pad)
+                    N, ks, stride, pad, pad, join=join)
 
     def forward(self, train: bool = True) -> None:
         C, B, r, A = self.C, self.B, self.r, self.act
@@ -361,8 +368,13 @@ class UNetEngine:
             self._conv(Lazy(A[f"e{k}_d2"], None, 0, H, F), s2, PK_PW, A[f"e{k}_y2"], F, 1, 1, 0, H,
                        self.P(s2, "bias"), self.bn[b2]["stats"] if train else None)
             ab2 = self._bn_final(b2, train)
-            self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None)
-            C.pool_res_fwd(A[f"e{k}_y2"], ab2, A[f"e{k}_res"], A[f"e{k}_x"], A[f"e{k}_am"], B, H, H, F)
+            if self.fuse_join:   # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
+                self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
+                           join=dict(join_mode=C.JOIN_POOL, join_y=A[f"e{k}_y2"], join_ab=ab2,
+                                     join_out=A[f"e{k}_x"], join_argmax=A[f"e{k}_am"], join_H=H, join_W=H))
+            else:
+                self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None)
+                C.pool_res_fwd(A[f"e{k}_y2"], ab2, A[f"e{k}_res"], A[f"e{k}_x"], A[f"e{k}_am"], B, H, H, F)
             x = Lazy(A[f"e{k}_x"], None, 0, H // 2, F)
         prev = x                                             # x3 at r[3]
         for k, F in enumerate(DEC_FILTERS):
@@ -375,8 +387,13 @@ class UNetEngine:
             self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
                         self.P(t2, "bias"), self.bn[b2]["stats"] if train else None)
             abB = self._bn_final(b2, train)
-            self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
-            C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
+            if self.fuse_join:   # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
+                self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None,
+                           join=dict(join_mode=C.JOIN_ADD_UP if up else C.JOIN_ADD, join_y=A[f"d{k}_c2"],
+                                     join_ab=abB, join_out=A[f"d{k}_xlo"], join_H=Rk, join_W=Rk))
+            else:
+                self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
+                C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
             prev = Lazy(A[f"d{k}_xlo"], None, 0, Rk, F)
         hl = next(n)
         C.head_fwd(prev.t, self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,

@@ -58,7 +58,8 @@ BnNodeEpi node_epi_args(const OptT& node_y, const OptT& node_ab, const OptT& nod
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
-                   int node_relu) {
+                   int node_relu, int join_mode, OptT join_y, OptT join_ab, OptT join_out, OptT join_argmax,
+                   int join_H, int join_W) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -79,6 +80,28 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
   p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, y.numel(), N);
   TORCH_CHECK(!p.node.y || (!p.stats && !p.bias), "conv_igemm: the node epilogue excludes stats and bias");
+  if (join_mode) {
+    TORCH_CHECK(join_mode >= JOIN_POOL && join_mode <= JOIN_ADD_UP && join_y && join_ab && join_out,
+                "conv_igemm: join needs join_y, join_ab, join_out");
+    TORCH_CHECK(ks == 1 && !p.stats && !p.node.y && N % 8 == 0, "conv_igemm: joins are for 1x1 convs without stats");
+    const int64_t yn = (int64_t)B * join_H * join_W * N;
+    TORCH_CHECK(join_y->numel() == yn && join_ab->numel() >= 4 * N, "conv_igemm: join_y / join_ab size");
+    if (join_mode == JOIN_POOL) {
+      TORCH_CHECK(Ho == (join_H + 1) / 2 && Wo == (join_W + 1) / 2 && join_argmax &&
+                  join_out->numel() == (int64_t)p.M * N && join_argmax->numel() == (int64_t)p.M * N,
+                  "conv_igemm: pool join shapes");
+    } else {
+      const int u = join_mode == JOIN_ADD_UP ? 2 : 1;
+      TORCH_CHECK(join_H == u * Ho && join_W == u * Wo && join_out->numel() == yn, "conv_igemm: add join shapes");
+    }
+    p.join.mode = join_mode;
+    p.join.y = ptr<const bf16_t>(*join_y, "join_y");
+    p.join.ab = ptr<const float>(*join_ab, "join_ab");
+    p.join.out = ptr<bf16_t>(*join_out, "join_out");
+    p.join.argmax = optr<uint8_t>(join_argmax, "join_argmax");
+    p.join.H = join_H;
+    p.join.W = join_W;
+  }
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
@@ -217,6 +240,7 @@ at::Tensor make_bn_moving_table(std::vector<std::tuple<at::Tensor, at::Tensor, a
     b.mmean = ptr<float>(std::get<1>(l), "mmean");
     b.mvar = ptr<float>(std::get<2>(l), "mvar");
     b.C = std::get<3>(l);
+    TORCH_CHECK(b.C > 0 && b.C <= 1024 && 1024 % b.C == 0, "bn moving table: C must divide 1024");
     b.count = (float)std::get<4>(l);
     h.push_back(b);
   }
@@ -504,7 +528,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"),
         py::arg("pad_l"), py::arg("ws") = py::none(), py::arg("algo") = 0, py::arg("node_y") = py::none(),
         py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,
-        py::arg("node_relu") = 1);
+        py::arg("node_relu") = 1, py::arg("join_mode") = 0, py::arg("join_y") = py::none(),
+        py::arg("join_ab") = py::none(), py::arg("join_out") = py::none(), py::arg("join_argmax") = py::none(),
+        py::arg("join_H") = 0, py::arg("join_W") = 0);
+  m.attr("JOIN_POOL") = (int)JOIN_POOL;
+  m.attr("JOIN_ADD") = (int)JOIN_ADD;
+  m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
   m.def("conv_splits", &conv_splits_op);
   m.def("conv_wgrad", &conv_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),

@@ -14,23 +14,47 @@ namespace {
 
 constexpr int NT = 256;
 
-__global__ void bn_finalize_kernel(const float* stats, const float* gamma, const float* beta, const float* mmean,
-                                   const float* mvar, float* ab, int C, float count, float eps, int train) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float mean, var;
-    if (train) {
-      float s = 0.f, s2 = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < STAT_REPLICAS; ++r) {
-        s += stats[r * 2 * C + c];
-        s2 += stats[r * 2 * C + C + c];
-      }
-      mean = s / count;
-      var = fmaxf(s2 / count - mean * mean, 0.f);
-    } else {
-      mean = mmean[c];
-      var = mvar[c];
+// Replica-row reduction shared by the finalize / moving-statistics kernels: FT threads, thread -> (channel c,
+// replica phase j), FT / C threads per channel, so every one of the STAT_REPLICAS * 2 loads of a channel is issued
+// in ONE round (the 1-block kernel is latency-bound: a per-thread serial walk over 32 replicas took ~5 us).
+constexpr int FT = 1024;
+
+// sums of channel threadIdx.x (valid for threadIdx.x < C after the call) into (s, s2)
+__device__ __forceinline__ void replica_sums(const float* stats, int C, float (*part)[FT], float& s, float& s2) {
+  const int per = FT / C, c = threadIdx.x % C, j = threadIdx.x / C;
+  float a = 0.f, b = 0.f;
+#pragma unroll 4
+  for (int r = j; r < STAT_REPLICAS; r += per) {
+    a += stats[r * 2 * C + c];
+    b += stats[r * 2 * C + C + c];
+  }
+  part[0][threadIdx.x] = a;
+  part[1][threadIdx.x] = b;
+  __syncthreads();
+  s = s2 = 0.f;
+  if (threadIdx.x < C)
+    for (int k = 0; k < per; ++k) {
+      s += part[0][k * C + threadIdx.x];
+      s2 += part[1][k * C + threadIdx.x];
     }
+}
+
+__global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, const float* gamma, const float* beta,
+                                                         const float* mmean, const float* mvar, float* ab, int C,
+                                                         float count, float eps, int train) {
+  __shared__ float part[2][FT];
+  const int c = threadIdx.x;
+  float mean = 0.f, var = 0.f;
+  if (train) {
+    float s, s2;
+    replica_sums(stats, C, part, s, s2);
+    mean = s / count;
+    var = fmaxf(s2 / count - mean * mean, 0.f);
+  } else if (c < C) {
+    mean = mmean[c];
+    var = mvar[c];
+  }
+  if (c < C) {
     const float rstd = rsqrtf(var + eps);
     const float a = gamma[c] * rstd;
     ab[c] = a;
@@ -40,14 +64,13 @@ __global__ void bn_finalize_kernel(const float* stats, const float* gamma, const
   }
 }
 
-__global__ void bn_moving_kernel(const BnMoving* layers, float momentum) {
+__global__ __launch_bounds__(FT) void bn_moving_kernel(const BnMoving* layers, float momentum) {
+  __shared__ float part[2][FT];
   const BnMoving L = layers[blockIdx.x];
-  for (int c = threadIdx.x; c < L.C; c += blockDim.x) {
-    float s = 0.f, s2 = 0.f;
-    for (int r = 0; r < STAT_REPLICAS; ++r) {
-      s += L.stats[r * 2 * L.C + c];
-      s2 += L.stats[r * 2 * L.C + L.C + c];
-    }
+  float s, s2;
+  replica_sums(L.stats, L.C, part, s, s2);
+  const int c = threadIdx.x;
+  if (c < L.C) {
     const float mean = s / L.count;
     const float var = fmaxf(s2 / L.count - mean * mean, 0.f);
     const float unbiased = var * (L.count / fmaxf(L.count - 1.f, 1.f));
@@ -266,14 +289,15 @@ bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
 int bn_finalize(const float* stats, const float* gamma, const float* beta, const float* mmean, const float* mvar,
                 float* ab, int C, float count, float eps, int train, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(256), 0, st, stats, gamma, beta, mmean, mvar, ab, C, count,
+  if (C < 1 || C > FT || FT % C) return 1;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(FT), 0, st, stats, gamma, beta, mmean, mvar, ab, C, count,
                      eps, train);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float momentum, hipStream_t st) {
-  (void)max_c;
-  hipLaunchKernelGGL(bn_moving_kernel, dim3(n_layers), dim3(256), 0, st, d_layers, momentum);
+  (void)max_c;                                 // every layer's C divides FT (checked when the table is built)
+  hipLaunchKernelGGL(bn_moving_kernel, dim3(n_layers), dim3(FT), 0, st, d_layers, momentum);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -29,7 +29,68 @@ constexpr int BK = 32;
 constexpr int LDK = BK + 8;   // padded LDS row (bf16 elements)
 constexpr int NT = 256;
 
-template <int BM_, int BN_, int WM, int WN>
+// Residual join (ConvJoin) of output pixel m, channels c..c+7, given the rounded conv output r (bias included).
+CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv) {
+  const ConvJoin& J = p.join;
+  float r[8], a[8], bb[8];
+  unpack8(rv, r);
+  load_f8(J.ab + c, a);
+  load_f8(J.ab + p.N + c, bb);
+  const int hw = p.Ho * p.Wo;
+  const int b = m / hw, rem = m - b * hw, oh = rem / p.Wo, ow = rem - oh * p.Wo;
+  if (J.mode == JOIN_POOL) {            // TF same 3x3/s2 window: rows 2*oh .. 2*oh+2 clipped at the bottom/right
+    float mx[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mx[j] = -INFINITY;
+      am[j] = 0;
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int ih = 2 * oh + ky;
+      if (ih >= J.H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iw = 2 * ow + kx;
+        if (iw >= J.W) continue;
+        float f[8];
+        load8(J.y + ((size_t)(b * J.H + ih) * J.W + iw) * p.N + c, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = fmaf(a[j], f[j], bb[j]);
+          if (v > mx[j]) {
+            mx[j] = v;
+            am[j] = ky * 3 + kx;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx[j] += r[j];
+    const size_t o = (size_t)m * p.N + c;
+    *reinterpret_cast<uint4*>(J.out + o) = pack8(mx);
+    uint2 packed;
+    packed.x = (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
+    packed.y = (uint32_t)am[4] | ((uint32_t)am[5] << 8) | ((uint32_t)am[6] << 16) | ((uint32_t)am[7] << 24);
+    *reinterpret_cast<uint2*>(J.argmax + o) = packed;
+  } else {
+    const int up = J.mode == JOIN_ADD_UP;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (d > 0 && !up) break;
+      const int h = (oh << up) + (d >> 1), w = (ow << up) + (d & 1);
+      const size_t o = ((size_t)(b * J.H + h) * J.W + w) * p.N + c;
+      float y[8];
+      load8(J.y + o, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = fmaf(a[j], y[j], bb[j]) + r[j];
+      *reinterpret_cast<uint4*>(J.out + o) = pack8(y);
+    }
+  }
+}
+
+template <int BM_, int BN_, int WM, int WN, bool JN = false>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_per_split, float* __restrict__ ws) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM_ / WM, TN = BN_ / WN;
@@ -220,6 +281,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
     if (m < p.M) {
       const size_t off = (size_t)m * p.N + nBlock + cg * 8;
       uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      if constexpr (JN) {                       // fused residual join: the conv output itself is not stored
+        join_store(p, m, nBlock + cg * 8, v);
+        continue;
+      }
       if (node) {
         v = node_epi(v, p.node.y + off, nk, p.node.relu, s, s2);
       } else if (p.stats) {
@@ -330,7 +395,10 @@ void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
   const int KT = p.K / BK;
   const int per = (KT + splits - 1) / splits;
   dim3 grid((p.M + BM_ - 1) / BM_, p.N / BN_, splits);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? ws : nullptr);
+  if (p.join.mode)   // separate instantiation: the join epilogue's registers must not cost the plain convs occupancy
+    hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN, true>), grid, dim3(NT), 0, st, p, per, nullptr);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? ws : nullptr);
 }
 
 }  // namespace
@@ -364,6 +432,7 @@ int conv_igemm_splits(const ConvParams& p) {
 
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
+  if (p.join.mode && (p.ks != 1 || p.stats || p.node.y || p.N % 8)) return 5;   // joins: 1x1 residual convs only
   if (use3x3(p)) {                       // halo-tile kernel for every 3x3 / stride-1 conv (conv3x3.hip)
     const int rc = conv3x3(p, st);
     if (rc > 0) return rc;
@@ -376,7 +445,7 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   if (p.algo == 2) return 4;
-  int splits = conv_igemm_splits(p);
+  int splits = p.join.mode ? 1 : conv_igemm_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const int cfg = cfl_tune(TUNE_IGEMM_CFG);
   if (cfg > 0) {                           // forced tile (micro-benchmark sweeps); must divide N

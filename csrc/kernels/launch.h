@@ -23,6 +23,21 @@ struct BnNodeEpi {
   int relu;
 };
 
+// Fused residual join in the epilogue of a forward 1x1 residual conv (its output r never goes to memory):
+//   JOIN_POOL   out[m] = maxpool3x3s2_same(a*y + b)[m] + r[m], argmax recorded   (encoder, replaces pool_res_fwd)
+//   JOIN_ADD    out[m] = a*y[m] + b + r[m]                                        (decoder level 0, bn_add_fwd)
+//   JOIN_ADD_UP out[p] = a*y[p] + b + r[p/2] for the 4 pixels p of each conv pixel (decoder, bn_add_fwd q_up)
+// y: the BN input at resolution H x W; ab: its BN coefficients (C = N rows).
+enum { JOIN_NONE = 0, JOIN_POOL = 1, JOIN_ADD = 2, JOIN_ADD_UP = 3 };
+struct ConvJoin {
+  int mode;
+  const bf16_t* y;
+  const float* ab;
+  bf16_t* out;
+  uint8_t* argmax;         // JOIN_POOL only
+  int H, W;
+};
+
 struct ConvParams {
   const bf16_t* x;     // [B, Hin, Win, Cin] NHWC (physical; logical = upsample2 if up_in)
   const bf16_t* wt;    // [N][K] packed bf16 weights, K = ks*ks*Cin, k = (ky*ks + kx)*Cin + ci
@@ -37,6 +52,7 @@ struct ConvParams {
   int64_t ws_elems;
   int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
   BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
+  ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)

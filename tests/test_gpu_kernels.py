@@ -706,3 +706,42 @@ def test_ops_autograd_layers_match_torch():
     (yr * gy).sum().backward()
     assert rel(y.float().cpu(), yr.detach()) < 1e-2
     assert rel(xb.grad.float().cpu(), xr.grad) < 2e-2 and rel(w.grad.cpu(), wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("mode,H,Cin,N,B", [("pool", 16, 32, 64, 2), ("pool", 15, 64, 128, 1), ("add", 8, 256, 256, 2),
+                                           ("add_up", 16, 64, 32, 2), ("add_up", 8, 128, 64, 3)])
+def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
+    """conv_igemm residual-join epilogue (max-pool(BN(y)) + conv / BN(y) + conv / BN(y) + up2(conv)) is
+    bit-identical to the separate conv + pool_res_fwd / bn_add_fwd launches it replaces."""
+    C_ = hip()
+    torch.manual_seed(11)
+    stride = 2 if mode == "pool" else 1
+    Hx = H if mode == "pool" else (H // 2 if mode == "add_up" else H)     # conv input resolution
+    Ho = (H + 1) // 2 if mode == "pool" else Hx
+    xb, _ = bf(torch.randn(B, Hx, Hx, Cin))
+    wb = pack(PK_CONV, torch.randn(1, 1, Cin, N) * 0.1, 1, Cin, N)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    yb, _ = bf(torch.randn(B, H, H, N))
+    ab, _, _ = ab_for(N, 12)
+    ab = ab.to(DEV)
+    r = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
+    C_.conv_igemm(xb, wb, bias, r, None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0, 0)
+    if mode == "pool":
+        ref = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
+        am_ref = torch.zeros(B, Ho, Ho, N, dtype=torch.uint8, device=DEV)
+        C_.pool_res_fwd(yb, ab, r, ref, am_ref, B, H, H, N)
+        out = torch.zeros_like(ref)
+        am = torch.zeros_like(am_ref)
+        C_.conv_igemm(xb, wb, bias, torch.zeros_like(r), None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0,
+                      0, join_mode=C_.JOIN_POOL, join_y=yb, join_ab=ab, join_out=out, join_argmax=am, join_H=H,
+                      join_W=H)
+        assert torch.equal(am, am_ref)
+    else:
+        up = 1 if mode == "add_up" else 0
+        ref = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+        C_.bn_add_fwd(yb, ab, r, up, ref, B, H, H, N)
+        out = torch.zeros_like(ref)
+        C_.conv_igemm(xb, wb, bias, torch.zeros_like(r), None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0,
+                      0, join_mode=C_.JOIN_ADD_UP if up else C_.JOIN_ADD, join_y=yb, join_ab=ab, join_out=out,
+                      join_H=H, join_W=H)
+    assert torch.equal(out, ref), int((out != ref).sum())
