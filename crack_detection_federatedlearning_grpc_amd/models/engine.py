@@ -247,6 +247,10 @@ class UNetEngine:
         spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:8]]
         self.zero_table = self.C.make_zero_table(spans)
         self.n_zero, self.max_zero = len(spans), max(t.numel() * t.element_size() for t in spans)
+        # inference BN coefficients of every layer (one launch per eval forward)
+        self.eval_table = self.C.make_bn_eval_table([
+            (self.P(n, "gamma"), self.P(n, "beta"), self.P(n, "moving_mean"), self.P(n, "moving_variance"),
+             self.bn[n]["ab"], self.bn[n]["C"]) for n in self.bn_names], self.bn_eps)
         # BN moving-stat table
         self.moving_table = self.C.make_bn_moving_table([
             (self.bn[n]["stats"], self.P(n, "moving_mean"), self.P(n, "moving_variance"), self.bn[n]["C"],
@@ -313,6 +317,8 @@ class UNetEngine:
     # ------------------------------------------------------------------------------------------------ schedule
     def _bn_final(self, name: str, train: bool) -> torch.Tensor:
         b = self.bn[name]
+        if not train:
+            return b["ab"]                     # inference: all coefficients written by forward()'s bn_eval_coefs
         self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
                            self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
                            float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
@@ -350,6 +356,10 @@ class UNetEngine:
 
     def forward(self, train: bool = True) -> None:
         C, B, r, A = self.C, self.B, self.r, self.act
+        if not train:                          # every BN's inference coefficients in one launch
+            if self._pending:
+                self._await_all()
+            C.bn_eval_coefs(self.eval_table, len(self.bn_names))
         n = iter(self.names)
         e_conv, e_bn = next(n), next(n)
         st = self.bn[e_bn]["stats"] if train else None

@@ -249,6 +249,33 @@ at::Tensor make_bn_moving_table(std::vector<std::tuple<at::Tensor, at::Tensor, a
   return cpu.to(dev);
 }
 
+// layers: list of (gamma, beta, moving_mean, moving_var, ab, C) -> device table (uint8 tensor)
+at::Tensor make_bn_eval_table(std::vector<std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, int>> layers,
+                              double eps) {
+  std::vector<BnEval> h;
+  at::Device dev = std::get<0>(layers.at(0)).device();
+  for (auto& l : layers) {
+    BnEval b{};
+    b.gamma = ptr<const float>(std::get<0>(l), "gamma");
+    b.beta = ptr<const float>(std::get<1>(l), "beta");
+    b.mmean = ptr<const float>(std::get<2>(l), "mmean");
+    b.mvar = ptr<const float>(std::get<3>(l), "mvar");
+    b.ab = ptr<float>(std::get<4>(l), "ab");
+    b.C = std::get<5>(l);
+    TORCH_CHECK(std::get<4>(l).numel() >= 4 * b.C && std::get<0>(l).numel() == b.C, "bn eval table: sizes");
+    b.eps = (float)eps;
+    h.push_back(b);
+  }
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(BnEval))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(BnEval));
+  return cpu.to(dev);
+}
+
+void bn_eval_coefs_op(at::Tensor table, int n_layers) {
+  TORCH_CHECK(table.numel() == (int64_t)n_layers * (int64_t)sizeof(BnEval), "bn_eval_coefs: table size");
+  ok(bn_eval_coefs(ptr<const BnEval>(table, "table"), n_layers, stream()), "bn_eval_coefs");
+}
+
 void bn_moving_update_op(at::Tensor table, int n_layers, double momentum) {
   TORCH_CHECK(table.numel() == (int64_t)n_layers * (int64_t)sizeof(BnMoving), "bn_moving_update: table size");
   ok(bn_moving_update(ptr<const BnMoving>(table, "table"), n_layers, 0, (float)momentum, stream()), "bn_moving_update");
@@ -571,6 +598,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);
+  m.def("make_bn_eval_table", &make_bn_eval_table);
+  m.def("bn_eval_coefs", &bn_eval_coefs_op);
   m.def("node_bwd", &node_bwd_op, py::arg("src0"), py::arg("mode0"), py::arg("mask0"), py::arg("src1"),
         py::arg("mode1"), py::arg("mask1"), py::arg("argmax"), py::arg("v"), py::arg("ab"), py::arg("relu_node"),
         py::arg("out"), py::arg("sums"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"),

@@ -64,6 +64,18 @@ __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, con
   }
 }
 
+__global__ __launch_bounds__(256) void bn_eval_kernel(const BnEval* layers) {
+  const BnEval L = layers[blockIdx.x];
+  for (int c = threadIdx.x; c < L.C; c += blockDim.x) {
+    const float rstd = rsqrtf(L.mvar[c] + L.eps);
+    const float a = L.gamma[c] * rstd;
+    L.ab[c] = a;
+    L.ab[L.C + c] = L.beta[c] - L.mmean[c] * a;
+    L.ab[2 * L.C + c] = L.mmean[c];
+    L.ab[3 * L.C + c] = rstd;
+  }
+}
+
 __global__ __launch_bounds__(FT) void bn_moving_kernel(const BnMoving* layers, float momentum) {
   __shared__ float part[2][FT];
   const BnMoving L = layers[blockIdx.x];
@@ -298,6 +310,11 @@ int bn_finalize(const float* stats, const float* gamma, const float* beta, const
 int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float momentum, hipStream_t st) {
   (void)max_c;                                 // every layer's C divides FT (checked when the table is built)
   hipLaunchKernelGGL(bn_moving_kernel, dim3(n_layers), dim3(FT), 0, st, d_layers, momentum);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int bn_eval_coefs(const BnEval* d_layers, int n_layers, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3(n_layers), dim3(256), 0, st, d_layers);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -140,6 +140,18 @@ struct BnMoving {          // one BatchNorm layer for the moving-statistics upda
 };
 int bn_moving_update(const BnMoving* d_layers, int n_layers, int max_c, float momentum, hipStream_t st);
 
+struct BnEval {             // one BatchNorm layer's inference coefficients (moving statistics)
+  const float* gamma;
+  const float* beta;
+  const float* mmean;
+  const float* mvar;
+  float* ab;               // [4][C]
+  int C;
+  float eps;
+};
+// every layer's ab from its moving statistics in ONE launch (blockIdx = layer): an inference forward needs them all
+int bn_eval_coefs(const BnEval* d_layers, int n_layers, hipStream_t st);
+
 enum GradMode { GM_NONE = 0, GM_SAME = 1, GM_SCATTER2 = 2, GM_SUM2X2 = 3, GM_MAXPOOL = 4 };
 struct GradSrc {
   const bf16_t* p;
