@@ -44,6 +44,8 @@ __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, con
                                                          float count, float eps, int train) {
   __shared__ float part[2][FT];
   const int c = threadIdx.x;
+  // every load this thread needs is issued before the replica reduction (one memory round trip, not two)
+  const float gm = c < C ? gamma[c] : 0.f, bt = c < C ? beta[c] : 0.f;
   float mean = 0.f, var = 0.f;
   if (train) {
     float s, s2;
@@ -56,9 +58,9 @@ __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, con
   }
   if (c < C) {
     const float rstd = rsqrtf(var + eps);
-    const float a = gamma[c] * rstd;
+    const float a = gm * rstd;
     ab[c] = a;
-    ab[C + c] = beta[c] - mean * a;
+    ab[C + c] = bt - mean * a;
     ab[2 * C + c] = mean;
     ab[3 * C + c] = rstd;
   }

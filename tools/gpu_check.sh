@@ -17,4 +17,5 @@ rm -rf $R/gpurun_out/pmc/p3; mkdir -p $R/gpurun_out/pmc
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE \
     --output-format csv -d $R/gpurun_out/pmc/p3 -o run -- python $R/bench.py --profile-steps 6 > $R/gpurun_out/pmc/p3.log 2>&1 \
     || { tail -5 $R/gpurun_out/pmc/p3.log; exit 1; }
+timeout -k 10 120 python $R/tools/graph_floor.py || exit 1
 echo done
