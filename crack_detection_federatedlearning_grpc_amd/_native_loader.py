@@ -39,4 +39,8 @@ def hip():
                     _build.build_hip(verbose=True)
                 import torch  # noqa: F401  (libtorch must be loaded before _C)
                 _hip = importlib.import_module(__package__ + "._C")
+                # launch-shape knobs for A/B runs: CFL_TUNE="9=1,3=256" (launch.h TuneKey = value)
+                for kv in filter(None, os.environ.get("CFL_TUNE", "").split(",")):
+                    k, v = kv.split("=")
+                    _hip.set_tune(int(k), int(v))
     return _hip

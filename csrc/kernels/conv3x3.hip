@@ -365,7 +365,20 @@ static bool use_wb(const ConvParams& p) {
   return v == 0 ? true : v == 1;           // 0 = default (whole-chunk B, BN <= 64), 2 = per-tap B (BN up to 128)
 }
 
+// Low-M layers (the 16x16 maps at 256^2: 4096 pixels, K up to 2304): rather than split K over a fp32 workspace and
+// a second epilogue launch, cut the output into 8x8-pixel x 32-channel tiles - enough blocks without a K split.
+static bool small_tiles(const ConvParams& p) {
+  const int v = cfl_tune(TUNE_CONV3_SMALL);
+  if (v == 1 || !use_wb(p) || p.N % 32 || p.Ho < 8 || p.Wo < 8) return false;
+  if (v == 2) return true;
+  const int tw = p.Wo >= 16 ? 16 : 8, th = 128 / tw, bn = p.N >= 64 ? 64 : p.N;
+  const int blocks = ((p.Ho + th - 1) / th) * ((p.Wo + tw - 1) / tw) * p.B * (p.N / bn);
+  const int small = ((p.Ho + 7) / 8) * ((p.Wo + 7) / 8) * p.B * (p.N / 32);
+  return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
+}
+
 int conv3x3_splits(const ConvParams& p) {
+  if (small_tiles(p)) return 1;
   const int tw = p.Wo >= 16 ? 16 : 8;
   const int th = 128 / tw;
   const int bn = use_wb(p) ? (p.N >= 64 ? 64 : p.N) : (p.N >= 128 ? 128 : p.N);
@@ -388,7 +401,9 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   int splits = conv3x3_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const bool w16 = p.Wo >= 16;
-  if (use_wb(p) && p.N % 64 == 0) {
+  if (small_tiles(p)) {
+    splits = launch<8, 8, 32, 2, 2, true>(p, 1, st);
+  } else if (use_wb(p) && p.N % 64 == 0) {
     if (w16) splits = launch<8, 16, 64, 2, 2, true>(p, splits, st);
     else splits = launch<16, 8, 64, 2, 2, true>(p, splits, st);
   } else if (use_wb(p)) {

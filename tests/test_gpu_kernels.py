@@ -394,6 +394,7 @@ def test_conv_igemm_split_k_with_stats():
     (2, 8, 32, 64, 1, False),     # upsampled input, 16x16 output
     (4, 8, 256, 256, 0, True),    # deep layer: split-K over input chunks, TW 8
     (2, 12, 128, 128, 0, True),   # ragged tiles (12 not a multiple of 8/16)
+    (16, 16, 256, 256, 0, True),  # the 16x16 decoder level at batch 16: 8x8x32 tiles instead of split-K
 ])
 def test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab):
     torch.manual_seed(11)
@@ -745,3 +746,14 @@ def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
                       0, join_mode=C_.JOIN_ADD_UP if up else C_.JOIN_ADD, join_y=yb, join_ab=ab, join_out=out,
                       join_H=H, join_W=H)
     assert torch.equal(out, ref), int((out != ref).sum())
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [(2, 12, 64, 32, 0, True), (3, 6, 128, 64, 1, False),
+                                                  (2, 16, 256, 128, 0, True)])
+def test_conv3x3_small_tiles_forced(B, Hs, Cin, N, up, use_ab):
+    """TUNE_CONV3_SMALL=2 forces the 8x8-pixel x 32-channel tile variant on ragged / upsampled / deep shapes."""
+    hip().set_tune(hip().TUNE_CONV3_SMALL, 2)
+    try:
+        test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
+    finally:
+        hip().set_tune(hip().TUNE_CONV3_SMALL, 0)
