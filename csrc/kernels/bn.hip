@@ -227,18 +227,39 @@ constexpr int BBA_IPT = 4;
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
   __shared__ float ssum[2 * 256];
+  __shared__ float part[NT];
   const int G = p.C >> 3, lg = ilog2(G);
   const float invM = 1.f / (float)p.M;
   const int total = p.M << lg;
+  // grid stride is a multiple of G, so a thread's channel group never changes
+  const int c0 = (threadIdx.x & (G - 1)) * 8;
+  const int S = gridDim.x * NT;
+  // the first BBA_IPT items and the BN coefficients are loaded BEFORE the replica reduction below, so their latency
+  // overlaps it (the low-resolution layers run one iteration per thread: prologue and loads were two serial
+  // memory round trips)
+  float a[8], mean[8], rstd[8], g[BBA_IPT][8], y[BBA_IPT][8];
+  load_f8(p.ab + c0, a);
+  load_f8(p.ab + 2 * p.C + c0, mean);
+  load_f8(p.ab + 3 * p.C + c0, rstd);
+  auto load_items = [&](int t0) {
+#pragma unroll
+    for (int u = 0; u < BBA_IPT; ++u) {
+      const int t = t0 + u * S;
+      const size_t m = (size_t)(t < total ? t : (t0 < total ? t0 : 0)) >> lg;   // clamped: loads unconditional
+      load8(p.g + m * p.C + c0, g[u]);
+      load8(p.y + m * p.C + c0, y[u]);
+    }
+  };
+  int t0 = blockIdx.x * NT + threadIdx.x;
+  load_items(t0);
   // sum the node_bwd replica rows [reps][2][C] once per block (L2-resident, 2*C*reps floats)
   // (all threads load in parallel: thread -> (element, replica subset), partials combined through LDS)
-  __shared__ float part[NT];
   const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
   const int C2 = 2 * p.C;                                  // power of two (C / 8 is)
   if (C2 <= NT) {
-    const int per = NT / C2, e = threadIdx.x & (C2 - 1), j = threadIdx.x / C2;
+    const int per = NT / C2, e = threadIdx.x & (C2 - 1), jj = threadIdx.x / C2;
     float v = 0.f;
-    for (int r = j; r < reps; r += per) v += p.sums[(size_t)r * C2 + e];
+    for (int r = jj; r < reps; r += per) v += p.sums[(size_t)r * C2 + e];
     part[threadIdx.x] = v;
     __syncthreads();
     if (threadIdx.x < C2) {
@@ -260,40 +281,27 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
       if (p.dgamma) p.dgamma[c] = ssum[p.C + c];
     }
   }
-  // grid stride is a multiple of G, so a thread's channel group never changes
-  const int c0 = (threadIdx.x & (G - 1)) * 8;
-  float a[8], mean[8], rstd[8], k1[8], k2[8];
-  load_f8(p.ab + c0, a);
-  load_f8(p.ab + 2 * p.C + c0, mean);
-  load_f8(p.ab + 3 * p.C + c0, rstd);
+  float k1[8], k2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    k1[j] = ssum[c0 + j] * invM;
-    k2[j] = ssum[p.C + c0 + j] * invM;
+  for (int jj = 0; jj < 8; ++jj) {
+    k1[jj] = ssum[c0 + jj] * invM;
+    k2[jj] = ssum[p.C + c0 + jj] * invM;
   }
   // BBA_IPT items per thread per iteration, all loads issued before any math (memory-level parallelism: the small
   // layers launch few blocks, so one item in flight per thread would leave HBM latency-bound)
-  const int S = gridDim.x * NT;
-  for (int t0 = blockIdx.x * NT + threadIdx.x; t0 < total; t0 += BBA_IPT * S) {
-    float g[BBA_IPT][8], y[BBA_IPT][8];
-#pragma unroll
-    for (int u = 0; u < BBA_IPT; ++u) {
-      const int t = t0 + u * S;
-      const size_t m = (size_t)(t < total ? t : t0) >> lg;   // clamped: loads stay unconditional
-      load8(p.g + m * p.C + c0, g[u]);
-      load8(p.y + m * p.C + c0, y[u]);
-    }
+  for (; t0 < total; t0 += BBA_IPT * S) {
 #pragma unroll
     for (int u = 0; u < BBA_IPT; ++u) {
       const int t = t0 + u * S;
       float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xhat = (y[u][j] - mean[j]) * rstd[j];
-        o[j] = a[j] * (g[u][j] - k1[j] - xhat * k2[j]);
+      for (int jj = 0; jj < 8; ++jj) {
+        const float xhat = (y[u][jj] - mean[jj]) * rstd[jj];
+        o[jj] = a[jj] * (g[u][jj] - k1[jj] - xhat * k2[jj]);
       }
       if (t < total) *reinterpret_cast<uint4*>(p.dy + (size_t)(t >> lg) * p.C + c0) = pack8(o);
     }
+    if (t0 + BBA_IPT * S < total) load_items(t0 + BBA_IPT * S);
   }
 }
 
