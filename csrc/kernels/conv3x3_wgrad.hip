@@ -11,6 +11,11 @@
 // per output element per block into the Keras-layout gradient slot, or (slab mode, used by the engine) stored
 // plainly into the block's pixel-split row of a slab that grad_finish sums: plain stores run at ~5x the
 // memory-side atomic rate and have no same-address serialisation.
+// Reduction order / LDS layout: the MFMA k-slots of a 32-pixel step are assigned so that the 32 lanes of each
+// ds_read_b64_tr_b16 read 8 CONSECUTIVE pixel rows (lo: 4g+q, hi: 16+4g+q; the same permutation on both operands,
+// so the sum is unchanged); with 96-byte halo rows and 96/160-byte dy rows those 8 rows x 32 bytes cover all 64
+// banks for any row base (the halo tap shifts move the base). The previous {b..b+3, b+8..b+11} assignment with
+// 80/144-byte rows left 2-4-way conflicts (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 46 %).
 #include "common.h"
 #include "launch.h"
 
@@ -20,7 +25,7 @@ constexpr int NT = 256;
 constexpr int CB = 32;            // input channels per block (the A-operand rows)
 constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;
-constexpr int LDH = CB + 8;
+constexpr int LDH = CB + 16;     // 96-byte halo rows (see the layout note above)
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
@@ -36,7 +41,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
   constexpr int NF = BNO / 16;              // n fragments
   constexpr int COMBOS = 2 * NF;            // (c fragment, n fragment) pairs per tap
   constexpr int CPW = COMBOS / 4;           // combos per wave
-  constexpr int LDD = BNO + 8;
+  constexpr int LDD = BNO + 16;    // 96 / 160-byte dy rows
   constexpr int HALO_CH = HP * (CB / 8), H_PER_T = (HALO_CH + NT - 1) / NT;
   constexpr int D_CH = TP * (BNO / 8), D_PER_T = (D_CH + NT - 1) / NT;
   static_assert(COMBOS % 4 == 0, "combos must split over 4 waves");
@@ -135,8 +140,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
     if (more) load(t + splits);
 #pragma unroll
     for (int j = 0; j < TP / 32; ++j) {            // pixel k-steps of 32
-      const int p0 = 32 * j + 8 * g + q;            // this lane's pixel rows: p0 (elements 0-3) and p0 + 4
-      const int p1 = p0 + 4;
+      const int p0 = 32 * j + 4 * g + q;            // this lane's pixel rows: p0 (elements 0-3) and p0 + 16
+      const int p1 = p0 + 16;
       s8v bop[CPW];
 #pragma unroll
       for (int u = 0; u < CPW; ++u) {
