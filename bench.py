@@ -89,8 +89,11 @@ def main() -> int:
         return 0
 
     val_steps = len(data.val_idx) // args.batch if args.val_steps < 0 else args.val_steps
-    vbatches = torch.as_tensor(epoch_batches(data.val_idx, args.batch, 0, 0)[:val_steps], dtype=torch.int32,
-                               device=dev) if val_steps else None
+    # the reference's 16-image validation batches, evaluated 3-8 at a time by an inference engine sharing the
+    # weights (per-pixel means are batching-invariant: models/engine.py UNetEngine.evaluator)
+    vimg = epoch_batches(data.val_idx, args.batch, 0, 0)[:val_steps].reshape(-1) if val_steps else None
+    ev = eng.evaluator(eng.eval_batch_for(len(vimg))) if val_steps else None
+    vbatches = torch.as_tensor(vimg.reshape(-1, ev.B), dtype=torch.int32, device=dev) if val_steps else None
 
     def fl_round() -> None:
         eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
@@ -98,9 +101,9 @@ def main() -> int:
             for s in range(args.local_steps):
                 eng.idx.copy_(batches[s])
                 eng.train_step(use_graph)
-            for v in range(val_steps):
-                eng.idx.copy_(vbatches[v])
-                eng.eval_step(use_graph)
+            for v in range(vbatches.shape[0] if val_steps else 0):
+                ev.idx.copy_(vbatches[v])
+                ev.eval_step(use_graph)
         if agg is not None:
             # weighted FedAvg over RCCL/xGMI, bucketed in layer order on a side stream; each bucket's layers are
             # repacked to bf16 there and the next round waits per bucket (engine.defer_until)
@@ -139,6 +142,7 @@ def main() -> int:
                "wall_clock_per_round_s": round(round_s, 4),
                "ms_per_iteration": round(round_s * 1000.0 / (args.epochs * args.local_steps), 4),
                "val_images_per_round": world * args.epochs * val_steps * args.batch,
+               "eval_batch": ev.B if val_steps else None,
                "peak_hbm_gb_per_client": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",

@@ -47,7 +47,10 @@ class Lazy:
 class UNetEngine:
     def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
                  lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
-                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, fp8: bool = False):
+                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, fp8: bool = False,
+                 share: Optional["UNetEngine"] = None):
+        """``share``: an inference-only engine (see ``evaluator``) reading another engine's parameters and packed
+        weights in place (no copy, no repack)."""
         self.fp8 = fp8                     # decoder Conv2DTranspose forward in fp8 e4m3 (conv3x3_fp8.hip)
         self._fp8_calibrated = False
         if img % 16:
@@ -66,7 +69,8 @@ class UNetEngine:
         dev = self.dev
         f32 = dict(dtype=torch.float32, device=dev)
         # ---- parameters / optimizer state (flat fp32) ----
-        self.flat = torch.zeros(table.total, **f32)
+        self._share = share
+        self.flat = share.flat if share is not None else torch.zeros(table.total, **f32)
         self.grad = torch.zeros(table.total, **f32)
         self.m = torch.zeros(table.total, **f32)
         self.v = torch.zeros(table.total, **f32)
@@ -83,6 +87,7 @@ class UNetEngine:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.eval_graph: Optional[torch.cuda.CUDAGraph] = None
         self._retired: List[torch.Tensor] = []   # replaced workspaces a captured graph may still reference
+        self._evaluators: Dict[int, "UNetEngine"] = {}
         self.images: Optional[torch.Tensor] = None
         self.masks: Optional[torch.Tensor] = None
 
@@ -149,7 +154,8 @@ class UNetEngine:
             elif ly.kind == "conv" and ly.ksize == 1 and ly.cout > 1:
                 add(PK_CONV, ly.name, "kernel", 1, ly.cin, ly.cout)
                 add(PK_CONV_DGRAD1x1, ly.name, "kernel", 1, ly.cin, ly.cout)
-        self.packed = torch.zeros(off, dtype=torch.int16, device=self.dev)
+        self.packed = self._share.packed if self._share is not None else torch.zeros(off, dtype=torch.int16,
+                                                                                     device=self.dev)
         self.pack_table = self.C.make_pack_table(views, self.flat)
         if self.fp8:   # fp8 copies of the forward ConvT weights + per-output-channel scales + delayed amax slots
             v8, off8, soff, self.p8_at = [], 0, 0, {}
@@ -313,6 +319,8 @@ class UNetEngine:
             raise ValueError("masks must be uint8 [N,S,S]")
         self.images, self.masks = images.contiguous(), masks.contiguous()
         self.n_data = images.shape[0]
+        for ev in self._evaluators.values():
+            ev.bind_data(self.images, self.masks)
 
     # ------------------------------------------------------------------------------------------------ schedule
     def _bn_final(self, name: str, train: bool) -> torch.Tensor:
@@ -626,6 +634,8 @@ class UNetEngine:
         """Inference-mode forward (moving BN statistics) of the batch in ``idx``; loss / accuracy accumulate into
         ``eval_metrics``. Replayed from its own hipGraph (captured after an eager warm-up)."""
         self._fp8_calibrate()
+        if self._share is not None:
+            self._share._await_all()                   # the parameters are the parent's (FedAvg buckets in flight)
         if not use_graph:
             self.forward(False)
             return
@@ -668,6 +678,33 @@ class UNetEngine:
         n = max(v[2], 1.0)
         return {"loss": float(v[0] / n) * 1.0, "bce_sum": float(v[0]), "accuracy": float(v[1] / n),
                 "pixels": float(v[2]), "dice_sum": float(v[3])}
+
+    def evaluator(self, batch: int) -> "UNetEngine":
+        """An inference-only engine of batch ``batch`` over THIS engine's parameters, packed weights and dataset.
+        Validation loss / accuracy are per-pixel means over the whole held-out split (head.hip sums, normalised by
+        the pixel count), so evaluating the same images in larger batches gives the same numbers - and larger
+        batches fill the GPU (the 16-image eval forward is launch/latency-bound). Not used for the fp8 path (its
+        activation scales are calibrated per engine) or with the per-batch Dice term."""
+        if batch == self.B or self.fp8 or self.dice:
+            return self
+        ev = self._evaluators.get(batch)
+        if ev is None:
+            ev = UNetEngine(self.table, batch, self.S, self.dev, "bce", self.lr, self.b1, self.b2, self.adam_eps,
+                            self.momentum, self.bn_eps, share=self)
+            if self.images is not None:
+                ev.bind_data(self.images, self.masks)
+            self._evaluators[batch] = ev
+        return ev
+
+    def eval_batch_for(self, n_images: int, cap: int = 128) -> int:
+        """Largest eval batch <= cap that is a multiple of B and divides ``n_images`` (a whole number of the
+        reference's batches), so every held-out image is evaluated exactly once."""
+        nb = n_images // self.B
+        best = 1
+        for k in range(1, nb + 1):
+            if nb % k == 0 and k * self.B <= cap:
+                best = k
+        return best * self.B
 
     def predict_probs(self) -> torch.Tensor:
         """Sigmoid probabilities at full resolution for the current ``idx`` batch (eval-mode BN)."""
@@ -716,13 +753,18 @@ class HipBackend:
         return m
 
     def eval_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        """Validation over the images of ``batches`` (the reference's 16-image batches), evaluated in the largest
+        multiple of them <= 128 per launch (engine.evaluator: same per-pixel means, fewer / fuller launches)."""
         e = self.eng
-        dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)
-        e.eval_metrics.zero_()
+        idx = np.asarray(batches, np.int32).reshape(-1)
+        ev = e.evaluator(e.eval_batch_for(len(idx)))
+        e._await_all()
+        dev_b = torch.as_tensor(idx.reshape(-1, ev.B)).to(e.dev)
+        ev.eval_metrics.zero_()
         for s in range(dev_b.shape[0]):
-            e.idx.copy_(dev_b[s])
-            e.eval_step(self.use_graph)
-        return e.read_metrics("eval")
+            ev.idx.copy_(dev_b[s])
+            ev.eval_step(self.use_graph)
+        return ev.read_metrics("eval")
 
     def predict(self, idx: np.ndarray) -> np.ndarray:
         e = self.eng

@@ -757,3 +757,28 @@ def test_conv3x3_small_tiles_forced(B, Hs, Cin, N, up, use_ab):
         test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
     finally:
         hip().set_tune(hip().TUNE_CONV3_SMALL, 0)
+
+
+def test_evaluator_engine_matches_per_batch_eval():
+    """UNetEngine.evaluator(k*B): the same held-out images evaluated k batches per launch over the SHARED
+    parameters give the same per-pixel loss / accuracy as the reference's B-image batches."""
+    table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=9)
+    for _ in range(2):
+        eng.train_step(use_graph=False)
+    idx = np.arange(6, dtype=np.int32)
+    assert eng.eval_batch_for(6) == 6
+    eng.eval_metrics.zero_()
+    for s in range(3):
+        eng.idx.copy_(torch.as_tensor(idx[2 * s:2 * s + 2]).to(DEV))
+        eng.eval_step(use_graph=False)
+    small = eng.read_metrics("eval")
+    ev = eng.evaluator(6)
+    assert ev is not eng and ev.flat.data_ptr() == eng.flat.data_ptr() and ev.packed.data_ptr() == eng.packed.data_ptr()
+    for use_graph in (False, True):
+        ev.eval_metrics.zero_()
+        ev.idx.copy_(torch.as_tensor(idx).to(DEV))
+        ev.eval_step(use_graph=use_graph)
+        big = ev.read_metrics("eval")
+        assert big["pixels"] == small["pixels"]
+        assert abs(big["loss"] - small["loss"]) < 1e-5 * max(1.0, abs(small["loss"])), (big, small)
+        assert abs(big["accuracy"] - small["accuracy"]) < 1e-6
