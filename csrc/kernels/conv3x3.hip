@@ -360,6 +360,14 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
 
 }  // namespace
 
+// output-channel tile of the whole-chunk path: 64 (fewer halo re-loads) unless tuned to 32 (more blocks, 122 vs 208
+// VGPRs -> 4 vs 2 waves per SIMD)
+static int wb_bn(const ConvParams& p) {
+  const int v = cfl_tune(TUNE_CONV3_BN);
+  if (v == 32 || p.N % 64 != 0) return 32;
+  return 64;
+}
+
 static bool use_wb(const ConvParams& p) {
   const int v = cfl_tune(TUNE_CONV3_WB);
   return v == 0 ? true : v == 1;           // 0 = default (whole-chunk B, BN <= 64), 2 = per-tap B (BN up to 128)
@@ -381,7 +389,7 @@ int conv3x3_splits(const ConvParams& p) {
   if (small_tiles(p)) return 1;
   const int tw = p.Wo >= 16 ? 16 : 8;
   const int th = 128 / tw;
-  const int bn = use_wb(p) ? (p.N >= 64 ? 64 : p.N) : (p.N >= 128 ? 128 : p.N);
+  const int bn = use_wb(p) ? wb_bn(p) : (p.N >= 128 ? 128 : p.N);
   const int blocks = ((p.Ho + th - 1) / th) * ((p.Wo + tw - 1) / tw) * p.B * (p.N / bn);
   const int chunks = p.Cin / BK;
   if (blocks >= 192 || chunks < 2) return 1;
@@ -403,7 +411,7 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   const bool w16 = p.Wo >= 16;
   if (small_tiles(p)) {
     splits = launch<8, 8, 32, 2, 2, true>(p, 1, st);
-  } else if (use_wb(p) && p.N % 64 == 0) {
+  } else if (use_wb(p) && wb_bn(p) == 64) {
     if (w16) splits = launch<8, 16, 64, 2, 2, true>(p, splits, st);
     else splits = launch<16, 8, 64, 2, 2, true>(p, splits, st);
   } else if (use_wb(p)) {

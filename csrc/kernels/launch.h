@@ -285,6 +285,7 @@ enum TuneKey {
   TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 1024)
   TUNE_DW_STREAM_BLOCKS = 8,   // depthwise row-streaming kernels: target grid size (default 1024)
   TUNE_CONV3_SMALL = 9,        // conv3x3 low-M layers: 0 = heuristic, 1 = split-K (+ epilogue launch), 2 = 8x8x32 tiles
+  TUNE_CONV3_BN = 10,          // conv3x3 whole-chunk path: output-channel tile (0 = 64 when N % 64 == 0, else 32)
   TUNE_N = 16
 };
 int cfl_tune(int key);
