@@ -564,7 +564,7 @@ class UNetEngine:
             self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats)
             return
         B = self.B
-        need = self.C.conv_splits(B, Ho, Ho, N, 3, 1, 1, x.C)
+        need = self.C.conv_splits_fp8(B, Ho, Ho, N, x.C)
         if need > 1 and need * B * Ho * Ho * N > self.ws.numel():
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")

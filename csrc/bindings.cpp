@@ -105,6 +105,14 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
+int conv_splits_fp8_op(int B, int Ho, int Wo, int N, int Cin) {
+  ConvParams p{};
+  p.B = B; p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = 3; p.stride = 1; p.pad_t = 1; p.pad_l = 1; p.Cin = Cin;
+  p.M = B * Ho * Wo;
+  p.K = 9 * Cin;
+  return conv3x3_split_k(p);
+}
+
 int conv_splits_op(int B, int Ho, int Wo, int N, int ks, int stride, int pad, int Cin) {
   ConvParams p{};
   p.B = B; p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad; p.pad_l = pad; p.Cin = Cin;
@@ -562,6 +570,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
   m.def("conv_splits", &conv_splits_op);
+  m.def("conv_splits_fp8", &conv_splits_fp8_op);
   m.def("conv_wgrad", &conv_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),
         py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("dst_mode"),

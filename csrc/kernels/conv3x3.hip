@@ -385,8 +385,10 @@ static bool small_tiles(const ConvParams& p) {
   return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
 }
 
-int conv3x3_splits(const ConvParams& p) {
-  if (small_tiles(p)) return 1;
+int conv3x3_splits(const ConvParams& p) { return small_tiles(p) ? 1 : conv3x3_split_k(p); }
+
+// K splits of the 8x16 / 16x8-pixel tiles (the fp8 kernel has no small-tile variant and always uses this)
+int conv3x3_split_k(const ConvParams& p) {
   const int tw = p.Wo >= 16 ? 16 : 8;
   const int th = 128 / tw;
   const int bn = use_wb(p) ? wb_bn(p) : (p.N >= 128 ? 128 : p.N);

@@ -346,7 +346,7 @@ bool conv3x3_fp8_supported(const ConvParams& c) {
 int conv3x3_fp8(const Conv8Params& p, hipStream_t st) {
   const ConvParams& c = p.c;
   if (!conv3x3_fp8_supported(c) || !p.wt8 || !p.wscale || !p.amax) return 1;
-  int splits = conv3x3_splits(c);
+  int splits = conv3x3_split_k(c);
   if (splits > 1 && (c.ws == nullptr || c.ws_elems < (int64_t)splits * c.M * c.N)) splits = 1;
   Conv8Params q = p;
   if (splits == 1) q.c.ws = nullptr;

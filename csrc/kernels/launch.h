@@ -57,6 +57,7 @@ struct ConvParams {
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
 int conv3x3_splits(const ConvParams& p);
+int conv3x3_split_k(const ConvParams& p);     // K splits of the standard tiles (fp8 path)
 int splitk_epilogue(const ConvParams& p, int splits, hipStream_t st);   // sum partials + bias/stats/node epilogue
 
 // fp8 (e4m3) forward 3x3 conv (conv3x3_fp8.hip): c.wt unused; per-output-channel weight scales, delayed
