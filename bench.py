@@ -61,6 +61,7 @@ def main() -> int:
     from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
     from crack_detection_federatedlearning_grpc_amd.parallel.rccl import FedAvgAllReduce
     from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
+    from crack_detection_federatedlearning_grpc_amd.utils.trace import phase
 
     table = ParamTable()
     plan = None
@@ -98,12 +99,14 @@ def main() -> int:
     def fl_round() -> None:
         eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
         for _ep in range(args.epochs):                     # model.fit(epochs=10, validation_data=val_gen)
-            for s in range(args.local_steps):
-                eng.idx.copy_(batches[s])
-                eng.train_step(use_graph)
-            for v in range(vbatches.shape[0] if val_steps else 0):
-                ev.idx.copy_(vbatches[v])
-                ev.eval_step(use_graph)
+            with phase("bench/train_epoch"):               # roctx ranges with CFL_ROCTX=1 (utils/trace.py)
+                for s in range(args.local_steps):
+                    eng.idx.copy_(batches[s])
+                    eng.train_step(use_graph)
+            with phase("bench/validate"):
+                for v in range(vbatches.shape[0] if val_steps else 0):
+                    ev.idx.copy_(vbatches[v])
+                    ev.eval_step(use_graph)
         if agg is not None:
             # weighted FedAvg over RCCL/xGMI, bucketed in layer order on a side stream; each bucket's layers are
             # repacked to bf16 there and the next round waits per bucket (engine.defer_until)

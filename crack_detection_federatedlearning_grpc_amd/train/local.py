@@ -21,6 +21,7 @@ import numpy as np
 from ..config import FLConfig
 from ..data.synthetic import CrackDataset
 from ..models.spec import ParamTable
+from ..utils.trace import phase
 
 
 class StepBackend(Protocol):
@@ -143,14 +144,16 @@ class LocalFit:
             seed = (cfg.data_seed * 1000003 + current_round * 1009 + ep) & 0x7FFFFFFF
             batches = epoch_batches(self.data.train_idx, cfg.batch_size, self.steps, seed)
             t0 = time.perf_counter()
-            m = self.backend.train_batches(batches)
+            with phase("fl/train_epoch"):
+                m = self.backend.train_batches(batches)
             dt = time.perf_counter() - t0
             rec = {"client": self.client, "round": current_round, "epoch": ep + 1, "loss": m["loss"],
                    "accuracy": m["accuracy"], "images": int(batches.size), "train_s": dt,
                    "images_per_s": batches.size / max(dt, 1e-9)}
             if cfg.validate and len(self.data.val_idx) >= cfg.batch_size:
                 vb = epoch_batches(self.data.val_idx, cfg.batch_size, 0, 0)
-                v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
+                with phase("fl/validate"):
+                    v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
                 rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
             self._log(rec)
             if tb is not None:
