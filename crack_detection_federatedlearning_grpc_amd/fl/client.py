@@ -26,7 +26,7 @@ import numpy as np
 from ..config import FLConfig
 from . import codec
 from . import proto as P
-from ..utils.trace import phase
+from ..utils.trace import phase as trace_phase
 from .rpc import TransportServiceStub, channel_options
 
 
@@ -196,10 +196,10 @@ class FLClient:
                 if self.cfg.fault_delay_s:
                     time.sleep(self.cfg.fault_delay_s)
                 t0 = time.perf_counter()
-                with phase("fl/aggregate"):
+                with trace_phase("fl/aggregate"):
                     payload = self._payload()             # RCCL mode: the all-reduce runs here
                 t1 = time.perf_counter()
-                with phase("fl/upload"):
+                with trace_phase("fl/upload"):
                     rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0))
                 t2 = time.perf_counter()
                 phase = {"round": cr, "aggregate_s": t1 - t0, "upload_s": t2 - t1, "wait_s": 0.0,

@@ -76,8 +76,8 @@ class UNetEngine:
         self.v = torch.zeros(table.total, **f32)
         self.trainable = torch.as_tensor(table.trainable_mask().astype(np.uint8), device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
-        self.eval_metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.metrics = torch.zeros(10, dtype=torch.float64, device=dev)        # head.hip metrics layout
+        self.eval_metrics = torch.zeros(10, dtype=torch.float64, device=dev)
         self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
@@ -250,7 +250,7 @@ class UNetEngine:
         self._wslabs: Dict[str, torch.Tensor] = {}
         self._build_finish()
         # per-step zeroing of gradients / statistics in one launch
-        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:8]]
+        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10]]
         self.zero_table = self.C.make_zero_table(spans)
         self.n_zero, self.max_zero = len(spans), max(t.numel() * t.element_size() for t in spans)
         # inference BN coefficients of every layer (one launch per eval forward)
@@ -676,8 +676,13 @@ class UNetEngine:
         if reset:
             mt.zero_()
         n = max(v[2], 1.0)
-        return {"loss": float(v[0] / n) * 1.0, "bce_sum": float(v[0]), "accuracy": float(v[1] / n),
-                "pixels": float(v[2]), "dice_sum": float(v[3])}
+        out = {"loss": float(v[0] / n) * 1.0, "bce_sum": float(v[0]), "accuracy": float(v[1] / n),
+               "pixels": float(v[2]), "dice_sum": float(v[3])}
+        if which != "train":       # crack-class overlap over the whole pass (train zeroes these every step)
+            tp, pp, t = float(v[7]), float(v[8]), float(v[6])
+            out["iou"] = tp / (pp + t - tp) if pp + t - tp > 0 else 1.0
+            out["dice"] = 2.0 * tp / (pp + t) if pp + t > 0 else 1.0
+        return out
 
     def evaluator(self, batch: int) -> "UNetEngine":
         """An inference-only engine of batch ``batch`` over THIS engine's parameters, packed weights and dataset.

@@ -212,8 +212,12 @@ class RefTrainer:
 
     @torch.no_grad()
     def evaluate(self, x: torch.Tensor, y: torch.Tensor) -> Dict[str, float]:
+        """Loss / accuracy of the batch plus the crack-class counts (tp, pp, t) for IoU / Dice over a pass."""
         logits, _ = unet_forward(self.flat, x, self.table, False, self.momentum, self.bn_eps)
-        return {"loss": float(seg_loss(logits, y, self.loss_kind)), "accuracy": float(binary_accuracy(logits, y))}
+        pred = logits > 0
+        tgt = y > 0.5
+        return {"loss": float(seg_loss(logits, y, self.loss_kind)), "accuracy": float(binary_accuracy(logits, y)),
+                "tp": float((pred & tgt).sum()), "pp": float(pred.sum()), "t": float(tgt.sum())}
 
     @torch.no_grad()
     def predict(self, x: torch.Tensor) -> torch.Tensor:

@@ -93,11 +93,15 @@ class RefBackend:
 
     def eval_batches(self, batches):
         ls, acc = [], []
+        tp = pp = t = 0.0
         for ids in batches:
             m = self.tr.evaluate(*self._batch(ids))
             ls.append(m["loss"])
             acc.append(m["accuracy"])
-        return {"loss": float(np.mean(ls)), "accuracy": float(np.mean(acc))}
+            tp, pp, t = tp + m["tp"], pp + m["pp"], t + m["t"]
+        return {"loss": float(np.mean(ls)), "accuracy": float(np.mean(acc)),
+                "iou": tp / (pp + t - tp) if pp + t - tp > 0 else 1.0,
+                "dice": 2.0 * tp / (pp + t) if pp + t > 0 else 1.0}
 
     def predict(self, idx):
         x, _ = self._batch(idx)
@@ -155,6 +159,8 @@ class LocalFit:
                 with phase("fl/validate"):
                     v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
                 rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
+                if "iou" in v:
+                    rec["val_iou"], rec["val_dice"] = v["iou"], v["dice"]
             self._log(rec)
             if tb is not None:
                 ws = None

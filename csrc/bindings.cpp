@@ -380,7 +380,7 @@ HeadParams headp(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, 
   p.metrics = ptr<double>(metrics, "metrics");
   p.B = B; p.R = R; p.Cin = Cin; p.dice = dice;
   TORCH_CHECK(x.numel() == (int64_t)B * R * R * Cin && h.numel() == (int64_t)B * R * R && idx.numel() == B &&
-              metrics.numel() >= 8 && masks.size(-1) == 2 * R, "head sizes");
+              metrics.numel() >= 10 && masks.size(-1) == 2 * R, "head sizes");
   return p;
 }
 

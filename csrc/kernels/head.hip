@@ -15,14 +15,15 @@ namespace {
 constexpr int NT = 256;
 constexpr float DICE_SMOOTH = 1.0f;
 
-// metrics layout (double): [0] bce sum, [1] correct, [2] pixels, [3] dice loss sum, [4] I, [5] P, [6] T (this step)
+// metrics layout (double): [0] bce sum, [1] correct, [2] pixels, [3] dice loss sum, [4] I, [5] P, [6] T (soft, this
+// step), [7] TP (predicted AND true crack pixels), [8] PP (predicted crack pixels) - hard-threshold IoU / Dice
 
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
-  __shared__ double red[5][NT / 64];
+  __shared__ double red[7][NT / 64];
   const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
-  double bce = 0, cor = 0, I = 0, P = 0, T = 0;
+  double bce = 0, cor = 0, I = 0, P = 0, T = 0, TP = 0, PP = 0;
   for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
     const int j = pix % p.R, i = (pix / p.R) % p.R;
     const int b = pix / (p.R * p.R);
@@ -45,24 +46,26 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
         const float t = mrow[(2 * i + dy) * S + 2 * j + dx] ? 1.f : 0.f;
         bce += sp - h * t;
         cor += ((h > 0.f) == (t > 0.5f)) ? 1.0 : 0.0;
+        TP += (h > 0.f && t > 0.5f) ? 1.0 : 0.0;
+        PP += h > 0.f ? 1.0 : 0.0;
         I += sg * t;
         P += sg;
         T += t;
       }
   }
-  double v[5] = {bce, cor, I, P, T};
+  double v[7] = {bce, cor, I, P, T, TP, PP};
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 7; ++k) {
     double x = v[k];
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
     if (lane == 0) red[k][wid] = x;
   }
   __syncthreads();
-  if (threadIdx.x < 5) {
+  if (threadIdx.x < 7) {
     double s = 0;
     for (int w = 0; w < NT / 64; ++w) s += red[threadIdx.x][w];
-    const int slot = threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 2;   // 0,1 -> 0,1 ; 2,3,4 -> 4,5,6
+    const int slot = threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 2;   // 0,1 -> 0,1 ; 2..6 -> 4..8
     atomicAdd(&p.metrics[slot], s);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.metrics[2], (double)npix * 4.0);

@@ -349,6 +349,12 @@ def test_engine_eval_graph_matches_eager_and_reference():
     logits, _ = R.unet_forward(p, x, table, training=False, emulate_bf16=True)
     ref = float(R.bce_with_logits_mean(logits, y))
     assert abs(eager["loss"] - ref) < 2e-2 * max(1.0, ref)
+    # crack-class IoU / Dice over the pass (head.hip TP / PP counters) vs the oracle's thresholded logits
+    pred, tgt = logits > 0, y > 0.5
+    tp, pp, t = float((pred & tgt).sum()), float(pred.sum()), float(tgt.sum())
+    iou_ref = tp / (pp + t - tp) if pp + t - tp > 0 else 1.0
+    assert abs(eager["iou"] - iou_ref) < 0.05, (eager["iou"], iou_ref)
+    assert 0.0 <= eager["dice"] <= 1.0
 
 
 @pytest.mark.parametrize("N", [32, 64])
