@@ -223,6 +223,79 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   }
 }
 
+// Gradient of a BN node routed back through MaxPooling2D(3, s2, same) (encoder: node_bwd<GM_MAXPOOL, GM_NONE>
+// without masks), one 2x2 input-pixel block per item: the four pooled windows (i-1..i) x (j-1..j) that can hold
+// these pixels' maxima are read ONCE for all four pixels (the per-pixel gather read each window's gradient and
+// argmax up to 4x from L2). Window (i,j) holds pixel (dy,dx) at tap dy*3+dx, window (i-1,j) the top row at tap
+// 6+dx, window (i,j-1) the left column at tap dy*3+2, window (i-1,j-1) pixel (0,0) at tap 8. Same BN-backward sums
+// as node_bwd (sum g, sum g * xhat).
+__global__ __launch_bounds__(NT) void node_pool_bwd_kernel(NodeBwdParams p) {
+  __shared__ float red[2][4][256];
+  const int G = p.C >> 3, lg = ilog2(G);
+  const int c0 = (threadIdx.x & (G - 1)) * 8;
+  const bool stats = p.sums != nullptr && p.ab != nullptr;
+  float mean[8], rstd[8];
+  load_f8_or(p.ab + 2 * p.C + c0, stats, 0.f, mean);
+  load_f8_or(p.ab + 3 * p.C + c0, stats, 0.f, rstd);
+  float s[2][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+  const int Hh = p.H >> 1, Wh = p.W >> 1;
+  const int total = (p.B * Hh * Wh) << lg;
+  const int HWh = Hh * Wh;
+  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += gridDim.x * NT) {
+    const int blk = it >> lg, b = blk / HWh, r = blk - b * HWh, i = r / Wh, j = r - i * Wh;
+    // windows q = (wi, wj): 0 = (i, j), 1 = (i, j-1), 2 = (i-1, j), 3 = (i-1, j-1); missing ones read window 0
+    // with a tap no argmax holds
+    float u[4][8];
+    uint2 am[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool up = q >= 2, left = q & 1;
+      const bool ok = (!up || i > 0) && (!left || j > 0);
+      const int wi = ok ? i - up : i, wj = ok ? j - left : j;
+      const size_t o = ((size_t)(b * Hh + wi) * Wh + wj) * p.C + c0;
+      am[q] = *reinterpret_cast<const uint2*>(p.argmax + o);
+      load8(p.src[0].p + o, u[q]);
+      if (!ok) am[q] = make_uint2(0xffffffffu, 0xffffffffu);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int dy = d >> 1, dx = d & 1;
+      const size_t pix = ((size_t)(b * p.H + 2 * i + dy) * p.W + 2 * j + dx);
+      float y[8], g[8];
+      if (stats) load8(p.v + pix * p.C + c0, y);
+      // taps of this pixel in windows 0..3 (64 = not contained)
+      const uint32_t tw[4] = {(uint32_t)(dy * 3 + dx), dx == 0 ? (uint32_t)(dy * 3 + 2) : 64u,
+                              dy == 0 ? (uint32_t)(6 + dx) : 64u, (dy == 0 && dx == 0) ? 8u : 64u};
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t word = jj < 4 ? am[q].x : am[q].y;
+          if (((word >> (8 * (jj & 3))) & 0xffu) == tw[q]) t += u[q][jj];
+        }
+        g[jj] = t;
+      }
+      const uint4 gv = pack8(g);
+      *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
+      if (stats) {
+        float gr[8];
+        unpack8(gv, gr);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          s[0][jj] += gr[jj];
+          s[1][jj] += gr[jj] * (y[jj] - mean[jj]) * rstd[jj];
+        }
+      }
+    }
+  }
+  if (!p.sums) return;
+  const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
+  block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * 2 * p.C, red);
+}
+
 constexpr int BBA_IPT = 4;
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
@@ -336,6 +409,15 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
   if (blocks > cap) blocks = cap;     // bounded grid: one set of channel atomics per block
   if (blocks < 1) blocks = 1;
   const int m0 = p.src[0].mode, m1 = p.src[1].mode;
+  if (m0 == GM_MAXPOOL && m1 == GM_NONE && !p.src[0].mask && !p.relu_node && !p.sy && p.ab && p.argmax &&
+      ((p.H | p.W) & 1) == 0 && cfl_tune(TUNE_NODE_POOL2X2) != 1) {
+    const int64_t items2 = (int64_t)p.B * (p.H / 2) * (p.W / 2) * (p.C / 8);
+    int b2 = (int)((items2 + NT - 1) / NT);
+    if (b2 > cap) b2 = cap;
+    if (b2 < 1) b2 = 1;
+    hipLaunchKernelGGL(node_pool_bwd_kernel, dim3(b2), dim3(NT), 0, st, p);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   // specialised instances for the engine's source combinations (fewer live registers, no mode branches)
   if (m0 == GM_SAME && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
   else if (m0 == GM_SUM2X2 && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);

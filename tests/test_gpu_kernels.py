@@ -788,3 +788,36 @@ def test_evaluator_engine_matches_per_batch_eval():
         assert big["pixels"] == small["pixels"]
         assert abs(big["loss"] - small["loss"]) < 1e-5 * max(1.0, abs(small["loss"])), (big, small)
         assert abs(big["accuracy"] - small["accuracy"]) < 1e-6
+
+
+@pytest.mark.parametrize("B,H,C", [(2, 16, 64), (3, 8, 128), (1, 32, 32)])
+def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C):
+    """node_pool_bwd_kernel (one 2x2 input block per item, each pooled window read once) == the per-pixel gather
+    of node_bwd<GM_MAXPOOL> (bit-identical gradient, same BN-backward sums), on argmaxes from the real forward."""
+    C_ = hip()
+    torch.manual_seed(23)
+    yb, _ = bf(torch.randn(B, H, H, C))
+    ab, _, _ = ab_for(C, 9)
+    ab[3 * C:] = torch.rand(C) + 0.5
+    ab[2 * C:3 * C] = torch.randn(C) * 0.1
+    ab = ab.to(DEV)
+    Ho = H // 2
+    res = torch.zeros(B, Ho, Ho, C, dtype=torch.int16, device=DEV)
+    x = torch.zeros_like(res)
+    am = torch.zeros(B, Ho, Ho, C, dtype=torch.uint8, device=DEV)
+    C_.pool_res_fwd(yb, ab, res, x, am, B, H, H, C)          # argmaxes as the engine's forward records them
+    dxb, _ = bf(torch.randn(B, Ho, Ho, C))
+    outs = []
+    for tune in (1, 0):                                          # 1 = per-pixel gather, 0 = 2x2 blocks
+        C_.set_tune(C_.TUNE_NODE_POOL2X2, tune)
+        try:
+            g = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
+            sums = torch.zeros(16 * 2 * C, device=DEV)
+            C_.node_bwd(dxb, 4, 0, None, 0, 0, am, yb, ab, 0, g, sums, B, H, H, C, 16)
+            outs.append((g.clone(), sums.view(16, 2, C).sum(0).cpu()))
+        finally:
+            C_.set_tune(C_.TUNE_NODE_POOL2X2, 0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-3)
+    # every pooled gradient lands exactly once: total mass is preserved
+    assert abs(float(from_bits(outs[1][0]).sum()) - float(from_bits(dxb).sum())) < 1e-2 * B * H * H
