@@ -115,7 +115,7 @@ def unet_forward(flat: torch.Tensor, x_nhwc: torch.Tensor, table: Optional[Param
     names = iter([ly.name for ly in table.weighted_layers()])
     x = x_nhwc.permute(0, 3, 1, 2)
     n = next(names)
-    x = r(conv2d_same(x, P(n, "kernel"), P(n, "bias"), 2))
+    x = r(conv2d_same(x, r(P(n, "kernel")), P(n, "bias"), 2))    # entry MFMA kernel: bf16 weights
     x = F.relu(bn(x, next(names)))
     prev = x
     for _f in ENC_FILTERS:

@@ -1,7 +1,8 @@
 // Entry block Conv2D(32, 3, strides=2, padding="same") on the 3-channel image (client_fit_model.py:100).
-// K = 27 is too small for an MFMA tile, so this is a direct VALU kernel that reads the uint8 dataset rows of the
-// batch through the index vector (batch assembly and the /255 normalisation of client_fit_model.py:43 are folded
-// into the load - no batch tensor is ever materialised). TF "same" at stride 2 pads bottom/right only.
+// The kernels read the uint8 dataset rows of the batch through the index vector (batch assembly and the /255
+// normalisation of client_fit_model.py:43 are folded into the load - no batch tensor is ever materialised).
+// TF "same" at stride 2 pads bottom/right only. Cout == 32 runs on MFMA (K = 27 taps padded to 32, see the MFMA
+// section below); the direct VALU kernels serve other widths.
 // Forward writes bf16 y + BN batch statistics (replica rows); wgrad accumulates dW (3,3,3,Cout) in fp32.
 // Blocks walk whole output rows (32-bit indices, shifts); the row's input pixels are staged in LDS with word loads.
 #include "common.h"
@@ -140,7 +141,195 @@ __global__ __launch_bounds__(NT) void entry_wgrad_kernel(EntryParams p, int repl
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// MFMA forms for Cout == 32 (the network's entry width). An output pixel's 27 taps (ky, kx, ci) are gathered from the
+// uint8 rows as the integers 0..255 - exact in bf16; the /255 goes onto the fp32 accumulator - zero-padded to K = 32
+// and staged per step of ECH output pixels as an LDS [pixel][tap] bf16 tile:
+//   forward  y[pix][co]  = bias[co] + (1/255) * X[pix][0:32] . W[0:32][co]   (W rounded to bf16, held in registers)
+//   wgrad    dW[tap][co] = (1/255) * sum_pix X[pix][tap] * dy[pix][co]      (the pixel reduction is the MFMA K axis:
+//            both [pixel][*] tiles are read with the transposing ds_read_b64_tr_b16, as conv_wgrad.hip does)
+// mfma_f32_16x16x32_bf16 lane maps: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
+// The VALU kernels above stay for other widths (TUNE_ENTRY_ALGO=1 forces them): they are LDS-bandwidth bound, two
+// 16-byte weight reads per 8 FMAs.
+constexpr int ECH = 128;   // output pixels per step (4 waves x 32)
+constexpr int ELD = 40;    // LDS row stride (bf16) of the [pixel][32] tiles (80-byte rows)
+
+typedef short s4v_lds __attribute__((ext_vector_type(4)));
+CFL_DEVICE s4v tr_read(const bf16_t* q) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(q));
+}
+
+// taps [16h, 16h + 16) of output pixel (row = b*Ho + oh, column ow) as integers; 0 outside the image (TF "same"
+// bottom/right pad), past the row end and for the padding taps >= 27 (addresses clamped, loads unconditional)
+CFL_DEVICE void entry_gather(const EntryParams& p, int row, int ow, int h, uint32_t (&xv)[16]) {
+  const int b = row / p.Ho, oh = row - b * p.Ho;
+  const uint8_t* img = p.images + (size_t)p.idx[b] * p.S * p.S * 3;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int T = 16 * h + i;
+    const int ky = T / 9, kx = (T / 3) % 3, ci = T % 3;
+    const int ih = 2 * oh + ky, iw = 2 * ow + kx;
+    const bool ok = T < 27 && ow < p.Wo && ih < p.S && iw < p.S;
+    const uint32_t v = img[ok ? (ih * p.S + iw) * 3 + ci : 0];
+    xv[i] = ok ? v : 0u;
+  }
+}
+
+CFL_DEVICE void entry_put(bf16_t* dst, const uint32_t (&xv)[16]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = pack2bf((float)xv[2 * k], (float)xv[2 * k + 1]);
+  *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+  *reinterpret_cast<uint4*>(dst + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+__global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int nch, int steps) {
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][ECH][ELD];
+  __shared__ __attribute__((aligned(16))) bf16_t sY[ECH][ELD];
+  __shared__ float red[2][4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int pl = tid & (ECH - 1), h = tid >> 7;
+  // B operand (fixed): lane holds output channel 16j + r16 at taps 8g .. 8g+7 (0 for the padding taps)
+  s8v wv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int T = 8 * g + e;
+      wv[j][e] = (short)f2bf(T < 27 ? p.w[T * 32 + 16 * j + r16] : 0.f);
+    }
+  const float bias0 = p.bias[r16], bias1 = p.bias[16 + r16];
+  float s[2][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+  uint32_t xv[16];
+  int st = blockIdx.x;
+  entry_gather(p, st / nch, (st % nch) * ECH + pl, h, xv);
+  entry_put(&sX[0][pl][16 * h], xv);
+  __syncthreads();
+  int buf = 0;
+  for (; st < steps; st += gridDim.x) {
+    const int nxt = st + gridDim.x;
+    const bool more = nxt < steps;
+    if (more) entry_gather(p, nxt / nch, (nxt % nch) * ECH + pl, h, xv);   // in flight during this step
+    f4v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const s8v a = *reinterpret_cast<const s8v*>(&sX[buf][32 * wid + 16 * i + r16][8 * g]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wv[j], f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bf16_t* yr = &sY[32 * wid + 16 * i + 4 * g + r][r16];
+        yr[0] = f2bf(fmaf(acc[i][0][r], 1.f / 255.f, bias0));
+        yr[16] = f2bf(fmaf(acc[i][1][r], 1.f / 255.f, bias1));
+      }
+    __syncthreads();
+    const int row = st / nch, ow0 = (st % nch) * ECH;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {       // 16-byte stores of 8 channels; channel group (tid & 3) fixed per thread
+      const int e = tid + NT * k, px = e >> 2, cq = (e & 3) * 8;
+      if (ow0 + px < p.Wo) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&sY[px][cq]);
+        *reinterpret_cast<uint4*>(p.y + ((size_t)row * p.Wo + ow0 + px) * 32 + cq) = v;
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[0][j] += f[j];
+          s[1][j] += f[j] * f[j];
+        }
+      }
+    }
+    if (more) entry_put(&sX[buf ^ 1][pl][16 * h], xv);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (p.stats) block_channel_atomics<2>(s, 4, 32, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 64, red);
+}
+
+__global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int nch, int steps, int replicas) {
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][ECH][ELD];
+  __shared__ __attribute__((aligned(16))) bf16_t sG[2][ECH][ELD];
+  __shared__ float red[4][32 * 32];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int pl = tid & (ECH - 1), h = tid >> 7;
+  uint32_t xv[16];
+  uint4 gv[2];
+  auto load = [&](int s) {
+    const int row = s / nch, ow0 = (s % nch) * ECH;
+    entry_gather(p, row, ow0 + pl, h, xv);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + NT * k, ow = ow0 + (e >> 2);
+      gv[k] = ow < p.Wo ? *reinterpret_cast<const uint4*>(p.dy + ((size_t)row * p.Wo + ow) * 32 + (e & 3) * 8)
+                        : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int b) {
+    entry_put(&sX[b][pl][16 * h], xv);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + NT * k;
+      *reinterpret_cast<uint4*>(&sG[b][e >> 2][(e & 3) * 8]) = gv[k];
+    }
+  };
+  f4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  int st = blockIdx.x;
+  load(st);
+  store(0);
+  __syncthreads();
+  // transposed fragment reads: lane 4q + pq of each 16-lane group addresses row r0 (+4 for the upper half), columns
+  // 16i + 4pq .. +3, and receives column 16i + (lane & 15) at pixels 32*wid + 8g + 0..7 (the MFMA K slice)
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int r0 = 32 * wid + 8 * g + q;
+  int buf = 0;
+  for (; st < steps; st += gridDim.x) {
+    const bool more = st + gridDim.x < steps;
+    if (more) load(st + gridDim.x);
+    s8v af[2], bg[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const s4v lo = tr_read(&sX[buf][r0][16 * i + 4 * pq]);
+      const s4v hi = tr_read(&sX[buf][r0 + 4][16 * i + 4 * pq]);
+      af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const s4v glo = tr_read(&sG[buf][r0][16 * i + 4 * pq]);
+      const s4v ghi = tr_read(&sG[buf][r0 + 4][16 * i + 4 * pq]);
+      bg[i] = s8v{glo[0], glo[1], glo[2], glo[3], ghi[0], ghi[1], ghi[2], ghi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bg[j], acc[i][j], 0, 0, 0);
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // C: tap 16i + 4g + r, channel 16j + (lane & 15); the 4 waves' pixel slices summed through LDS
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(16 * i + 4 * g + r) * 32 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 27 * 32;
+  for (int e = tid; e < 27 * 32; e += NT)
+    atomicAdd(&dst[e], (red[0][e] + red[1][e] + red[2][e] + red[3][e]) * (1.f / 255.f));
+}
+
 bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
+
+bool use_mfma(const EntryParams& p) { return p.Cout == 32 && cfl_tune(TUNE_ENTRY_ALGO) != 1; }
 
 }  // namespace
 
@@ -148,9 +337,14 @@ int entry_fwd(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
+  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 1024;
+  if (use_mfma(p)) {
+    const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
+    hipLaunchKernelGGL(entry_fwd_mfma_kernel, dim3(steps < cap ? steps : cap), dim3(NT), 0, st, p, nch, steps);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   const size_t lds = (size_t)3 * p.S * 3 * sizeof(float);
   if (lds > 48 * 1024) return 1;
-  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 1024;
   hipLaunchKernelGGL(entry_fwd_kernel, dim3(rows < cap ? rows : cap), dim3(NT), lds, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
@@ -159,8 +353,15 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
-  const int cap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 256;   // measured
   const int reps = p.replicas > 1 ? p.replicas : 1;
+  if (use_mfma(p)) {
+    const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
+    const int mcap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 512;
+    hipLaunchKernelGGL(entry_wgrad_mfma_kernel, dim3(steps < mcap ? steps : mcap), dim3(NT), 0, st, p, nch, steps,
+                       reps);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
+  const int cap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 256;   // measured
   hipLaunchKernelGGL(entry_wgrad_kernel, dim3(rows < cap ? rows : cap, 3), dim3(NT), (size_t)p.S * 3 * sizeof(float),
                      st, p, reps);
   return hipGetLastError() == hipSuccess ? 0 : 3;

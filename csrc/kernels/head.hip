@@ -7,6 +7,10 @@
 // dataset through the batch index vector. Optional Dice term (north-star "Dice/BCE loss").
 //   head_fwd: h = x . w + b; accumulates bce, correct pixels and the Dice sums (I, P, T)
 //   head_bwd: dh = sum_children (sigmoid(h) - t) / (B*S*S) [+ Dice grad]; dx = dh * w; dw, db reductions
+// Four lanes per low-resolution pixel: lane q = tid & 3 owns channels 8q .. 8q+7 (one 16-byte load; the partial dot
+// products meet through two lane shuffles) and target sub-pixel (q >> 1, q & 1) of the pixel's 2x2 block, so a
+// wave's activation loads / stores are 1 KiB contiguous and the loss terms spread over every lane (one pixel per
+// thread with a 64-byte row each left the head latency-bound).
 #include "common.h"
 #include "launch.h"
 
@@ -14,44 +18,47 @@ namespace {
 
 constexpr int NT = 256;
 constexpr float DICE_SMOOTH = 1.0f;
+constexpr int HEAD_BLOCKS = 1024;
 
 // metrics layout (double): [0] bce sum, [1] correct, [2] pixels, [3] dice loss sum, [4] I, [5] P, [6] T (soft, this
 // step), [7] TP (predicted AND true crack pixels), [8] PP (predicted crack pixels) - hard-threshold IoU / Dice
 
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
+  static_assert(CIN == 32, "4 lanes x 8 channels per pixel");
   __shared__ double red[7][NT / 64];
   const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
+  const int q = threadIdx.x & 3;
+  float w[8];
+  load_f8(p.w + 8 * q, w);
+  const float bias = p.bias[0];
   double bce = 0, cor = 0, I = 0, P = 0, T = 0, TP = 0, PP = 0;
-  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
+  // the grid stride is a multiple of 4: the 4 lanes of a pixel take every trip together (shuffles below)
+  for (int t = blockIdx.x * NT + threadIdx.x; (t >> 2) < npix; t += gridDim.x * NT) {
+    const int pix = t >> 2;
+    float f[8];
+    load8(p.x + (size_t)pix * CIN + 8 * q, f);
+    float h = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h = fmaf(f[k], w[k], h);
+    h += __shfl_xor(h, 1, 64);          // commutative pairings: all 4 lanes end with the same bits
+    h += __shfl_xor(h, 2, 64);
+    h += bias;
+    if (q == 0) p.h[pix] = h;
     const int j = pix % p.R, i = (pix / p.R) % p.R;
     const int b = pix / (p.R * p.R);
-    float h = p.bias[0];
-#pragma unroll
-    for (int c0 = 0; c0 < CIN; c0 += 8) {
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.x + pix * CIN + c0), f);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) h = fmaf(f[k], p.w[c0 + k], h);
-    }
-    p.h[pix] = h;
+    const float tt =
+        p.masks[(int64_t)p.idx[b] * S * S + (2 * i + (q >> 1)) * S + 2 * j + (q & 1)] ? 1.f : 0.f;
     const float sp = fmaxf(h, 0.f) + log1pf(expf(-fabsf(h)));   // softplus(h) = BCE for t = 0
     const float sg = 1.f / (1.f + expf(-h));
-    const uint8_t* mrow = p.masks + (int64_t)p.idx[b] * S * S;
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const float t = mrow[(2 * i + dy) * S + 2 * j + dx] ? 1.f : 0.f;
-        bce += sp - h * t;
-        cor += ((h > 0.f) == (t > 0.5f)) ? 1.0 : 0.0;
-        TP += (h > 0.f && t > 0.5f) ? 1.0 : 0.0;
-        PP += h > 0.f ? 1.0 : 0.0;
-        I += sg * t;
-        P += sg;
-        T += t;
-      }
+    bce += sp - h * tt;
+    cor += ((h > 0.f) == (tt > 0.5f)) ? 1.0 : 0.0;
+    TP += (h > 0.f && tt > 0.5f) ? 1.0 : 0.0;
+    PP += h > 0.f ? 1.0 : 0.0;
+    I += sg * tt;
+    P += sg;
+    T += tt;
   }
   double v[7] = {bce, cor, I, P, T, TP, PP};
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -73,9 +80,11 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
 
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
+  static_assert(CIN == 32, "4 lanes x 8 channels per pixel");
   __shared__ float red[CIN + 1][NT / 64];
   const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
+  const int q = threadIdx.x & 3;
   const float inv_n = 1.f / (float)(npix * 4);
   float dI = 0.f, dP = 0.f, den = 1.f;
   if (p.dice) {
@@ -85,68 +94,67 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
     dP = (2.f * I + DICE_SMOOTH) / (den * den);        // d/dP (and d/dT)
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.metrics[3], (double)(1.f - (2.f * I + DICE_SMOOTH) / den));
   }
-  float gw[CIN];
+  float w[8], gw[8];
+  load_f8(p.w + 8 * q, w);
 #pragma unroll
-  for (int c = 0; c < CIN; ++c) gw[c] = 0.f;
+  for (int k = 0; k < 8; ++k) gw[k] = 0.f;
   float gb = 0.f;
-  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
-    const int j = pix % p.R, i = (pix / p.R) % p.R;
-    const int b = pix / (p.R * p.R);
+  for (int t = blockIdx.x * NT + threadIdx.x; (t >> 2) < npix; t += gridDim.x * NT) {
+    const int pix = t >> 2;
     const float h = p.h[pix];
     const float sg = 1.f / (1.f + expf(-h));
-    const uint8_t* mrow = p.masks + (int64_t)p.idx[b] * S * S;
-    float dh = 0.f;
+    const int j = pix % p.R, i = (pix / p.R) % p.R;
+    const int b = pix / (p.R * p.R);
+    const float tt =
+        p.masks[(int64_t)p.idx[b] * S * S + (2 * i + (q >> 1)) * S + 2 * j + (q & 1)] ? 1.f : 0.f;
+    float dh = (sg - tt) * inv_n;
+    if (p.dice) dh += (dI * tt + dP) * sg * (1.f - sg);
+    dh += __shfl_xor(dh, 1, 64);        // the pixel's gradient: sum over its 2x2 target block
+    dh += __shfl_xor(dh, 2, 64);
+    if (q == 0) gb += dh;
+    float f[8], o[8];
+    load8(p.x + (size_t)pix * CIN + 8 * q, f);
 #pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const float t = mrow[(2 * i + dy) * S + 2 * j + dx] ? 1.f : 0.f;
-        dh += (sg - t) * inv_n;
-        if (p.dice) dh += (dI * t + dP) * sg * (1.f - sg);
-      }
-    gb += dh;
-#pragma unroll
-    for (int c0 = 0; c0 < CIN; c0 += 8) {
-      float f[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.x + pix * CIN + c0), f);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        o[k] = dh * p.w[c0 + k];
-        gw[c0 + k] = fmaf(dh, f[k], gw[c0 + k]);
-      }
-      *reinterpret_cast<uint4*>(p.dx + pix * CIN + c0) = pack8(o);
+    for (int k = 0; k < 8; ++k) {
+      o[k] = dh * w[k];
+      gw[k] = fmaf(dh, f[k], gw[k]);
     }
+    *reinterpret_cast<uint4*>(p.dx + (size_t)pix * CIN + 8 * q) = pack8(o);
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int c = 0; c <= CIN; ++c) {
-    float x = c < CIN ? gw[c] : gb;
-    x = wave_sum(x);
-    if (lane == 0) red[c][wid] = x;
+  for (int k = 0; k < 8; ++k)
+    for (int o = 4; o < 64; o <<= 1) gw[k] += __shfl_xor(gw[k], o, 64);   // lanes of one q hold the same channels
+  gb = wave_sum(gb);
+  if (lane < 4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[8 * lane + k][wid] = gw[k];
   }
+  if (lane == 0) red[CIN][wid] = gb;
   __syncthreads();
   if (threadIdx.x <= CIN) {
     float s = 0.f;
-    for (int w = 0; w < NT / 64; ++w) s += red[threadIdx.x][w];
+    for (int w2 = 0; w2 < NT / 64; ++w2) s += red[threadIdx.x][w2];
     if (threadIdx.x < CIN) atomicAdd(&p.dw[threadIdx.x], s);
     else atomicAdd(p.db, s);
   }
+}
+
+int head_blocks(const HeadParams& p) {
+  const int64_t blocks = ((int64_t)p.B * p.R * p.R * 4 + NT - 1) / NT;
+  return (int)(blocks > HEAD_BLOCKS ? HEAD_BLOCKS : (blocks < 1 ? 1 : blocks));
 }
 
 }  // namespace
 
 int head_fwd(const HeadParams& p, hipStream_t st) {
   if (p.Cin != 32) return 1;
-  int64_t blocks = ((int64_t)p.B * p.R * p.R + NT - 1) / NT;
-  if (blocks > 512) blocks = 512;
-  hipLaunchKernelGGL(head_fwd_kernel<32>, dim3((int)blocks), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(head_blocks(p)), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int head_bwd(const HeadParams& p, hipStream_t st) {
   if (p.Cin != 32) return 1;
-  int64_t blocks = ((int64_t)p.B * p.R * p.R + NT - 1) / NT;
-  if (blocks > 512) blocks = 512;
-  hipLaunchKernelGGL(head_bwd_kernel<32>, dim3((int)blocks), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(head_blocks(p)), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

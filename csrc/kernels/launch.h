@@ -288,6 +288,7 @@ enum TuneKey {
   TUNE_CONV3_SMALL = 9,        // conv3x3 low-M layers: 0 = heuristic, 1 = split-K (+ epilogue launch), 2 = 8x8x32 tiles
   TUNE_CONV3_BN = 10,          // conv3x3 whole-chunk path: output-channel tile (0 = 64 when N % 64 == 0, else 32)
   TUNE_NODE_POOL2X2 = 11,      // max-pool node gradient: 0 = 2x2-block kernel, 1 = per-pixel gather
+  TUNE_ENTRY_ALGO = 12,        // entry conv (Cout 32): 0 = MFMA kernels, 1 = VALU kernels
   TUNE_N = 16
 };
 int cfl_tune(int key);

@@ -60,6 +60,30 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
   const int total = N * K;                      // < 2^31 for every layer (32-bit index math, no 64-bit division)
   const float* src = flat + v.src;
   bf16_t* dst = packed + v.dst;
+  if (v.kind == PK_CONV || v.kind == PK_CONVT_DGRAD || v.kind == PK_PW) {
+    // these views are plain transposes of the Keras array: src is [K][N] (N contiguous), dst [N][K]. Staged
+    // through a 64x64 LDS tile so both the fp32 reads and the bf16 writes are coalesced rows (a per-element
+    // gather reads one float per cache line at stride N)
+    __shared__ float tl[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int tk = (K + 63) >> 6, tn = (N + 63) >> 6;
+    for (int t = blockIdx.x; t < tk * tn; t += gridDim.x) {   // block-uniform loop: the barriers are safe
+      const int k0 = (t / tn) << 6, n0 = (t % tn) << 6;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = k0 + ty + 4 * j, n = n0 + tx;
+        tl[ty + 4 * j][tx] = (k < K && n < N) ? src[k * N + n] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int n = n0 + ty + 4 * j, k = k0 + tx;
+        if (n < N && k < K) dst[n * K + k] = f2bf(tl[tx][ty + 4 * j]);
+      }
+      __syncthreads();
+    }
+    return;
+  }
   for (int e = blockIdx.x * NT + threadIdx.x; e < total; e += gridDim.x * NT) {
     const int n = e / K, k = e - n * K;
     int s;
@@ -94,9 +118,12 @@ __global__ void gather_rows_kernel(const uint8_t* src, const int32_t* idx, uint8
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < row_bytes; i += (int64_t)gridDim.x * NT) d[i] = s[i];
 }
 
-// One block per work item = (entry, 1024-float element tile, group of GF_ROWS rows): the rows are loaded as 16
-// independent float4 loads per thread (memory-level parallelism over a long row list), summed, and added to the
-// destination - plainly when the entry has a single row group, else with one atomic per element per group.
+// One block per work item = (entry, 1024-float element tile, group of GF_ROWS rows). Thread t owns elements
+// 256 * u + t (u = 0..3) of the tile, so every load / store / atomic wave-instruction covers 256 contiguous bytes - the
+// full-rate shape of the memory-side float atomics (a float4 per lane split into four scalar atomics put each
+// instruction's lanes 16 B apart: four times the atomic requests). The GF_ROWS x 4 loads are issued before any sum
+// (memory-level parallelism over a long row list); the sum goes to the destination plainly when the entry has a
+// single row group, else with one atomic per element per group.
 constexpr int GF_ROWS = 16;
 
 __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __restrict__ e, int n_entries) {
@@ -108,37 +135,40 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
   const int ngroups = (rows + GF_ROWS - 1) / GF_ROWS;
   const int local = blockIdx.x - g.work_begin;
   const int tile = local / ngroups, rg = local - tile * ngroups;
-  const int i4 = tile * NT + threadIdx.x;
-  const int n4 = g.n >> 2;
-  if (i4 >= n4) return;
-  float4* src = reinterpret_cast<float4*>(g.src);
-  float4* dst = reinterpret_cast<float4*>(g.dst);
+  const int i0 = tile * 4 * NT + threadIdx.x;
   if (g.mode == GF_COPY) {
-    dst[i4] = src[i4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * NT < g.n) g.dst[i0 + u * NT] = g.src[i0 + u * NT];
     return;
   }
   const int r0 = rg * GF_ROWS;
-  float4 v[GF_ROWS];
+  float v[GF_ROWS][4];
 #pragma unroll
   for (int r = 0; r < GF_ROWS; ++r)
-    v[r] = r0 + r < rows ? src[(size_t)(r0 + r) * n4 + i4] : make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int r = 0; r < GF_ROWS; ++r) {
-    s.x += v[r].x; s.y += v[r].y; s.z += v[r].z; s.w += v[r].w;
-  }
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT;
+      v[r][u] = (r0 + r < rows && i < g.n) ? g.src[(size_t)(r0 + r) * g.n + i] : 0.f;
+    }
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < GF_ROWS; ++r)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] += v[r][u];
   if (g.mode == GF_REDUCE) {        // atomic replica rows: re-zero for the next step
 #pragma unroll
     for (int r = 0; r < GF_ROWS; ++r)
-      if (r0 + r < rows) src[(size_t)(r0 + r) * n4 + i4] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r0 + r < rows && i0 + u * NT < g.n) g.src[(size_t)(r0 + r) * g.n + i0 + u * NT] = 0.f;
   }
-  if (ngroups == 1) {
-    float4 d = dst[i4];
-    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
-    dst[i4] = d;
-  } else {
-    float* d = g.dst + 4 * (size_t)i4;
-    atomicAdd(d, s.x); atomicAdd(d + 1, s.y); atomicAdd(d + 2, s.z); atomicAdd(d + 3, s.w);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u * NT;
+    if (i >= g.n) continue;
+    if (ngroups == 1) g.dst[i] += s[u];
+    else atomicAdd(&g.dst[i], s[u]);
   }
 }
 

@@ -821,3 +821,86 @@ def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C):
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-3)
     # every pooled gradient lands exactly once: total mass is preserved
     assert abs(float(from_bits(outs[1][0]).sum()) - float(from_bits(dxb).sum())) < 1e-2 * B * H * H
+
+
+@pytest.mark.parametrize("S,B", [(64, 3), (256, 2), (512, 1)])
+def test_entry_conv_mfma_and_valu_match_reference(S, B):
+    """entry.hip: the MFMA forward / weight gradient (Cout 32; pixels as exact integers in bf16, /255 on the fp32
+    accumulator; one or several 128-pixel chunks per row) and the VALU kernels (TUNE_ENTRY_ALGO=1) against the fp32
+    TF-SAME stride-2 conv (bottom/right pad) of the batch gathered through the index vector."""
+    C = hip()
+    g = torch.Generator().manual_seed(31)
+    imgs = torch.randint(0, 256, (5, S, S, 3), dtype=torch.uint8, generator=g)
+    idx = torch.tensor([4, 0, 2][:B], dtype=torch.int32)
+    w = torch.randn(3, 3, 3, 32, generator=g) * 0.2
+    bias = torch.randn(32, generator=g) * 0.1
+    Ho = S // 2
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, 32, generator=g))
+    x = imgs[idx.long()].float().div(255.0).permute(0, 3, 1, 2)
+    wr = w.clone().requires_grad_(True)
+    yref = R.conv2d_same(x, wr, bias, 2)
+    gw, = torch.autograd.grad(yref, wr, dyf.permute(0, 3, 1, 2))
+    yref = yref.detach().permute(0, 2, 3, 1)
+    reps = C.STAT_REPLICAS
+    ys = []
+    for algo in (0, 1):
+        C.set_tune(C.TUNE_ENTRY_ALGO, algo)
+        try:
+            y = torch.zeros(B, Ho, Ho, 32, dtype=torch.int16, device=DEV)
+            stats = torch.zeros(reps * 64, device=DEV)
+            C.entry_fwd(imgs.to(DEV), idx.to(DEV), w.reshape(-1).to(DEV), bias.to(DEV), y, stats, B, S, 32)
+            dw = torch.zeros(4 * 27 * 32, device=DEV)
+            C.entry_wgrad(imgs.to(DEV), idx.to(DEV), dyb, dw, B, S, 32, 4)
+            torch.cuda.synchronize()
+        finally:
+            C.set_tune(C.TUNE_ENTRY_ALGO, 0)
+        yk = from_bits(y)
+        assert rel(yk, yref) < 1e-2, (algo, rel(yk, yref))
+        st = stats.view(reps, 2, 32).sum(0).cpu()
+        assert torch.allclose(st[0], yk.sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
+        assert torch.allclose(st[1], (yk * yk).sum((0, 1, 2)), rtol=1e-3, atol=1e-1)
+        dwk = dw.view(4, 3, 3, 3, 32).sum(0).cpu()
+        assert rel(dwk, gw) < 2e-3, (algo, rel(dwk, gw))
+        ys.append(yk)
+    assert rel(ys[0], ys[1]) < 1e-2
+
+
+@pytest.mark.parametrize("dice", [0, 1])
+def test_head_loss_metrics_and_gradients_match_autograd(dice):
+    """head.hip (4 lanes per low-resolution pixel: 8 channels and one sub-pixel of the 2x2 target block each):
+    logits, BCE / accuracy / Dice sums and dx, dw, db against autograd of the fp32 head on the 2x-upsampled logits
+    (UpSampling2D commutes with the 1x1 conv), masks gathered through the batch index vector."""
+    C = hip()
+    g = torch.Generator().manual_seed(41)
+    B, Rr = 3, 24
+    S = 2 * Rr
+    xb, xf = bf(torch.randn(B, Rr, Rr, 32, generator=g))
+    w = torch.randn(32, generator=g) * 0.3
+    bias = torch.randn(1, generator=g) * 0.1
+    masks = (torch.rand(5, S, S, generator=g) > 0.7).to(torch.uint8)
+    idx = torch.tensor([3, 1, 4], dtype=torch.int32)
+    h = torch.zeros(B, Rr, Rr, device=DEV)
+    met = torch.zeros(10, dtype=torch.float64, device=DEV)
+    dx = torch.zeros(B, Rr, Rr, 32, dtype=torch.int16, device=DEV)
+    dw, db = torch.zeros(32, device=DEV), torch.zeros(1, device=DEV)
+    args = (xb, w.to(DEV), bias.to(DEV), masks.to(DEV), idx.to(DEV), h, met)
+    C.head_fwd(*args, B, Rr, 32, dice)
+    C.head_bwd(*args, dx, dw, db, B, Rr, 32, dice)
+    torch.cuda.synchronize()
+    xr, wr, br = xf.clone().requires_grad_(True), w.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+    logit = xr @ wr + br
+    up = logit.repeat_interleave(2, 1).repeat_interleave(2, 2)
+    t = masks[idx.long()].float()
+    loss = R.seg_loss(up, t, "bce_dice" if dice else "bce")
+    gx, gw, gb = torch.autograd.grad(loss, (xr, wr, br))
+    assert torch.allclose(h.cpu(), logit.detach(), atol=1e-4, rtol=1e-4)
+    m = met.cpu()
+    n = B * S * S
+    assert m[2] == n
+    assert abs(float(m[0]) / n - float(R.bce_with_logits_mean(up.detach(), t))) < 1e-5
+    assert abs(float(m[1]) / n - float(R.binary_accuracy(up.detach(), t))) < 1e-6
+    p = torch.sigmoid(up.detach())
+    assert abs(float(m[4]) - float((p * t).sum())) < 1e-2 and abs(float(m[5]) - float(p.sum())) < 1e-2
+    assert float(m[6]) == float(t.sum())
+    assert rel(from_bits(dx), gx) < 1e-2
+    assert rel(dw.cpu(), gw) < 1e-3 and rel(db.cpu(), gb) < 1e-3
