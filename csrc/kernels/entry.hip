@@ -142,54 +142,70 @@ __global__ __launch_bounds__(NT) void entry_wgrad_kernel(EntryParams p, int repl
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// MFMA forms for Cout == 32 (the network's entry width). An output pixel's 27 taps (ky, kx, ci) are gathered from the
-// uint8 rows as the integers 0..255 - exact in bf16; the /255 goes onto the fp32 accumulator - zero-padded to K = 32
-// and staged per step of ECH output pixels as an LDS [pixel][tap] bf16 tile:
+// MFMA forms for Cout == 32 (the network's entry width). A step covers ECH output pixels of one output row: the three
+// input rows it reads (columns 2*ow0 .. 2*ow0 + 2*ECH) are staged as raw bytes in LDS with dword loads (zeros past the
+// image's bottom / right edge = TF "same" padding), and every lane builds its MFMA operand straight from those
+// bytes: the 27 taps (ky, kx, ci) of a pixel as the integers 0..255 - exact in bf16; the /255 goes onto the fp32
+// accumulator - zero-padded to K = 32:
 //   forward  y[pix][co]  = bias[co] + (1/255) * X[pix][0:32] . W[0:32][co]   (W rounded to bf16, held in registers)
-//   wgrad    dW[tap][co] = (1/255) * sum_pix X[pix][tap] * dy[pix][co]      (the pixel reduction is the MFMA K axis:
-//            both [pixel][*] tiles are read with the transposing ds_read_b64_tr_b16, as conv_wgrad.hip does)
+//   wgrad    dW[tap][co] = (1/255) * sum_pix X[pix][tap] * dy[pix][co]      (the pixel reduction is the MFMA K axis;
+//            the [pixel][channel] dy tile is read with the transposing ds_read_b64_tr_b16, as conv_wgrad.hip does)
 // mfma_f32_16x16x32_bf16 lane maps: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
 // The VALU kernels above stay for other widths (TUNE_ENTRY_ALGO=1 forces them): they are LDS-bandwidth bound, two
 // 16-byte weight reads per 8 FMAs.
-constexpr int ECH = 128;   // output pixels per step (4 waves x 32)
-constexpr int ELD = 40;    // LDS row stride (bf16) of the [pixel][32] tiles (80-byte rows)
+constexpr int ECH = 128;          // output pixels per step (4 waves x 32)
+constexpr int ELD = 40;           // LDS row stride (bf16) of the [pixel][32] dy / y tiles (80-byte rows)
+constexpr int ERB = 784;          // staged bytes per input row: (2 * ECH + 1) * 3 = 771, rounded up to 16
+constexpr int EDW = ERB / 4;      // dwords per staged row
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 CFL_DEVICE s4v tr_read(const bf16_t* q) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(q));
 }
 
-// taps [16h, 16h + 16) of output pixel (row = b*Ho + oh, column ow) as integers; 0 outside the image (TF "same"
-// bottom/right pad), past the row end and for the padding taps >= 27 (addresses clamped, loads unconditional)
-CFL_DEVICE void entry_gather(const EntryParams& p, int row, int ow, int h, uint32_t (&xv)[16]) {
+// byte offset of tap T inside the staged [3][ERB] rows (relative to the pixel's column 2*px), or -1 for T >= 27
+CFL_DEVICE int tap_off(int T) { return T < 27 ? (T / 9) * ERB + ((T / 3) % 3) * 3 + T % 3 : -1; }
+
+// the three input rows of step (row = b*Ho + oh, first output column ow0): thread t holds dwords t, t + NT, t + 2NT
+// of the [3][EDW] image (addresses clamped, loads unconditional)
+CFL_DEVICE void rows_load(const EntryParams& p, int row, int ow0, uint32_t (&rv)[3]) {
   const int b = row / p.Ho, oh = row - b * p.Ho;
-  const uint8_t* img = p.images + (size_t)p.idx[b] * p.S * p.S * 3;
+  const int rowbytes = p.S * 3;                       // multiple of 4 (S % 4 == 0)
+  const uint8_t* img = p.images + (size_t)p.idx[b] * p.S * rowbytes;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int T = 16 * h + i;
-    const int ky = T / 9, kx = (T / 3) % 3, ci = T % 3;
-    const int ih = 2 * oh + ky, iw = 2 * ow + kx;
-    const bool ok = T < 27 && ow < p.Wo && ih < p.S && iw < p.S;
-    const uint32_t v = img[ok ? (ih * p.S + iw) * 3 + ci : 0];
-    xv[i] = ok ? v : 0u;
+  for (int k = 0; k < 3; ++k) {
+    const int e = threadIdx.x + NT * k;
+    const int r = e / EDW, byte = ow0 * 6 + (e - r * EDW) * 4;
+    const int ih = 2 * oh + r;
+    const bool ok = e < 3 * EDW && ih < p.S && byte < rowbytes;
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(img + (ok ? (size_t)ih * rowbytes + byte : 0));
+    rv[k] = ok ? v : 0u;
   }
 }
 
-CFL_DEVICE void entry_put(bf16_t* dst, const uint32_t (&xv)[16]) {
-  uint32_t w[8];
+CFL_DEVICE void rows_store(uint8_t* sR, const uint32_t (&rv)[3]) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) w[k] = pack2bf((float)xv[2 * k], (float)xv[2 * k + 1]);
-  *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-  *reinterpret_cast<uint4*>(dst + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+  for (int k = 0; k < 3; ++k) {
+    const int e = threadIdx.x + NT * k;
+    if (e < 3 * EDW) reinterpret_cast<uint32_t*>(sR)[e] = rv[k];
+  }
+}
+
+// 8 staged bytes at sR + base + off[j] (off < 0: 0) as an MFMA operand of 8 bf16 integers
+CFL_DEVICE s8v bytes_frag(const uint8_t* sR, const int (&off)[8], const int (&stride)[8], int base) {
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = off[j] < 0 ? 0.f : (float)sR[base + off[j] + stride[j]];
+  return __builtin_bit_cast(s8v, u4v{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
+                                     pack2bf(f[6], f[7])});
 }
 
 __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int nch, int steps) {
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][ECH][ELD];
+  __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sY[ECH][ELD];
   __shared__ float red[2][4][256];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int pl = tid & (ECH - 1), h = tid >> 7;
   // B operand (fixed): lane holds output channel 16j + r16 at taps 8g .. 8g+7 (0 for the padding taps)
   s8v wv[2];
 #pragma unroll
@@ -199,24 +215,31 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
       const int T = 8 * g + e;
       wv[j][e] = (short)f2bf(T < 27 ? p.w[T * 32 + 16 * j + r16] : 0.f);
     }
+  // A operand: lane holds pixel 32*wid + 16i + r16 at taps 8g .. 8g+7
+  int off[8], zero[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    off[e] = tap_off(8 * g + e);
+    zero[e] = 0;
+  }
   const float bias0 = p.bias[r16], bias1 = p.bias[16 + r16];
   float s[2][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
-  uint32_t xv[16];
+  uint32_t rv[3];
   int st = blockIdx.x;
-  entry_gather(p, st / nch, (st % nch) * ECH + pl, h, xv);
-  entry_put(&sX[0][pl][16 * h], xv);
+  rows_load(p, st / nch, (st % nch) * ECH, rv);
+  rows_store(sR[0], rv);
   __syncthreads();
   int buf = 0;
   for (; st < steps; st += gridDim.x) {
     const int nxt = st + gridDim.x;
     const bool more = nxt < steps;
-    if (more) entry_gather(p, nxt / nch, (nxt % nch) * ECH + pl, h, xv);   // in flight during this step
+    if (more) rows_load(p, nxt / nch, (nxt % nch) * ECH, rv);   // in flight during this step
     f4v acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const s8v a = *reinterpret_cast<const s8v*>(&sX[buf][32 * wid + 16 * i + r16][8 * g]);
+      const s8v a = bytes_frag(sR[buf], off, zero, 6 * (32 * wid + 16 * i + r16));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wv[j], f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -246,7 +269,7 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
         }
       }
     }
-    if (more) entry_put(&sX[buf ^ 1][pl][16 * h], xv);
+    if (more) rows_store(sR[buf ^ 1], rv);
     __syncthreads();
     buf ^= 1;
   }
@@ -254,16 +277,24 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
 }
 
 __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int nch, int steps, int replicas) {
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][ECH][ELD];
+  __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sG[2][ECH][ELD];
   __shared__ float red[4][32 * 32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int pl = tid & (ECH - 1), h = tid >> 7;
-  uint32_t xv[16];
+  const int g = lane >> 4, r16 = lane & 15;
+  // A operand (X^T): lane holds tap row 16i + r16 at pixels 32*wid + 8g + 0..7 (column stride 2 pixels = 6 bytes)
+  int aoff[2][8], astr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    aoff[0][j] = tap_off(r16);
+    aoff[1][j] = tap_off(16 + r16);
+    astr[j] = 6 * j;
+  }
+  uint32_t rv[3];
   uint4 gv[2];
   auto load = [&](int s) {
     const int row = s / nch, ow0 = (s % nch) * ECH;
-    entry_gather(p, row, ow0 + pl, h, xv);
+    rows_load(p, row, ow0, rv);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + NT * k, ow = ow0 + (e >> 2);
@@ -272,7 +303,7 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
     }
   };
   auto store = [&](int b) {
-    entry_put(&sX[b][pl][16 * h], xv);
+    rows_store(sR[b], rv);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + NT * k;
@@ -288,10 +319,11 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
   load(st);
   store(0);
   __syncthreads();
-  // transposed fragment reads: lane 4q + pq of each 16-lane group addresses row r0 (+4 for the upper half), columns
-  // 16i + 4pq .. +3, and receives column 16i + (lane & 15) at pixels 32*wid + 8g + 0..7 (the MFMA K slice)
-  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  // transposed dy reads: lane 4q + pq of each 16-lane group addresses row r0 (+4 for the upper half), columns
+  // 16j + 4pq .. +3, and receives column 16j + (lane & 15) at pixels 32*wid + 8g + 0..7 (the MFMA K slice)
+  const int q = r16 >> 2, pq = lane & 3;
   const int r0 = 32 * wid + 8 * g + q;
+  const int pbase = 6 * (32 * wid + 8 * g);
   int buf = 0;
   for (; st < steps; st += gridDim.x) {
     const bool more = st + gridDim.x < steps;
@@ -299,9 +331,7 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
     s8v af[2], bg[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const s4v lo = tr_read(&sX[buf][r0][16 * i + 4 * pq]);
-      const s4v hi = tr_read(&sX[buf][r0 + 4][16 * i + 4 * pq]);
-      af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = bytes_frag(sR[buf], aoff[i], astr, pbase);
       const s4v glo = tr_read(&sG[buf][r0][16 * i + 4 * pq]);
       const s4v ghi = tr_read(&sG[buf][r0 + 4][16 * i + 4 * pq]);
       bg[i] = s8v{glo[0], glo[1], glo[2], glo[3], ghi[0], ghi[1], ghi[2], ghi[3]};
@@ -320,7 +350,7 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[wid][(16 * i + 4 * g + r) * 32 + 16 * j + (lane & 15)] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) red[wid][(16 * i + 4 * g + r) * 32 + 16 * j + r16] = acc[i][j][r];
   __syncthreads();
   float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 27 * 32;
   for (int e = tid; e < 27 * 32; e += NT)

@@ -19,6 +19,14 @@ namespace {
 constexpr int NT = 256;
 constexpr float DICE_SMOOTH = 1.0f;
 constexpr int HEAD_BLOCKS = 1024;
+constexpr int HPT = 4;            // pixels per lane per trip (all loads of a trip in flight together)
+
+// target bit of sub-pixel (q >> 1, q & 1) of low-resolution pixel pix, through the batch index vector
+CFL_DEVICE float mask_at(const HeadParams& p, int pix, int S, int q) {
+  const int j = pix % p.R, i = (pix / p.R) % p.R;
+  const int b = pix / (p.R * p.R);
+  return p.masks[(int64_t)p.idx[b] * S * S + (2 * i + (q >> 1)) * S + 2 * j + (q & 1)] ? 1.f : 0.f;
+}
 
 // metrics layout (double): [0] bce sum, [1] correct, [2] pixels, [3] dice loss sum, [4] I, [5] P, [6] T (soft, this
 // step), [7] TP (predicted AND true crack pixels), [8] PP (predicted crack pixels) - hard-threshold IoU / Dice
@@ -34,31 +42,40 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
   load_f8(p.w + 8 * q, w);
   const float bias = p.bias[0];
   double bce = 0, cor = 0, I = 0, P = 0, T = 0, TP = 0, PP = 0;
-  // the grid stride is a multiple of 4: the 4 lanes of a pixel take every trip together (shuffles below)
-  for (int t = blockIdx.x * NT + threadIdx.x; (t >> 2) < npix; t += gridDim.x * NT) {
-    const int pix = t >> 2;
-    float f[8];
-    load8(p.x + (size_t)pix * CIN + 8 * q, f);
-    float h = 0.f;
+  // the grid stride is a multiple of 4: the 4 lanes of a pixel take every trip together (shuffles below); each
+  // trip issues all HPT items' loads (activations, batch index -> mask byte) before any math
+  const int stride = gridDim.x * NT;
+  for (int t0 = blockIdx.x * NT + threadIdx.x; (t0 >> 2) < npix; t0 += HPT * stride) {
+    float f[HPT][8], tt[HPT];
+    int pix[HPT];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h = fmaf(f[k], w[k], h);
-    h += __shfl_xor(h, 1, 64);          // commutative pairings: all 4 lanes end with the same bits
-    h += __shfl_xor(h, 2, 64);
-    h += bias;
-    if (q == 0) p.h[pix] = h;
-    const int j = pix % p.R, i = (pix / p.R) % p.R;
-    const int b = pix / (p.R * p.R);
-    const float tt =
-        p.masks[(int64_t)p.idx[b] * S * S + (2 * i + (q >> 1)) * S + 2 * j + (q & 1)] ? 1.f : 0.f;
-    const float sp = fmaxf(h, 0.f) + log1pf(expf(-fabsf(h)));   // softplus(h) = BCE for t = 0
-    const float sg = 1.f / (1.f + expf(-h));
-    bce += sp - h * tt;
-    cor += ((h > 0.f) == (tt > 0.5f)) ? 1.0 : 0.0;
-    TP += (h > 0.f && tt > 0.5f) ? 1.0 : 0.0;
-    PP += h > 0.f ? 1.0 : 0.0;
-    I += sg * tt;
-    P += sg;
-    T += tt;
+    for (int u = 0; u < HPT; ++u) {
+      const int t = t0 + u * stride;
+      pix[u] = (t >> 2) < npix ? t >> 2 : -1;
+      const int pc = pix[u] < 0 ? 0 : pix[u];
+      load8(p.x + (size_t)pc * CIN + 8 * q, f[u]);
+      tt[u] = mask_at(p, pc, S, q);
+    }
+#pragma unroll
+    for (int u = 0; u < HPT; ++u) {
+      float h = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h = fmaf(f[u][k], w[k], h);
+      h += __shfl_xor(h, 1, 64);        // commutative pairings: all 4 lanes end with the same bits
+      h += __shfl_xor(h, 2, 64);
+      h += bias;
+      if (pix[u] < 0) continue;
+      if (q == 0) p.h[pix[u]] = h;
+      const float sp = fmaxf(h, 0.f) + log1pf(expf(-fabsf(h)));   // softplus(h) = BCE for t = 0
+      const float sg = 1.f / (1.f + expf(-h));
+      bce += sp - h * tt[u];
+      cor += ((h > 0.f) == (tt[u] > 0.5f)) ? 1.0 : 0.0;
+      TP += (h > 0.f && tt[u] > 0.5f) ? 1.0 : 0.0;
+      PP += h > 0.f ? 1.0 : 0.0;
+      I += sg * tt[u];
+      P += sg;
+      T += tt[u];
+    }
   }
   double v[7] = {bce, cor, I, P, T, TP, PP};
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -99,27 +116,36 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) gw[k] = 0.f;
   float gb = 0.f;
-  for (int t = blockIdx.x * NT + threadIdx.x; (t >> 2) < npix; t += gridDim.x * NT) {
-    const int pix = t >> 2;
-    const float h = p.h[pix];
-    const float sg = 1.f / (1.f + expf(-h));
-    const int j = pix % p.R, i = (pix / p.R) % p.R;
-    const int b = pix / (p.R * p.R);
-    const float tt =
-        p.masks[(int64_t)p.idx[b] * S * S + (2 * i + (q >> 1)) * S + 2 * j + (q & 1)] ? 1.f : 0.f;
-    float dh = (sg - tt) * inv_n;
-    if (p.dice) dh += (dI * tt + dP) * sg * (1.f - sg);
-    dh += __shfl_xor(dh, 1, 64);        // the pixel's gradient: sum over its 2x2 target block
-    dh += __shfl_xor(dh, 2, 64);
-    if (q == 0) gb += dh;
-    float f[8], o[8];
-    load8(p.x + (size_t)pix * CIN + 8 * q, f);
+  const int stride = gridDim.x * NT;
+  for (int t0 = blockIdx.x * NT + threadIdx.x; (t0 >> 2) < npix; t0 += HPT * stride) {
+    float f[HPT][8], hv[HPT], tt[HPT];
+    int pix[HPT];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      o[k] = dh * w[k];
-      gw[k] = fmaf(dh, f[k], gw[k]);
+    for (int u = 0; u < HPT; ++u) {     // all loads first (see head_fwd_kernel)
+      const int t = t0 + u * stride;
+      pix[u] = (t >> 2) < npix ? t >> 2 : -1;
+      const int pc = pix[u] < 0 ? 0 : pix[u];
+      hv[u] = p.h[pc];
+      load8(p.x + (size_t)pc * CIN + 8 * q, f[u]);
+      tt[u] = mask_at(p, pc, S, q);
     }
-    *reinterpret_cast<uint4*>(p.dx + (size_t)pix * CIN + 8 * q) = pack8(o);
+#pragma unroll
+    for (int u = 0; u < HPT; ++u) {
+      const float sg = 1.f / (1.f + expf(-hv[u]));
+      float dh = (sg - tt[u]) * inv_n;
+      if (p.dice) dh += (dI * tt[u] + dP) * sg * (1.f - sg);
+      dh += __shfl_xor(dh, 1, 64);      // the pixel's gradient: sum over its 2x2 target block
+      dh += __shfl_xor(dh, 2, 64);
+      if (pix[u] < 0) continue;
+      if (q == 0) gb += dh;
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o[k] = dh * w[k];
+        gw[k] = fmaf(dh, f[u][k], gw[k]);
+      }
+      *reinterpret_cast<uint4*>(p.dx + (size_t)pix[u] * CIN + 8 * q) = pack8(o);
+    }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -141,7 +167,7 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 }
 
 int head_blocks(const HeadParams& p) {
-  const int64_t blocks = ((int64_t)p.B * p.R * p.R * 4 + NT - 1) / NT;
+  const int64_t blocks = ((int64_t)p.B * p.R * p.R * 4 + HPT * NT - 1) / (HPT * NT);
   return (int)(blocks > HEAD_BLOCKS ? HEAD_BLOCKS : (blocks < 1 ? 1 : blocks));
 }
 
