@@ -18,7 +18,11 @@ namespace {
 
 constexpr int NT = 256;
 constexpr float DICE_SMOOTH = 1.0f;
-constexpr int HEAD_BLOCKS = 1024;
+// grid cap: every block ends with same-address atomics (7 doubles fwd, 33 floats bwd) that serialise at the memory
+// side - 1024 blocks: 19.9 / 19.4 us, 512: 15.0 / 13.7 us, 256: 17.1 / 13.4 us (fwd / bwd, bench shape). A per-block
+// slot + last-block reduction needs device-scope release/acquire fences (an L2 writeback / invalidate per block on
+// the multi-XCD part) and measured 84 / 153 us.
+constexpr int HEAD_BLOCKS = 512;
 constexpr int HPT = 4;            // pixels per lane per trip (all loads of a trip in flight together)
 
 // target bit of sub-pixel (q >> 1, q & 1) of low-resolution pixel pix, through the batch index vector
@@ -168,7 +172,8 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 
 int head_blocks(const HeadParams& p) {
   const int64_t blocks = ((int64_t)p.B * p.R * p.R * 4 + HPT * NT - 1) / (HPT * NT);
-  return (int)(blocks > HEAD_BLOCKS ? HEAD_BLOCKS : (blocks < 1 ? 1 : blocks));
+  const int cap = cfl_tune(TUNE_HEAD_BLOCKS) > 0 ? cfl_tune(TUNE_HEAD_BLOCKS) : HEAD_BLOCKS;
+  return (int)(blocks > cap ? cap : (blocks < 1 ? 1 : blocks));
 }
 
 }  // namespace

@@ -289,6 +289,7 @@ enum TuneKey {
   TUNE_CONV3_BN = 10,          // conv3x3 whole-chunk path: output-channel tile (0 = 64 when N % 64 == 0, else 32)
   TUNE_NODE_POOL2X2 = 11,      // max-pool node gradient: 0 = 2x2-block kernel, 1 = per-pixel gather
   TUNE_ENTRY_ALGO = 12,        // entry conv (Cout 32): 0 = MFMA kernels, 1 = VALU kernels
+  TUNE_HEAD_BLOCKS = 13,       // head fwd / bwd grid cap (default 512)
   TUNE_N = 16
 };
 int cfl_tune(int key);
