@@ -42,6 +42,8 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="decoder Conv2DTranspose forward in fp8 e4m3 (config 5)")
     ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
+    ap.add_argument("--profile-eval-steps", type=int, default=0,
+                    help="if >0: run this many validation (inference) steps at the bench's eval batch and exit")
     args = ap.parse_args()
 
     import numpy as np
@@ -95,6 +97,15 @@ def main() -> int:
     vimg = epoch_batches(data.val_idx, args.batch, 0, 0)[:val_steps].reshape(-1) if val_steps else None
     ev = eng.evaluator(eng.eval_batch_for(len(vimg))) if val_steps else None
     vbatches = torch.as_tensor(vimg.reshape(-1, ev.B), dtype=torch.int32, device=dev) if val_steps else None
+
+    if args.profile_eval_steps and val_steps:
+        for s in range(args.profile_eval_steps):
+            ev.idx.copy_(vbatches[s % vbatches.shape[0]])
+            ev.eval_step(use_graph)
+        torch.cuda.synchronize()
+        print(json.dumps({"profile_eval_steps": args.profile_eval_steps, "eval_batch": ev.B,
+                          "metrics": ev.read_metrics("eval")}))
+        return 0
 
     def fl_round() -> None:
         eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
