@@ -405,7 +405,7 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
   const int64_t items = (int64_t)p.B * p.H * p.W * (p.C / 8);
   int blocks = (int)((items + 2 * NT - 1) / (2 * NT));
-  const int cap = cfl_tune(TUNE_NODE_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_NODE_BWD_BLOCKS) : 1024;
+  const int cap = cfl_tune(TUNE_NODE_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_NODE_BWD_BLOCKS) : 512;   // A/B-measured
   if (blocks > cap) blocks = cap;     // bounded grid: one set of channel atomics per block
   if (blocks < 1) blocks = 1;
   const int m0 = p.src[0].mode, m1 = p.src[1].mode;

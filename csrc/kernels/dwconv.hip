@@ -672,7 +672,7 @@ template <int MODE>
 int launch_stream(const DwParams& p, int replicas, hipStream_t st) {
   const int steps = (p.H + dws::SR - 1) / dws::SR;
   const int strips = p.B * ((p.W + 31) / 32) * (p.C / dws::CT);
-  const int target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 1024;
+  const int target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 768;   // A/B-measured (256 / 384 / 512 / 768 / 1024 / 2048)
   int nseg = (target + strips - 1) / strips;
   nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
   const int seg_rows = ((steps + nseg - 1) / nseg) * dws::SR;

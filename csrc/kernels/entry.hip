@@ -367,7 +367,7 @@ int entry_fwd(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
-  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 1024;
+  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 512;   // A/B-measured
   if (use_mfma(p)) {
     const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
     hipLaunchKernelGGL(entry_fwd_mfma_kernel, dim3(steps < cap ? steps : cap), dim3(NT), 0, st, p, nch, steps);
