@@ -279,7 +279,7 @@ int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStrea
 // launch-shape tuning knobs (0 = built-in heuristic), set from Python for micro-benchmark sweeps
 enum TuneKey {
   TUNE_NODE_BWD_BLOCKS = 0, TUNE_DW_WGRAD_BLOCKS = 1, TUNE_ENTRY_WGRAD_BLOCKS = 2,
-  TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 768)
+  TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 512)
   TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 4)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
