@@ -44,6 +44,11 @@ def main() -> int:
     ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
     ap.add_argument("--profile-eval-steps", type=int, default=0,
                     help="if >0: run this many validation (inference) steps at the bench's eval batch and exit")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo: rehearsal of N ranks "
+                         "sharing one GPU, which RCCL refuses)")
+    ap.add_argument("--verify-fedavg", action="store_true",
+                    help="after the timed rounds, check one weighted FedAvg against an all-gathered reference")
     args = ap.parse_args()
 
     import numpy as np
@@ -53,10 +58,20 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 ranks with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus} (one rank per GPU)")
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev)               # local % ndev: a gloo rehearsal may share one GPU
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+        print(f"[bench] rank {rank}/{world} local_rank {local} -> {dev} ({torch.cuda.get_device_name(dev)}, "
+              f"{ndev} visible), backend {dist.get_backend()}, master "
+              f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}", file=sys.stderr, flush=True)
 
     from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
     from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
@@ -73,7 +88,9 @@ def main() -> int:
         args.batch = plan.batch
         if args.local_steps == 388:                        # reference epoch = 6213 // batch iterations
             args.local_steps = max(1, min(6213, args.samples) // args.batch)
-    data = make_synthetic_device(args.samples, args.img, seed=1000 + rank, split=min(6213, args.samples))
+    # reference split: the first 6213 of the ~8k images train, the rest validate (kept in proportion for small sets)
+    data = make_synthetic_device(args.samples, args.img, seed=1000 + rank,
+                                 split=min(6213, max(args.batch, int(args.samples * 0.7766))))
     eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
@@ -145,6 +162,26 @@ def main() -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    fedavg_err = None
+    if args.verify_fedavg and agg is not None:
+        # one weighted FedAvg with unequal n_k against sum_k n_k w_k / sum n from all-gathered copies
+        eng._await_all()
+        n_k = float(n_local + 97 * rank)
+        mine = eng.flat.clone()
+        allw = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allw, mine)
+        ns = torch.tensor([n_k], dtype=torch.float64, device=dev)
+        alln = [torch.empty_like(ns) for _ in range(world)]
+        dist.all_gather(alln, ns)
+        nn = torch.cat(alln)
+        ref = sum(w.double() * float(n) for w, n in zip(allw, nn)) / float(nn.sum())
+        agg.average(n_k)
+        fedavg_err = float((eng.flat.double() - ref).abs().max())
+        spread = torch.tensor([float(eng.flat.double().sum())], dtype=torch.float64, device=dev)
+        lo, hi = spread.clone(), spread.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        fedavg_err = max(fedavg_err, float(hi - lo) / max(1.0, abs(float(hi))))
     round_s = dt / args.steps
     imgs_per_round = world * args.epochs * args.local_steps * args.batch
     value = imgs_per_round / round_s
@@ -159,11 +196,14 @@ def main() -> int:
                "eval_batch": ev.B if val_steps else None,
                "peak_hbm_gb_per_client": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
+               "dist_backend": (dist.get_backend() if world > 1 else None),
+               **({"fedavg_max_abs_err": fedavg_err} if fedavg_err is not None else {}),
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",
                           "img_size": args.img, "global_batch": args.batch * world, "per_client_batch": args.batch,
                           "seq_len": None, "epochs_per_round": args.epochs,
                           "local_steps_per_round": args.epochs * args.local_steps,
-                          "parallelism": f"fedavg-dp{world} (1 FL client per GPU, RCCL weighted all-reduce)",
+                          "parallelism": f"fedavg-dp{world} (1 FL client per GPU, weighted all-reduce over "
+                                         f"{'RCCL' if world == 1 or dist.get_backend() == 'nccl' else dist.get_backend()})",
                           "graph": use_graph, "memplan": plan.as_dict() if plan else None}}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -61,13 +61,32 @@ def hip_path() -> str:
     return os.path.join(PKG, "_C" + EXT)
 
 
-def build_native(force: bool = False, verbose: bool = True) -> str:
+def _native_inputs():
     srcs = sorted(glob.glob(os.path.join(CSRC, "native", "*.cpp")))
     flags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-Wno-unused-variable"] + _pybind_includes()
+    import pybind11
+    portable = [f for f in flags if not f.startswith("-I")] + [pybind11.__version__, sys.version.split()[0]]
+    return srcs, flags, _hash(srcs, portable)
+
+
+def is_current(path: str, key: str) -> bool:
+    """The built module exists and its stamp matches the hash of the sources/flags it must be built from."""
+    stamp = path + ".stamp"
+    if not (os.path.exists(path) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read() == key
+
+
+def native_key() -> str:
+    return _native_inputs()[2]
+
+
+def build_native(force: bool = False, verbose: bool = True) -> str:
+    srcs, flags, key = _native_inputs()
     out = native_path()
     stamp = out + ".stamp"
-    key = _hash(srcs, flags)
-    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+    if not force and is_current(out, key):
         return out
     os.makedirs(os.path.join(BUILD, "native"), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
@@ -100,17 +119,30 @@ def _torch_flags():
     return inc, libs, abi
 
 
-def build_hip(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
+def _hip_inputs():
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     headers = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "*.h")))
     binding = os.path.join(CSRC, "bindings.cpp")
     inc, libs, abi = _torch_flags()
     base = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{CSRC}", f"-I{CSRC}/kernels",
             "-Wno-unused-result", "-Wno-unused-command-line-argument", "-ffp-contract=fast"]
+    import torch
+    # the key must not depend on where the tree or torch live (the snapshot runs from another path on the GPU
+    # box): source bytes + path-free flags + torch version + arch
+    portable = [f for f in base if not f.startswith("-I")] + [torch.__version__, ARCH, str(abi)]
+    key = _hash(kern + headers + [binding], portable)
+    return kern, headers, binding, inc, libs, abi, base, key
+
+
+def hip_key() -> str:
+    return _hip_inputs()[-1]
+
+
+def build_hip(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
+    kern, headers, binding, inc, libs, abi, base, key = _hip_inputs()
     out = hip_path()
     stamp = out + ".stamp"
-    key = _hash(kern + headers + [binding], base + inc)
-    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+    if not force and is_current(out, key):
         return out
     if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")

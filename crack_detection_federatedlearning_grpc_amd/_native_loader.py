@@ -21,8 +21,8 @@ def native():
         with _lock:
             if _native is None:
                 from . import _build
-                if not os.path.exists(_build.native_path()):
-                    _build.build_native(verbose=False)
+                if not _build.is_current(_build.native_path(), _build.native_key()):
+                    _build.build_native(verbose=False)      # missing or stale (stamp != source hash)
                 _native = importlib.import_module(__package__ + "._native")
     return _native
 
@@ -33,9 +33,13 @@ def hip():
         with _lock:
             if _hip is None:
                 from . import _build
-                if not os.path.exists(_build.hip_path()):
+                if not _build.is_current(_build.hip_path(), _build.hip_key()):
+                    # missing, or built from other sources than these (its stamp != the source hash): never
+                    # import a stale kernel module silently
+                    state = "stale" if os.path.exists(_build.hip_path()) else "not built"
                     if os.environ.get("CFL_NO_JIT_BUILD"):
-                        raise RuntimeError("HIP extension _C is not built (run __graft_entry__.build())")
+                        raise RuntimeError(f"HIP extension _C is {state} (run __graft_entry__.build())")
+                    print(f"[native] HIP extension _C is {state}; rebuilding", flush=True)
                     _build.build_hip(verbose=True)
                 import torch  # noqa: F401  (libtorch must be loaded before _C)
                 _hip = importlib.import_module(__package__ + "._C")

@@ -50,7 +50,9 @@ class FLConfig:
     data_plane: str = "grpc"             # grpc | rccl
     rccl_timeout_s: float = 300.0        # collective timeout; on expiry / peer loss the client aborts the
                                          # communicator and falls back to the gRPC data plane
-    codec: str = "flat"                  # flat (safe, default) | pickle (reference wire format)
+    codec: str = "flat"                  # client upload / advertised reply format: flat (safe) | pickle (reference
+                                         # wire format). The server answers each client in the format it
+                                         # advertised, pickle for a reference client that advertises none
     wire_dtype: str = "fp32"             # fp32 | bf16 for the flat codec
 
     # --- local training ------------------------------------------------------------------------

@@ -77,13 +77,20 @@ class FLClient:
                 time.sleep(delay)
                 delay = min(delay * 2, 10.0)
 
+    def _codec_cfg(self) -> Dict[str, "P.Scalar"]:
+        """The reply format this client decodes, advertised to the server (a reference client sends none and
+        gets pickles)."""
+        return {"codec": P.Scalar(scstring=self.cfg.codec), "wire_dtype": P.Scalar(scstring=self.cfg.wire_dtype)}
+
     def _ready(self, stub):
         req = P.transportRequest(ready_req=P.ReadyReq(type="R", cname=self.name, state=P.ON,
-                                                     config={"current_round": P.Scalar(scint32=0)}))
+                                                     config={"current_round": P.Scalar(scint32=0),
+                                                             **self._codec_cfg()}))
         return self._call(stub, req).ready_rep.config
 
     def _params(self, stub) -> bytes:
-        return self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="P"))).update_rep.buffer_chunk
+        return self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="P", cname=self.name))
+                          ).update_rep.buffer_chunk
 
     def _log_phase(self, phase: Dict) -> None:
         """Per-round phase wall-clock (aggregate = RCCL all-reduce in rccl mode, upload = TRAIN_DONE RPC incl. the
@@ -106,7 +113,8 @@ class FLClient:
     def _version(self, stub, mv: int, cr: int, wait_s: float):
         req = P.transportRequest(version_req=P.VersionReq(type="P", config={
             "model_version": P.Scalar(scint32=mv), "current_round": P.Scalar(scint32=cr),
-            "wait_s": P.Scalar(scfloat=float(wait_s))}))
+            "wait_s": P.Scalar(scfloat=float(wait_s)), "cname": P.Scalar(scstring=self.name),
+            **self._codec_cfg()}))
         return self._call(stub, req).version_rep
 
     def send_logs(self, stub, root: Optional[str] = None) -> int:
@@ -145,24 +153,30 @@ class FLClient:
             codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
 
     def _payload(self) -> bytes:
-        arrays = self.trainer.get_weights()
         n = getattr(self.trainer, "n_samples", 0)
+        arrays = None
         if self.aggregator is not None:
             try:
-                avg = self.aggregator.average(arrays, n)         # weighted all-reduce over RCCL
+                dev = getattr(self.trainer, "fedavg_device", None)
+                if dev is not None and dev(self.aggregator, n):
+                    pass                                         # averaged in place on the GPU (no host staging)
+                else:
+                    arrays = self.aggregator.average(self.trainer.get_weights(), n)   # host-array trainers
+                    self.trainer.set_weights(arrays)             # local model <- global average
             except Exception as e:                               # peer lost / collective timed out
                 print(f"[{self.name}] RCCL aggregation failed ({type(e).__name__}: {e}); aborting the "
                       f"communicator, falling back to the gRPC data plane")
                 self.aggregator.abort()
                 self.aggregator = None
                 self.fallbacks += 1
+                arrays = None
             else:
-                self.trainer.set_weights(avg)                    # local model <- global average
                 if self.aggregator.rank != 0:
-                    return b""
-                arrays = avg
+                    return b""                                   # rank 0 alone uploads the server's copy
         if self.cfg.fault_corrupt:
             return b"\x80corrupt" + os.urandom(64)
+        if arrays is None:
+            arrays = self.trainer.get_weights()                  # (rank 0: the D2H waits for the last bucket)
         return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype)
 
     def _apply(self, blob: bytes) -> None:

@@ -10,6 +10,12 @@ Reference: fl_server.py. Same single bidi-stream RPC and verbs (dispatcher fl_se
 Extra READY reply keys (ignored by reference clients): ``rank``, ``world_size``, ``dist_addr``, ``dist_port``,
 ``data_plane`` - the server doubles as the RCCL rendezvous for on-node GPU clients.
 ``UpdateReq.file_len`` on a 'D' request carries the client's sample count n_k for weighted FedAvg.
+
+Reply codec per client (drop-in compatibility): a reference client ``pickle.loads`` whatever arrives in
+``buffer_chunk`` (client_fit_model.py:51,231) and never says what it can read, so parameters go out as the
+reference pickle unless the client advertised the flat codec - a ``codec`` (+ ``wire_dtype``) key in its READY
+config, or in the VERSION config / a ``cname`` on the PARAM request that identifies a client that did. A client
+whose TRAIN_DONE payload was a pickle is answered in pickle from then on.
 """
 from __future__ import annotations
 
@@ -50,21 +56,26 @@ class FLServer(TransportServiceServicer):
                  evaluator: Optional[Callable[[np.ndarray], Dict[str, float]]] = None):
         self.cfg = cfg
         self.table = table or ParamTable()
-        start_round, version = 0, cfg.initial_model_version
+        start_round, version, snap = 0, cfg.initial_model_version, None
         if global_flat is None:
             global_flat = self.table.init_flat(cfg.seed)
         if cfg.resume and cfg.snapshot_dir:
             snap = load_snapshot(cfg.snapshot_dir, self.table)
+            finished = False
             if snap is not None:
-                global_flat, start_round, version = snap
-                print(f"[fl_server] resumed from snapshot: round {start_round}, version {version}")
+                global_flat, start_round, version, finished = snap
+                print(f"[fl_server] resumed from snapshot: round {start_round}, version {version}"
+                      + (" (run already finished: every client gets FIN)" if finished else ""))
         self.evaluator = evaluator
         self.state = RoundState(global_flat, max_rounds=cfg.max_rounds, register_window_s=cfg.register_window_s,
                                 num_clients=cfg.num_clients, initial_version=version,
                                 weighted=(cfg.aggregation == "weighted"), round_deadline_s=cfg.round_deadline_s,
                                 quorum=cfg.quorum, start_round=start_round, on_aggregate=self._on_aggregate)
+        if cfg.resume and cfg.snapshot_dir and snap is not None and finished and start_round > cfg.max_rounds:
+            self.state.finished = True       # a completed run stays completed (a larger max_rounds extends it)
         self._blob_lock = threading.Lock()
-        self._blob_cache: Dict[int, bytes] = {}
+        self._blob_cache: Dict[tuple, bytes] = {}
+        self._codec: Dict[str, tuple] = {}          # client name -> (codec, wire_dtype) it can decode
         self.server: Optional[grpc.Server] = None
         self.port: Optional[int] = None
         self.dist_port = 0
@@ -72,16 +83,34 @@ class FLServer(TransportServiceServicer):
         self.log_root = os.path.abspath(os.path.join(cfg.work_dir, "."))
 
     # -- parameters --------------------------------------------------------------------------------
-    def send_parameter(self) -> bytes:
-        """fl_server.py:23-24 (``eval_model.get_weights(made_model)``) - here the current global average."""
+    def send_parameter(self, fmt: tuple = ("pickle", "fp32")) -> bytes:
+        """fl_server.py:23-24 (``eval_model.get_weights(made_model)``) - here the current global average, encoded
+        in the format the requesting client reads (``fmt`` = (codec, wire_dtype); reference pickle by default)."""
         with self.state.cv:
             v, flat = self.state.model_version, self.state.global_flat
+        key = (v,) + tuple(fmt)
         with self._blob_lock:
-            blob = self._blob_cache.get(v)
+            blob = self._blob_cache.get(key)
             if blob is None:
-                blob = codec.encode(self.table.to_list(flat), self.cfg.codec, wire_dtype=self.cfg.wire_dtype)
-                self._blob_cache = {v: blob}
+                blob = codec.encode(self.table.to_list(flat), fmt[0], wire_dtype=fmt[1])
+                self._blob_cache = {k: b for k, b in self._blob_cache.items() if k[0] == v}
+                self._blob_cache[key] = blob
             return blob
+
+    @staticmethod
+    def _advertised(config) -> Optional[tuple]:
+        if "codec" not in config or config["codec"].scstring not in ("flat", "pickle"):
+            return None
+        dt = config["wire_dtype"].scstring if "wire_dtype" in config else "fp32"
+        return config["codec"].scstring, dt if dt in ("fp32", "bf16") else "fp32"
+
+    def client_format(self, name: str = "", config=None) -> tuple:
+        """The reply codec of a request: advertised in this request's config, else what the named client
+        advertised at READY / last uploaded, else the reference pickle."""
+        adv = self._advertised(config) if config is not None else None
+        if adv is not None:
+            return adv
+        return self._codec.get(name, ("pickle", "fp32"))
 
     def global_weights(self):
         with self.state.cv:
@@ -112,7 +141,8 @@ class FLServer(TransportServiceServicer):
             if req.ready_req.type == "R":
                 yield self._ready(req.ready_req)
             elif req.update_req.type == "P":
-                yield P.transportResponse(update_rep=P.UpdateRep(type="P", buffer_chunk=self.send_parameter(),
+                fmt = self.client_format(req.update_req.cname)
+                yield P.transportResponse(update_rep=P.UpdateRep(type="P", buffer_chunk=self.send_parameter(fmt),
                                                                 title="parameters"))
             elif req.update_req.type == "T":
                 self.state.heartbeat(req.update_req.cname)
@@ -133,6 +163,7 @@ class FLServer(TransportServiceServicer):
             time.sleep(self.cfg.ready_stall_s)      # fl_server.py:56 (kept for compat; presets set 0)
         conf = self.state.ready(r.cname, client_round)
         if conf["state"] == SW:
+            self._codec[r.cname] = self._advertised(r.config) or ("pickle", "fp32")
             print(f"### Check Train Round ### {r.cname} registered as rank {conf['rank']}")
             conf["model_type"] = self.cfg.model_type
             conf["data_plane"] = self.cfg.data_plane
@@ -149,18 +180,20 @@ class FLServer(TransportServiceServicer):
         if u.buffer_chunk:
             try:
                 arrays, hdr = codec.decode(u.buffer_chunk)
+                if u.buffer_chunk[:4] != codec.MAGIC:      # a pickle sender reads pickle replies
+                    self._codec[u.cname] = ("pickle", "fp32")
                 flat = self.table.from_list(arrays)
-                n = float(hdr.get("n_samples") or n or 1.0)
+                n = float(hdr.get("n_samples") or n or 0.0)   # 0: not reported (reference client)
             except Exception as e:
                 print(f"[fl_server] rejected payload from {u.cname}: {e}")
                 context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad weight payload: {e}")
         try:
-            state, conf = self.state.submit(u.cname, u.current_round, flat, max(n, 1.0))
+            state, conf = self.state.submit(u.cname, u.current_round, flat, max(n, 0.0))
         except ValueError as e:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         conf = dict(conf, state=state)
         print(f"### Current state: {state} ###")
-        chunk = self.send_parameter() if state == RESP_ARY else b""
+        chunk = self.send_parameter(self.client_format(u.cname)) if state == RESP_ARY else b""
         return P.transportResponse(update_rep=P.UpdateRep(type="D", buffer_chunk=chunk, config=_cfg(conf)))
 
     def _version(self, v):
@@ -169,7 +202,8 @@ class FLServer(TransportServiceServicer):
         wait = v.config["wait_s"].scfloat if "wait_s" in v.config else 0.0
         state, conf = self.state.version(mv, cr, min(wait, self.cfg.long_poll_s))
         if state == NOT_WAIT:
-            return P.transportResponse(version_rep=P.VersionRep(state=P.NOT_WAIT, buffer_chunk=self.send_parameter(),
+            fmt = self.client_format(v.config["cname"].scstring if "cname" in v.config else "", v.config)
+            return P.transportResponse(version_rep=P.VersionRep(state=P.NOT_WAIT, buffer_chunk=self.send_parameter(fmt),
                                                                 config=_cfg(conf)))
         if state == FIN:
             return P.transportResponse(version_rep=P.VersionRep(state=P.FIN, config=_cfg(conf)))
@@ -246,4 +280,4 @@ def load_snapshot(d: str, table: ParamTable):
     with open(sp) as f:
         st = json.load(f)
     flat = load_weights_h5(os.path.join(d, "global.h5"), table)
-    return flat, int(st["current_round"]), int(st["model_version"])
+    return flat, int(st["current_round"]), int(st["model_version"]), bool(st.get("finished", False))

@@ -9,7 +9,10 @@ SURVEY §5.2 / §A8). Here all state lives in one ``RoundState`` guarded by a ``
   real reply (fixes §A2)
 * version check (``version``)   fl_server.py:138-149 WAIT / NOT_WAIT / FIN, plus an optional server-side long-poll
   so a waiting client is released as soon as the round completes instead of on a 20 s sleep boundary
-* liveness: optional per-round deadline with a quorum fraction - survivors are re-weighted (§5.3, fixes §A9)
+* liveness: optional per-round deadline with a quorum fraction - survivors are re-weighted (§5.3, fixes §A9).
+  Clients dropped at a deadline leave the LIVE set, so later rounds close as soon as every live client reported
+  (a dead client is not waited for again, and the quorum is a fraction of the live clients); a dropped client
+  that speaks again (READY, TRAINING or TRAIN_DONE) rejoins it
 """
 from __future__ import annotations
 
@@ -57,6 +60,7 @@ class RoundState:
         self.on_aggregate = on_aggregate
         self.clock = clock
         self.registered: List[str] = []
+        self.live: set = set()                    # registered clients not dropped at a deadline
         self.window_started: Optional[float] = None
         self.window_closed = False
         self.updates: Dict[str, Tuple[np.ndarray, float]] = {}
@@ -84,6 +88,8 @@ class RoundState:
 
     def ready(self, name: str, client_round: int) -> Dict[str, object]:
         with self.cv:
+            if self.finished:                      # e.g. resumed from the snapshot of a finished run
+                return dict(self._cfg_locked(), state=FIN)
             if self.window_started is None:
                 self.window_started = self.clock()
                 self._start_monitor()
@@ -91,7 +97,7 @@ class RoundState:
                 return {"state": CTW}
             if name not in self.registered:
                 self.registered.append(name)
-            self.heartbeats[name] = self.clock()
+            self._touch_locked(name)
             if self.num_clients and len(self.registered) >= self.num_clients:
                 self._close_window_locked()
             if self.current_round == 0 and client_round == 0:
@@ -110,13 +116,20 @@ class RoundState:
                 self.cv.wait(timeout=min(0.05, rem) if rem is not None else 0.05)
             return len(self.registered)
 
+    def _touch_locked(self, name: str) -> None:
+        self.heartbeats[name] = self.clock()
+        if name in self.registered and name not in self.live:
+            if self.history:
+                print(f"[fl_server] {name} is back; expected again from round {self.current_round}")
+            self.live.add(name)
+
     def heartbeat(self, name: str) -> None:
         with self.cv:
-            self.heartbeats[name] = self.clock()
+            self._touch_locked(name)
 
     # -- round accounting ---------------------------------------------------------------------------
     def _expected_locked(self) -> int:
-        return len(self.registered)
+        return len(self.live)
 
     def submit(self, name: str, client_round: int, flat: Optional[np.ndarray], n_samples: float
                ) -> Tuple[str, Dict[str, object]]:
@@ -125,7 +138,7 @@ class RoundState:
                 return FIN, self._cfg_locked()
             if name not in self.registered:
                 return CTW, self._cfg_locked()
-            self.heartbeats[name] = self.clock()
+            self._touch_locked(name)
             if client_round != self.current_round:
                 return RESP_ACY, self._cfg_locked()   # stale: client polls VERSION and picks up new params
             if flat is not None:
@@ -140,9 +153,11 @@ class RoundState:
     def _aggregate_locked(self, dropped: List[str]) -> Tuple[str, Dict[str, object]]:
         ups = [(f, n) for f, n in self.updates.values() if f is not None]
         if ups:
-            self.global_flat = fedavg_flat(ups, self.weighted)
+            # a reference client reports no sample count (n = 0): that round is the reference's plain mean
+            self.global_flat = fedavg_flat(ups, self.weighted and all(n > 0 for _, n in ups))
         rec = RoundRecord(self.current_round, list(self.updates), [n for _, n in self.updates.values()],
                           self.round_started or self.clock(), self.clock(), dropped)
+        self.live.difference_update(dropped)
         self.history.append(rec)
         self.updates = {}
         done = self.current_round >= self.max_rounds
@@ -195,11 +210,11 @@ class RoundState:
                     self._aggregate_locked([])   # window closed after every registered client had reported
                 elif self.deadline_s > 0 and self.round_started is not None and \
                         self.clock() - self.round_started >= self.deadline_s and self.updates:
-                    need = max(1, math.ceil(self.quorum * len(self.registered)))
+                    need = max(1, math.ceil(self.quorum * len(self.live)))
                     if len(self.updates) >= need:
-                        dropped = [c for c in self.registered if c not in self.updates]
+                        dropped = [c for c in self.live if c not in self.updates]
                         print(f"[fl_server] round {self.current_round} deadline: aggregating "
-                              f"{len(self.updates)}/{len(self.registered)}, dropped {dropped}")
+                              f"{len(self.updates)}/{len(self.live)} live clients, dropped {dropped}")
                         self._aggregate_locked(dropped)
             self._stop.wait(0.05)
 

@@ -126,6 +126,9 @@ class UNetEngine:
         t = self._bucket_packs[key]
         if t is not None:
             self.C.pack_weights(self.flat, self.packed, t[0], t[1], t[2])
+        if self.fp8 and sl.stop >= self.table.total:     # last bucket: the fp8 ConvT copies of the new average
+            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
+                            None, self.n_views8)
 
     def G(self, layer: str, w: str) -> torch.Tensor:
         e = self.table.entry(layer, w)
@@ -572,7 +575,7 @@ class UNetEngine:
             self.ws = torch.empty(need * B * Ho * Ho * N, dtype=torch.float32, device=self.dev)
         off8, n8, soff, cout, i = self.p8_at[layer]
         if self._pending:
-            self.P(layer, "kernel")                           # wait for this layer's FedAvg bucket
+            self._await_all()                # the fp8 copies are repacked after the LAST FedAvg bucket
         self.C.conv3x3_fp8(x.t, self.packed8[off8:off8 + n8], self.scales8[soff:soff + cout], self.amax8[i],
                            bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho, N,
                            self.ws if need > 1 else None)
@@ -622,10 +625,13 @@ class UNetEngine:
         self.graph = g
 
     def train_step(self, use_graph: bool = True) -> None:
-        if use_graph:
-            if self.graph is None:
-                self.capture()
-            self._await_all()
+        """One training iteration. The first step after an overlapped FedAvg (``defer_until``) runs eagerly so
+        each layer waits only for the bucket holding its parameters (the early layers' kernels start while the
+        late buckets are still reducing); every other step replays the captured hipGraph."""
+        if use_graph and self.graph is not None and not self._pending:
+            self.graph.replay()
+        elif use_graph and self.graph is None:
+            self.capture()
             self.graph.replay()
         else:
             self.train_step_eager()

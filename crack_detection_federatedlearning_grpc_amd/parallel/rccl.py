@@ -38,20 +38,26 @@ class FedAvgAllReduce:
         self.group = group
         self.world = world or dist.get_world_size(group)
         self.buckets = _buckets(flat.numel(), max(1024, int(bucket_mb * (1 << 20)) // 4))
-        self._total_n: Optional[float] = None
-        self._last_n: Optional[float] = None
         self._side = None
 
+    def _weight(self, n_local: float, weighted: bool):
+        """This client's FedAvg weight n_k / sum n. The sample-count all-reduce runs on EVERY call (each rank
+        must issue the same sequence of collectives; a per-rank cache could desynchronise them) and stays on the
+        device (no host sync): the weight is a 1-element tensor the bucket scaling broadcasts."""
+        if not weighted:
+            return 1.0 / float(self.world)
+        t = torch.tensor([float(n_local)], dtype=torch.float32, device=self.flat.device)
+        tot = t.clone()
+        dist.all_reduce(tot, group=self.group)
+        return t / tot.clamp_min(1e-12)
+
     def total_samples(self, n_local: float) -> float:
-        if self._total_n is None or self._last_n != n_local:
-            t = torch.tensor([float(n_local)], dtype=torch.float64, device=self.flat.device)
-            dist.all_reduce(t, group=self.group)
-            self._total_n, self._last_n = float(t.item()), n_local
-        return self._total_n
+        t = torch.tensor([float(n_local)], dtype=torch.float64, device=self.flat.device)
+        dist.all_reduce(t, group=self.group)
+        return float(t.item())
 
     def average(self, n_local: float, weighted: bool = True) -> None:
-        tot = self.total_samples(n_local) if weighted else float(self.world)
-        w = (float(n_local) if weighted else 1.0) / max(tot, 1e-12)
+        w = self._weight(n_local, weighted)
         works = []
         for sl in self.buckets:
             b = self.flat[sl]
@@ -73,8 +79,7 @@ class FedAvgAllReduce:
                 for sl in self.buckets:
                     on_bucket(sl)
             return []
-        tot = self.total_samples(n_local) if weighted else float(self.world)
-        w = (float(n_local) if weighted else 1.0) / max(tot, 1e-12)
+        w = self._weight(n_local, weighted)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.flat.device)
         out = []
@@ -108,6 +113,9 @@ class RcclAggregator:
                                     world_size=world, timeout=timedelta(seconds=timeout_s),
                                     **({"device_id": device} if cuda else {}))
         self.device = device if cuda else torch.device("cpu")
+        self._cached = None
+        print(f"[rccl] rank {rank}/{world} backend {dist.get_backend()} device "
+              f"{self.device if not cuda else torch.cuda.get_device_name(device)} ({self.device})", flush=True)
 
     @classmethod
     def from_ready_info(cls, info: Dict, cfg=None) -> "RcclAggregator":
@@ -117,7 +125,14 @@ class RcclAggregator:
         return cls(int(info.get("rank", 0)), int(info["world_size"]), str(info.get("dist_addr") or "127.0.0.1"),
                    int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)))
 
+    def _reducer(self, flat: torch.Tensor) -> FedAvgAllReduce:
+        key = (flat.data_ptr(), flat.numel())
+        if self._cached is None or self._cached[0] != key:
+            self._cached = (key, FedAvgAllReduce(flat, world=self.world))
+        return self._cached[1]
+
     def average(self, arrays: Sequence[np.ndarray], n_local: float) -> List[np.ndarray]:
+        """Host-array form (trainers without a device buffer, e.g. the CPU oracle over gloo)."""
         shapes = [np.shape(a) for a in arrays]
         flat = torch.as_tensor(np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in arrays])).to(self.device)
         FedAvgAllReduce(flat, world=self.world).average(float(max(n_local, 1)))
@@ -128,6 +143,12 @@ class RcclAggregator:
             out.append(host[off:off + n].reshape(s).copy())
             off += n
         return out
+
+    def average_device(self, flat: torch.Tensor, n_local: float,
+                       on_bucket: Optional[Callable[[slice], None]] = None) -> List[Tuple[slice, object]]:
+        """Device-resident FedAvg of a trainer's flat fp32 parameter buffer, in place: bucketed weighted
+        all-reduce on a side stream (no host staging); returns the per-bucket events for ``defer_until``."""
+        return self._reducer(flat).average_async(float(max(n_local, 1)), on_bucket=on_bucket)
 
     def abort(self) -> None:
         """A peer died or a collective timed out: tear the communicator down without a collective shutdown

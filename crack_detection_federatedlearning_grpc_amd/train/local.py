@@ -127,6 +127,16 @@ class LocalFit:
     def get_weights(self) -> List[np.ndarray]:
         return self.table.to_list(self.backend.get_flat())
 
+    def fedavg_device(self, aggregator, n_local: float) -> bool:
+        """Device-resident FedAvg (RCCL data plane): reduce the engine's flat fp32 parameter buffer in place,
+        bucketed on a side stream with each bucket's layers repacked to bf16 there; the next round's first step
+        waits per layer (``UNetEngine.defer_until``). False when the backend holds no device buffer."""
+        eng = getattr(self.backend, "eng", None)
+        if eng is None or eng.flat.device.type != "cuda" or not hasattr(aggregator, "average_device"):
+            return False
+        eng.defer_until(aggregator.average_device(eng.flat, n_local, on_bucket=eng.pack_bucket))
+        return True
+
     def _log(self, rec: Dict) -> None:
         line = json.dumps(rec)
         print(line)

@@ -26,8 +26,8 @@ class TransportService(FLServer):
 
 
 def send_parameter() -> bytes:
-    """fl_server.py:23-24."""
-    return SERVER.send_parameter()
+    """fl_server.py:23-24 (the reference pickle a reference client unpickles)."""
+    return SERVER.send_parameter(("pickle", "fp32"))
 
 
 def ready_client(name, config):
@@ -65,7 +65,7 @@ def serve(cfg=None) -> FLServer:
     SERVER = FLServer(cfg, evaluator=evaluator)
     port = SERVER.start()
     print(f"[fl_server] listening on {cfg.bind}:{port} ({cfg.max_rounds} rounds, window {cfg.register_window_s}s, "
-          f"data plane {cfg.data_plane}, codec {cfg.codec})")
+          f"data plane {cfg.data_plane}, replies in each client's advertised codec, pickle by default)")
     SERVER.serve_forever(exit_on_fin=True)
     return SERVER
 

@@ -28,20 +28,32 @@ class evaluate_LocalModel:
         return self.table.init_flat(self.cfg.seed)
 
     def get_weights(self, model: np.ndarray) -> bytes:
-        return codec.encode(self.table.to_list(model), self.cfg.codec)
+        """Bytes for ``buffer_chunk``: the reference client ``pickle.loads`` them (client_fit_model.py:51)."""
+        return codec.encode(self.table.to_list(model), "pickle")
 
-    def train_model_tosave(self, model: np.ndarray) -> Dict[str, float]:
-        """fl_server.py:31 expects {'loss','accuracy'} of the global model."""
+    def train_model_tosave(self, model: np.ndarray, max_batches: int = 0) -> Dict[str, float]:
+        """fl_server.py:31 expects {'loss','accuracy'} of the global model.
+
+        With a visible GPU the global model is evaluated by the MI355X engine at the clients' resolution
+        (``cfg.img_size``) over the held-out split of a synthetic shard (inference-mode BN, the same validation
+        path the clients run); on a CPU-only server the fp32 oracle evaluates a small (<= 64^2) shard."""
         if self._eval is None:
             import dataclasses
-            from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer
-            cfg = dataclasses.replace(self.cfg, device="cpu", synthetic_samples=max(2 * self.bs, 32),
-                                      val_samples=self.bs, img_size=min(self.cfg.img_size, 64))
-            self._eval = make_trainer(cfg, "server-eval", table=self.table)
+            from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer, resolve_device
+            dev = resolve_device(self.cfg)
+            if dev == "cuda":
+                n_val = max(self.bs, min(self.cfg.val_samples, 8 * self.bs) // self.bs * self.bs)
+                cfg = dataclasses.replace(self.cfg, device="cuda", synthetic_samples=2 * n_val, val_samples=n_val,
+                                          batch_size=self.bs)
+            else:
+                cfg = dataclasses.replace(self.cfg, device="cpu", synthetic_samples=max(2 * self.bs, 32),
+                                          val_samples=self.bs, img_size=min(self.cfg.img_size, 64),
+                                          batch_size=self.bs)
+            self._eval = make_trainer(cfg, "server-eval", table=self.table, device=dev)
         self._eval.backend.set_flat(model)
         from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
         vb = epoch_batches(self._eval.data.val_idx, self.bs, 0, 0)
-        return self._eval.backend.eval_batches(vb[:1])
+        return self._eval.backend.eval_batches(vb[:max_batches] if max_batches else vb)
 
     def saved_model(self, model: np.ndarray, path: str = "global_model.h5") -> str:
         save_keras_h5(path, self.table, model, self.img)

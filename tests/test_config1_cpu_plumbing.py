@@ -39,3 +39,11 @@ def test_two_cpu_clients_real_training(tmp_path, table):
                             work_dir=str(tmp_path))
     srv2 = FLServer(cfg2, table=table)
     assert srv2.state.current_round == 3 and np.allclose(srv2.state.global_flat, srv.state.global_flat)
+    # resuming the snapshot of a FINISHED run under the same max_rounds: READY / VERSION answer FIN, no extra round
+    cfg3 = config.from_args(None, preset="cpu-plumbing", snapshot_dir=str(tmp_path / "snap"), resume=True,
+                            work_dir=str(tmp_path), max_rounds=2)
+    srv3 = FLServer(cfg3, table=table)
+    assert srv3.state.finished
+    assert srv3.state.ready("late", 0)["state"] == "FIN"
+    assert srv3.state.version(srv3.state.model_version, 3)[0] == "FIN"
+    assert not srv2.state.finished            # max_rounds 5 > 2 finished rounds: the run continues

@@ -95,3 +95,120 @@ def test_straggler_dropped_at_deadline(tmp_path, table):
     srv.stop()
     assert res == {"good": "FIN", "bad": "crashed"}
     assert any(r.dropped == ["bad"] for r in srv.state.history)
+
+
+def test_dropped_client_not_waited_for_again(table):
+    """A client dropped at a deadline leaves the live set: later rounds close as soon as the live clients report
+    (no second deadline wait), the quorum is a fraction of the live clients, and the client rejoins when it
+    speaks again."""
+    from crack_detection_federatedlearning_grpc_amd.fl.state import RESP_ACY, RESP_ARY, RoundState
+    st_ = RoundState(np.zeros(table.total, np.float32), max_rounds=5, register_window_s=0.2, num_clients=3,
+                     round_deadline_s=0.5, quorum=0.5)
+    for n in "abc":
+        st_.ready(n, 0)
+    one = np.ones(table.total, np.float32)
+    for n in "ab":
+        assert st_.submit(n, 1, one, 1.0)[0] == RESP_ACY
+    assert st_.submit("c", 1, one, 1.0)[0] == RESP_ARY                # round 1: everyone
+    assert st_.submit("a", 2, one, 1.0)[0] == RESP_ACY
+    assert st_.submit("b", 2, one, 1.0)[0] == RESP_ACY                # c is silent: deadline drops it
+    import time
+    t0 = time.monotonic()
+    while st_.current_round == 2 and time.monotonic() - t0 < 5:
+        time.sleep(0.02)
+    assert st_.history[1].dropped == ["c"] and st_.live == {"a", "b"}
+    assert st_.submit("a", 3, one, 1.0)[0] == RESP_ACY
+    t1 = time.monotonic()
+    assert st_.submit("b", 3, one, 1.0)[0] == RESP_ARY                # closes at once: c is not expected
+    assert time.monotonic() - t1 < 0.2 and st_.history[2].dropped == []
+    assert st_.submit("c", 2, one, 1.0)[0] == RESP_ACY                # c speaks again (stale round) -> live
+    assert st_.live == {"a", "b", "c"}
+    for n in "ab":
+        assert st_.submit(n, 4, one, 1.0)[0] == RESP_ACY              # round 4 waits for c again
+    assert st_.submit("c", 4, one, 1.0)[0] == RESP_ARY
+    assert sorted(st_.history[3].clients) == ["a", "b", "c"]
+    st_.stop()
+
+
+def test_reference_pickle_client_against_default_server(tmp_path, table):
+    """Drop-in wire compatibility: the reference client's exact verb sequence (fl_client.py:77-175) - READY
+    without a codec key, PARAM without a name, raw ``pickle.dumps(list[np.ndarray])`` uploads - against the
+    DEFAULT server config gets pickles it can ``pickle.loads`` (client_fit_model.py:51,231) on every reply path
+    (PARAM, RESP_ARY, NOT_WAIT), while a flat-advertising client on the same server gets flat payloads."""
+    import pickle
+    import grpc
+    from crack_detection_federatedlearning_grpc_amd.fl import codec
+    from crack_detection_federatedlearning_grpc_amd.fl import proto as P
+    from crack_detection_federatedlearning_grpc_amd.fl.rpc import TransportServiceStub, channel_options
+    cfg = _cfg(tmp_path, max_rounds=2)                                   # default codec config
+    srv = FLServer(cfg, global_flat=np.zeros(table.total, np.float32), table=table)
+    port = srv.start(0)
+    got = {}
+
+    def one(stub, req):
+        return list(stub.transport(iter([req]), timeout=30))[-1]
+
+    def reference_client():
+        with grpc.insecure_channel(f"127.0.0.1:{port}", options=channel_options(512)) as ch:
+            stub = TransportServiceStub(ch)
+            rep = one(stub, P.transportRequest(ready_req=P.ReadyReq(
+                type="R", cname="client42", state=P.ON, config={"current_round": P.Scalar(scint32=0)})))
+            conf = rep.ready_rep.config
+            cr, mv = conf["current_round"].scint32, conf["model_version"].scint32
+            params = pickle.loads(one(stub, P.transportRequest(update_req=P.UpdateReq(type="P"))
+                                      ).update_rep.buffer_chunk)              # fl_client.py:98-103
+            got["p"] = params
+            one(stub, P.transportRequest(update_req=P.UpdateReq(type="T", cname="client42", state=P.TRAINING)))
+            while True:
+                w = [a + 1.0 for a in params]
+                rep = one(stub, P.transportRequest(update_req=P.UpdateReq(
+                    type="D", buffer_chunk=pickle.dumps(w), state=P.TRAIN_DONE, cname="client42",
+                    current_round=cr))).update_rep
+                st = rep.config["state"].scstring
+                if st == "FIN":
+                    return
+                if st == "RESP_ARY":
+                    params = pickle.loads(rep.buffer_chunk)
+                    got.setdefault("ary", []).append(params)
+                    cr, mv = rep.config["current_round"].scint32, rep.config["model_version"].scint32
+                    continue
+                assert st == "RESP_ACY"
+                while True:                                                  # fl_client.py:136-155
+                    vr = one(stub, P.transportRequest(version_req=P.VersionReq(type="P", config={
+                        "model_version": P.Scalar(scint32=mv), "current_round": P.Scalar(scint32=cr)}))
+                             ).version_rep
+                    if vr.state == P.NOT_WAIT:
+                        params = pickle.loads(vr.buffer_chunk)
+                        got.setdefault("nw", []).append(params)
+                        cr, mv = vr.config["current_round"].scint32, vr.config["model_version"].scint32
+                        break
+                    if vr.state == P.FIN:
+                        return
+                    time.sleep(0.05)
+
+    import time
+    flat_trainer = FakeTrainer(table, 3.0)
+    ours = FLClient(dataclasses_replace(cfg, codec="flat"), lambda: flat_trainer, name="ours",
+                    target=f"127.0.0.1:{port}")
+    blobs = []
+    orig = ours._params
+    ours._params = lambda stub: blobs.append(orig(stub)) or blobs[-1]
+    res = {}
+    ts = [threading.Thread(target=reference_client), threading.Thread(target=lambda: res.__setitem__("o", ours.run()))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    srv.stop()
+    assert res["o"] == "FIN"
+    assert len(got["p"]) == len(table.entries) and all(isinstance(a, np.ndarray) for a in got["p"])
+    assert len(got.get("ary", [])) + len(got.get("nw", [])) == 1             # round-2 params reached it as pickle
+    r2 = (got.get("ary") or got.get("nw"))[0]
+    e = table.entries[0]
+    assert np.allclose(r2[0], 0.5 * (1.0 + 3.0)) and r2[0].shape == tuple(e.shape)
+    assert blobs and blobs[0][:4] == codec.MAGIC                             # the flat client got flat
+
+
+def dataclasses_replace(cfg, **kw):
+    import dataclasses
+    return dataclasses.replace(cfg, **kw)

@@ -1,0 +1,98 @@
+"""The FL product path and the multi-rank bench path on a real MI355X (gpu marker; run via gpurun).
+
+* ``test_fl_product_path_on_gpu``: the reference's main loop end to end - an in-process ``FLServer`` (gRPC, the
+  drop-in server of /root/reference/fl_server.py:107-135,152-207) and ONE ``fl_client.py`` process training on the
+  HIP engine (/root/reference/fl_client.py:77-175, client_fit_model.py:152-174), preset gpu1-256, 2 rounds, to FIN.
+* ``test_bench_two_ranks_share_one_gpu``: bench.py's N-rank path (torch.distributed.run, FedAvgAllReduce with the
+  overlapped per-bucket repack) as 2 ranks on cuda:0 over gloo (RCCL refuses two ranks on one device), with the
+  weighted FedAvg checked against an all-gathered reference.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0", CFL_NO_JIT_BUILD="1")
+    env.pop("FL_PRESET", None)
+    return env
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_fl_product_path_on_gpu(tmp_path):
+    from crack_detection_federatedlearning_grpc_amd import config
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.fl import codec
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    common = dict(max_rounds=2, epochs=2, steps_per_epoch=24, synthetic_samples=512, val_samples=448)
+    cfg = config.from_args(None, preset="gpu1-256", work_dir=str(tmp_path), snapshot_dir=str(tmp_path / "snap"),
+                           server_weight_file=str(tmp_path / "server_weights/weights.pickle"), **common)
+    srv = FLServer(cfg, table=table)
+    port = srv.start(0)
+    metrics = tmp_path / "client.jsonl"
+    args = [sys.executable, "-u", os.path.join(ROOT, "fl_client.py"), "--preset", "gpu1-256", "--host", "127.0.0.1",
+            "--port", str(port), "--metrics-file", str(metrics),
+            "--client-weight-file", str(tmp_path / "saved_weight/weights.pickle")]
+    for k, v in common.items():
+        args += ["--" + k.replace("_", "-"), str(v)]
+    try:
+        p = subprocess.run(args, cwd=str(tmp_path), env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           text=True, timeout=240)
+    finally:
+        srv.stop()
+    print(p.stdout[-4000:])
+    assert p.returncode == 0, p.stdout[-4000:]
+    assert [h.round for h in srv.state.history] == [1, 2] and srv.state.finished
+    recs = [json.loads(x) for x in open(metrics)]
+    ep = [r for r in recs if "epoch" in r]
+    assert len(ep) == 4 and all(np.isfinite(r["loss"]) and np.isfinite(r["val_loss"]) for r in ep)
+    assert ep[-1]["loss"] < ep[0]["loss"], [r["loss"] for r in ep]                  # it learns
+    phases = [r for r in recs if r.get("kind") == "phases"]
+    assert [r["round"] for r in phases] == [1, 2] and all(r["payload_bytes"] > 0 for r in phases)
+    # the server's copy == the client's upload (one client: FedAvg is the identity), in every persisted form
+    w_srv = codec.load_weight_file(str(tmp_path / "server_weights/weights.pickle"))
+    w_cli = codec.load_weight_file(str(tmp_path / "saved_weight/weights.pickle"))
+    assert len(w_srv) == len(table.entries) == len(w_cli)
+    assert np.allclose(table.from_list(w_srv), srv.state.global_flat)
+    assert np.allclose(table.from_list(w_cli), srv.state.global_flat)
+    assert (tmp_path / "snap" / "global.h5").exists() and (tmp_path / "snap" / "state.json").exists()
+    assert np.abs(srv.state.global_flat - table.init_flat(cfg.seed)).max() > 1e-3     # weights moved
+
+
+def test_bench_two_ranks_share_one_gpu():
+    port = _free_port()
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+            "--gpus", "2", "--steps", "1", "--warmup", "1", "--epochs", "1", "--local-steps", "6", "--val-steps", "2",
+            "--samples", "256", "--dist-backend", "gloo", "--verify-fedavg"]
+    p = subprocess.run(args, cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=240)
+    print(p.stdout[-4000:])
+    assert p.returncode == 0, p.stdout[-4000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1                                                       # rank 0 alone prints
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["dist_backend"] == "gloo" and out["value"] > 0
+    assert out["config"]["global_batch"] == 32
+    assert out["fedavg_max_abs_err"] < 1e-5, out["fedavg_max_abs_err"]
+    assert p.stdout.count("[bench] rank ") == 2                                 # each rank logged its view
+

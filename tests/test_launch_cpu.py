@@ -16,3 +16,15 @@ def test_launch_two_cpu_clients_rccl_gloo(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "2 round(s)" in r.stdout
     assert (tmp_path / "s.pickle").exists()
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py --gpus N must run as N torch.distributed ranks; a mismatch fails loudly (no silent 1-rank number)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"], cwd=root,
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stdout
