@@ -47,6 +47,10 @@ def main() -> int:
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo: rehearsal of N ranks "
                          "sharing one GPU, which RCCL refuses)")
+    ap.add_argument("--fl", action="store_true",
+                    help="also run the FL product path (FLServer + one FLClient per rank over real gRPC, HIP engine, "
+                         "RCCL data plane for N>1) for warmup+steps rounds and print a SECOND JSON line: wall-clock "
+                         "per round from server release to next release, vs the engine-only round above")
     ap.add_argument("--verify-fedavg", action="store_true",
                     help="after the timed rounds, check one weighted FedAvg against an all-gathered reference")
     args = ap.parse_args()
@@ -206,9 +210,77 @@ def main() -> int:
                                          f"{'RCCL' if world == 1 or dist.get_backend() == 'nccl' else dist.get_backend()})",
                           "graph": use_graph, "memplan": plan.as_dict() if plan else None}}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if args.fl:
+        del eng, ev, data
+        torch.cuda.empty_cache()
+        fl_line = run_fl_bench(args, world, rank, round_s)
+        if rank == 0:
+            print(json.dumps(fl_line), flush=True)
+    if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
     return 0
+
+
+def run_fl_bench(args, world: int, rank: int, engine_round_s: float) -> dict:
+    """The reference's product loop, timed: rank 0 hosts the gRPC FLServer (fl_server.py:107-135,152-207), every
+    rank runs one FLClient (fl_client.py:77-175) whose LocalFit trains on the HIP engine with the bench's config
+    (client_fit_model.py:152-174); for N>1 the clients' FedAvg is the device-resident RCCL all-reduce (the existing
+    process group), rank 0 uploading the average. Per-round wall-clock = the server's RoundRecord span: from the
+    release of the previous global (window close for round 1) to this round's aggregation - distribution, local
+    fit with validation, upload and FedAvg included."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from crack_detection_federatedlearning_grpc_amd import config as C
+    from crack_detection_federatedlearning_grpc_amd.fl.client import FLClient
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer
+    rounds = args.warmup + args.steps
+    split = min(6213, max(args.batch, int(args.samples * 0.7766)))
+    cfg = C.from_args(None, preset="gpu1-256", img_size=args.img, batch_size=args.batch, epochs=args.epochs,
+                      steps_per_epoch=args.local_steps, synthetic_samples=args.samples, val_samples=split,
+                      max_rounds=rounds, num_clients=world, register_window_s=120.0, codec="flat",
+                      data_plane="rccl" if world > 1 else "grpc", client_weight_file="", server_weight_file="",
+                      predict_round=0, use_graph=not args.no_graph, conv_dtype="fp8" if args.fp8 else "bf16",
+                      work_dir="/tmp", data_seed=7)
+    port = torch.zeros(1, dtype=torch.int64, device="cuda")
+    srv = None
+    if rank == 0:
+        srv = FLServer(cfg, table=ParamTable())
+        port.fill_(srv.start(0))
+    if world > 1:
+        dist.all_reduce(port)                                         # server port -> every rank
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1") if world > 1 else "127.0.0.1"
+    agg_factory = None
+    if world > 1:
+        from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+        agg_factory = lambda info: RcclAggregator.from_ready_info(info, cfg)  # noqa: E731 (reuses the group)
+    client = FLClient(cfg, lambda: make_trainer(cfg, f"bench{rank}", rank), name=f"bench{rank}",
+                      target=f"{host}:{int(port.item())}", aggregator_factory=agg_factory)
+    state = client.run()
+    out = {}
+    if rank == 0:
+        srv.done.wait(30)
+        srv.stop()
+        recs = srv.state.history[args.warmup:]
+        spans = [r.t_end - r.t_start for r in recs]
+        fl_round_s = sum(spans) / max(1, len(spans))
+        hist = client.history[args.warmup:]
+        train_s = sum(h["train_s"] for h in hist) / max(1, len(hist))
+        ph = [p for p in client.phases if p["round"] > args.warmup]
+        mean = lambda k: round(sum(p[k] for p in ph) / max(1, len(ph)), 4)  # noqa: E731
+        imgs = world * args.epochs * args.local_steps * args.batch
+        out = {"metric": "FL product path: wall-clock per round (server release -> next release, gRPC)",
+               "value": round(fl_round_s, 4), "unit": "s/round", "higher_is_better": False, "n_gpus": world,
+               "steps": len(spans), "warmup": args.warmup, "final_state": state,
+               "images_per_s": round(imgs / fl_round_s, 2), "engine_round_s": round(engine_round_s, 4),
+               "control_plane_overhead_s": round(fl_round_s - engine_round_s, 4),
+               "client_train_round_s": round(train_s, 4), "client_aggregate_s": mean("aggregate_s"),
+               "client_upload_s": mean("upload_s"), "client_wait_s": mean("wait_s"),
+               "payload_bytes": ph[-1]["payload_bytes"] if ph else None, "codec": cfg.codec,
+               "data_plane": cfg.data_plane, "round_spans_s": [round(x, 4) for x in spans]}
+    return out
 
 
 if __name__ == "__main__":
