@@ -82,6 +82,10 @@ class UNetEngine:
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
         self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
+        # CFL_WGRAD_STREAM=1: weight gradients on a second HIP stream, concurrent with the dgrad chain. Off: the
+        # forked graph measured 9% SLOWER per step (8,670 -> 7,880 img/s, profiles/README.md)
+        self.side = torch.cuda.Stream(device=self.dev) if (self.dev.type == "cuda" and share is None and os.environ.get(
+            "CFL_WGRAD_STREAM", "0") == "1") else None
         self._build_pack()
         self._alloc()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -295,6 +299,24 @@ class UNetEngine:
         self.C.conv_wgrad(x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l,
                           dst_mode, 0, 0, rows)
 
+    def _side(self, fn) -> None:
+        """Launch ``fn``'s kernels on the weight-gradient stream after everything issued so far on the current
+        stream (a forked graph branch under capture). Weight gradients only read forward activations and the
+        incoming gradient and write their own slabs, so the dgrad chain continues concurrently; the branch joins
+        before grad_finish. Buffers a wgrad reads are never rewritten later in the same backward (dc2 / dy2)."""
+        if self.side is None:
+            fn()
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn()
+
+    def _join_side(self) -> None:
+        if self.side is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self.side)
+
     def bn_count(self, name: str) -> int:
         """Pixels per channel in the batch statistics of a BN layer."""
         i = self.bn_names.index(name)
@@ -454,21 +476,24 @@ class UNetEngine:
             else:
                 dq = D[f"d{k}_dq"]
                 C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
-            self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres, F, 1, 1, 0, 0, 0)
+            self._side(lambda: self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
+                                           F, 1, 1, 0, 0, 0))
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
             # convT2: input relu(BN_A(c1))
-            self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, 1)
+            self._side(lambda: self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
+                                           F, 3, 1, 1, 1, 1))
             # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
             self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None, 0, B, Rk, Rk, F,
                         0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1))
-            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc"],
+            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
                            self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
             # convT1: input relu(up?(prev))
-            self._wgrad(prev_t, D[f"d{k}_dc"], t1, None, 1, B, prevres, prevres, cprev, up, Rk, Rk, F, 3, 1, 1, 1, 1)
-            self._igemm(D[f"d{k}_dc"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk,
-                         F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
+            self._side(lambda: self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
+                                           Rk, F, 3, 1, 1, 1, 1))
+            self._igemm(D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk,
+                         Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
             # for k > 0 this gradient is also BN_B(k-1)'s node gradient: accumulate that BN's backward sums here
             if k > 0:
@@ -499,30 +524,31 @@ class UNetEngine:
             C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"], self.G(b2, "gamma"),
                            self.G(b2, "beta"), B * H * H, F, self.RS)
             # pointwise 2
-            self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H, F, 0, H, H, F, 1, 1,
-                        0, 0, 0)
+            self._side(lambda: self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
+                                           F, 0, H, H, F, 1, 1, 0, 0, 0))
             self._igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
                          H, H, F, 1, 1, 0, 0)
             # depthwise 2 on relu(BN_a(y1))
-            C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B, H, H, F,
-                       self.C.STAT_REPLICAS)
+            self._side(lambda: C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")],
+                                          bna["ab"], 1, B, H, H, F, self.C.STAT_REPLICAS))
             # depthwise dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
             C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
                        node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
                        node_relu=1)
-            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy"], self.G(b1, "gamma"),
+            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy2"], self.G(b1, "gamma"),
                            self.G(b1, "beta"), B * H * H, F, self.RS)
             # pointwise 1
-            self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy"], (s1, "pointwise_kernel"), None, 0, B, H, H, cin, 0, H, H, F, 1,
-                        1, 0, 0, 0)
-            self._igemm(D[f"e{k}_dy"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
+            self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
+                                           H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
+            self._igemm(D[f"e{k}_dy2"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
                          H, H, cin, 1, 1, 0, 0)
             # depthwise 1 on relu(x_in)
-            C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H, cin,
-                       self.C.STAT_REPLICAS)
+            self._side(lambda: C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B,
+                                          H, H, cin, self.C.STAT_REPLICAS))
             C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
-            self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F, 1, 2, 0, 0, 0)
+            self._side(lambda: self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
+                                           1, 2, 0, 0, 0))
             # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                          H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
@@ -538,6 +564,7 @@ class UNetEngine:
                                self.G(names[1], "beta"), B * H * H, cin, self.RS)
                 C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
                               ENTRY_FILTERS, self.C.STAT_REPLICAS)
+        self._join_side()
         if self._finish_dirty:
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("grad_finish table changed during graph capture")

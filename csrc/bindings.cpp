@@ -608,6 +608,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_CONV3_BN") = (int)TUNE_CONV3_BN;
   m.attr("TUNE_NODE_POOL2X2") = (int)TUNE_NODE_POOL2X2;
   m.attr("TUNE_ENTRY_ALGO") = (int)TUNE_ENTRY_ALGO;
+  m.attr("TUNE_CONV3_WS") = (int)TUNE_CONV3_WS;
+  m.attr("TUNE_CONV3_WS_GRID") = (int)TUNE_CONV3_WS_GRID;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

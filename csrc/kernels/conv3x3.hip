@@ -346,6 +346,252 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Weight-stationary persistent variant for the high-resolution decoder convs (Cin <= 64: the 128^2 / 64^2 maps at
+// 256^2 input, M = 65k-262k pixels, N = 32-128, K = 288-576). The per-tile kernel above re-loads the block's whole
+// weight tile (9 taps x BN x 32 per chunk) for every 128-pixel tile - more L2->LDS bytes than the activations - and
+// pays one global-load latency per tile with nothing to overlap it. Here a block keeps ALL K of its 32 output
+// channels in LDS for its lifetime (CH x 18.4 KB) and walks a strided list of pixel tiles; the next tile's raw halo
+// (every chunk) is in flight in registers while the current tile's 9 x CH taps run, and is BN-applied / ReLU'd
+// only when it is written to LDS (after the MFMAs), so the loads are never waited for early. BN statistics /
+// BN-node sums accumulate in registers across the block's tiles: one set of channel atomics per block.
+// LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
+template <int TH, int TW, int CH>
+__global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
+  constexpr int BN_ = 32, WM = 4;
+  constexpr int BM = TH * TW;
+  constexpr int HW = TW + 2, HP = (TH + 2) * HW;
+  constexpr int TM = BM / WM, FM = TM / 16, FN = BN_ / 16;
+  constexpr int HALO_CHUNKS = HP * (BK / 8);
+  constexpr int H_PER_T = (HALO_CHUNKS + NT - 1) / NT;
+  constexpr int SW = CH * 9 * BN_ * LDB, SH = CH * HP * LDH;
+  constexpr int LDC = BN_ + 8;
+  constexpr int CG = BN_ / 8, ROWS_PER_PASS = NT / CG;
+  static_assert(TM % 16 == 0 && H_PER_T <= 32, "tiling");
+
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SW + SH + BM * LDC];
+  __shared__ float sred[2][4][BN_];
+  bf16_t* sB = smem;                 // [CH][9][BN_][32]
+  bf16_t* sH = smem + SW;            // [CH][HP][32]
+  bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem + SW + SH);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nb = p.N / BN_;
+  const int nBlock = (blockIdx.x % nb) * BN_;       // gridDim.x % nb == 0: one column block per block
+  const int tiles_w = p.Wo / TW, tiles_hw = tiles_w * (p.Ho / TH);
+  const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
+  const bool has_ab = p.xf.ab != nullptr;
+  const int relu = p.xf.relu;
+
+  // ---- all weights of this column block: piece e -> (row = (ch*9 + tap)*BN_ + n, quarter q) ----
+  for (int e = tid; e < CH * 9 * BN_ * 4; e += NT) {
+    const int row = e >> 2, q = e & 3;
+    const int n = row % BN_, ct = row / BN_, ch = ct / 9, tap = ct - ch * 9;
+    *reinterpret_cast<uint4*>(sB + swz_off(row, q)) = *reinterpret_cast<const uint4*>(
+        p.wt + (size_t)(nBlock + n) * p.K + (size_t)tap * p.Cin + ch * BK + q * 8);
+  }
+  // producer BN coefficients of this thread's channel quarter, per chunk (constant over the block's tiles)
+  float a8[CH][8], b8[CH][8];
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch) {
+    load_f8_or(p.xf.ab + ch * BK + (tid & 3) * 8, has_ab, 1.f, a8[ch]);
+    load_f8_or(p.xf.ab + p.xf.C + ch * BK + (tid & 3) * 8, has_ab, 0.f, b8[ch]);
+  }
+
+  auto tile_of = [&](int item, int& b, int& ty0, int& tx0) {
+    int t = item / nb;
+    b = t / tiles_hw;
+    t -= b * tiles_hw;
+    ty0 = (t / tiles_w) * TH;
+    tx0 = (t % tiles_w) * TW;
+  };
+  // raw halo of a tile into registers (no use of the values here: the loads stay in flight)
+  uint4 rh[CH][H_PER_T];
+  uint32_t rvalid = 0;                                  // bit i: piece i lies inside the image
+  auto load_halo = [&](int item) {
+    int b, ty0, tx0;
+    tile_of(item, b, ty0, tx0);
+    rvalid = 0;
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      const int e = tid + i * NT;
+      const int hp = e >> 2, q = e & 3;
+      const int hy = hp / HW, hx = hp - hy * HW;
+      const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
+      const bool ok = e < HALO_CHUNKS && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+      rvalid |= (ok ? 1u : 0u) << i;
+      const bf16_t* src = p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + q * 8;
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok) v = *reinterpret_cast<const uint4*>(src + ch * BK);
+        rh[ch][i] = v;
+      }
+    }
+  };
+  // producer BN-apply + ReLU on the way into LDS; padding stays exactly 0 (it is outside the transform)
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (e >= HALO_CHUNKS) continue;
+      const bool ok = (rvalid >> i) & 1u;
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        uint4 v = rh[ch][i];
+        if (has_ab || relu) {
+          float f[8];
+          unpack8(v, f);
+          if (has_ab) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaf(a8[ch][j], f[j], b8[ch][j]);
+          }
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          }
+          v = ok ? pack8(f) : make_uint4(0, 0, 0, 0);
+        }
+        *reinterpret_cast<uint4*>(sH + ch * HP * LDH + swz_off(e >> 2, e & 3)) = v;
+      }
+    }
+  };
+
+  int fhp[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int pp = wid * TM + i * 16 + (lane & 15);
+    fhp[i] = (pp / TW) * HW + pp % TW;
+  }
+  const int fq = lane >> 4;
+  const int cg = tid % CG;
+  const bool node = p.node.y != nullptr;
+  NodeCoef nk;
+  if (node) node_coef_load(p.node.ab, p.N, nBlock + cg * 8, nk);
+  float biasf[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) biasf[j] = p.bias ? p.bias[nBlock + j * 16 + (lane & 15)] : 0.f;
+  float s[2][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[0][q] = s[1][q] = 0.f;
+
+  int item = blockIdx.x;
+  if (item < n_items) {
+    load_halo(item);
+    store_halo();
+  }
+  __syncthreads();
+  for (; item < n_items; item += gridDim.x) {
+    const int next = item + gridDim.x;
+    if (next < n_items) load_halo(next);               // in flight during this tile's MFMAs
+    f4v acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        s8v af[FM], bfg[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = *reinterpret_cast<const s8v*>(sH + ch * HP * LDH + swz_off(fhp[i] + ky * HW + kx, fq));
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bfg[j] = *reinterpret_cast<const s8v*>(sB + swz_off((ch * 9 + tap) * BN_ + j * 16 + (lane & 15), fq));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      }
+    // accumulators + bias -> bf16 staging tile (one rounding, as the per-tile kernel)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int cl = j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sC[wid * TM + i * 16 + (lane >> 4) * 4 + r][cl] = f2bf(acc[i][j][r] + biasf[j]);
+    }
+    __syncthreads();                                    // halo reads done, C tile complete
+    if (next < n_items) store_halo();
+    int b, ty0, tx0;
+    tile_of(item, b, ty0, tx0);
+#pragma unroll
+    for (int r0 = 0; r0 < BM; r0 += ROWS_PER_PASS) {
+      const int row = r0 + tid / CG;
+      const int m = (b * p.Ho + ty0 + row / TW) * p.Wo + tx0 + row % TW;
+      const size_t off = (size_t)m * p.N + nBlock + cg * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
+      if (node) {
+        v = node_epi(v, p.node.y + off, nk, p.node.relu, s[0], s[1]);
+      } else {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          s[0][q] += f[q];
+          s[1][q] += f[q] * f[q];
+        }
+      }
+      *reinterpret_cast<uint4*>(p.y + off) = v;
+    }
+    __syncthreads();                                    // next halo visible, C tile consumed
+  }
+  if (p.stats || node) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      for (int o = CG; o < 64; o <<= 1) {
+        s[0][q] += __shfl_xor(s[0][q], o, 64);
+        s[1][q] += __shfl_xor(s[1][q], o, 64);
+      }
+    if (lane < CG) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        sred[0][wid][cg * 8 + q] = s[0][q];
+        sred[1][wid][cg * 8 + q] = s[1][q];
+      }
+    }
+    __syncthreads();
+    const int rb = blockIdx.x / nb;                     // replica row (blocks of one column block spread)
+    float* rep = node ? p.node.sums + (size_t)(rb % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+                      : p.stats + (size_t)(rb % STAT_REPLICAS) * 2 * p.N;
+    for (int e = tid; e < 2 * BN_; e += NT) {
+      const int st = e / BN_, cc = e - st * BN_;
+      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+    }
+  }
+}
+
+// every 3x3 / stride-1 conv with Cin in {32, 64} on maps tiled exactly by 8x16 (or 16x8) pixel tiles
+// (TUNE_CONV3_WS: 1 = never, 2 = whenever the shape allows it, regardless of the tile count - tests)
+static bool ws_eligible(const ConvParams& p) {
+  const int v = cfl_tune(TUNE_CONV3_WS);
+  if (v == 1) return false;
+  if (!(p.Cin == 32 || p.Cin == 64) || p.N % 32) return false;
+  const int tw = p.Wo >= 16 ? 16 : 8, th = 128 / tw;
+  if (p.Ho % th || p.Wo % tw) return false;
+  const int items = (p.Ho / th) * (p.Wo / tw) * p.B * (p.N / 32);
+  // measured (tools/kbench.py, 256^2 / B16): the 128^2 level (2048-4096 items, >= 3 tiles per block) gains 15-22 %,
+  // the 64^2 level (1024 items, 2 tiles per block) loses 15 % - the per-tile kernel stays there
+  return v == 2 || items >= 2048;
+}
+
+template <int TH, int TW, int CH>
+void launch_ws(const ConvParams& p, hipStream_t st) {
+  const int nb = p.N / 32;
+  const int items = (p.Ho / TH) * (p.Wo / TW) * p.B * nb;
+  int grid = cfl_tune(TUNE_CONV3_WS_GRID) > 0 ? cfl_tune(TUNE_CONV3_WS_GRID) : (CH == 1 ? 768 : 512);
+  grid = grid / nb * nb;
+  if (grid < nb) grid = nb;
+  if (grid > items) grid = items;
+  hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
+}
+
 template <int TH, int TW, int BN_, int WM, int WN, bool WB = false>
 int launch(const ConvParams& p, int splits, hipStream_t st) {
   const int chunks = p.Cin / BK;
@@ -385,7 +631,7 @@ static bool small_tiles(const ConvParams& p) {
   return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
 }
 
-int conv3x3_splits(const ConvParams& p) { return small_tiles(p) ? 1 : conv3x3_split_k(p); }
+int conv3x3_splits(const ConvParams& p) { return small_tiles(p) || ws_eligible(p) ? 1 : conv3x3_split_k(p); }
 
 // K splits of the 8x16 / 16x8-pixel tiles (the fp8 kernel has no small-tile variant and always uses this)
 int conv3x3_split_k(const ConvParams& p) {
@@ -408,6 +654,17 @@ bool conv3x3_supported(const ConvParams& p) {
 
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
+  if (ws_eligible(p)) {                     // weight-stationary persistent tiles (no split-K)
+    const bool w16 = p.Wo >= 16;
+    if (p.Cin == 32) {
+      if (w16) launch_ws<8, 16, 1>(p, st);
+      else launch_ws<16, 8, 1>(p, st);
+    } else {
+      if (w16) launch_ws<8, 16, 2>(p, st);
+      else launch_ws<16, 8, 2>(p, st);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   int splits = conv3x3_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const bool w16 = p.Wo >= 16;

@@ -290,6 +290,8 @@ enum TuneKey {
   TUNE_NODE_POOL2X2 = 11,      // max-pool node gradient: 0 = 2x2-block kernel, 1 = per-pixel gather
   TUNE_ENTRY_ALGO = 12,        // entry conv (Cout 32): 0 = MFMA kernels, 1 = VALU kernels
   TUNE_HEAD_BLOCKS = 13,       // head fwd / bwd grid cap (default 512)
+  TUNE_CONV3_WS = 14,          // conv3x3 Cin <= 64: 0 = weight-stationary persistent kernel, 1 = per-tile kernel
+  TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
   TUNE_N = 16
 };
 int cfl_tune(int key);

@@ -765,6 +765,53 @@ def test_conv3x3_small_tiles_forced(B, Hs, Cin, N, up, use_ab):
         hip().set_tune(hip().TUNE_CONV3_SMALL, 0)
 
 
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,grid", [
+    (2, 16, 64, 32, 0, True, 0),     # 128^2-level shape family: CH 2, 8x16 tiles
+    (2, 8, 32, 64, 1, False, 0),     # upsampled input, CH 1, two column blocks
+    (3, 16, 32, 128, 0, True, 6),    # 4 column blocks, grid 6 -> 4: several tiles per block
+    (2, 8, 64, 32, 1, True, 2),      # upsampled, CH 2: a 2-block grid walks all 4 tiles
+])
+def test_conv3x3_weight_stationary_forced(B, Hs, Cin, N, up, use_ab, grid):
+    """TUNE_CONV3_WS=2 forces the weight-stationary persistent kernel (every K of a 32-column block resident in
+    LDS, halos prefetched across the block's tiles, statistics accumulated across tiles) on small shapes; output and
+    BN statistics vs the generic implicit GEMM and the fp32 reference."""
+    C_ = hip()
+    C_.set_tune(C_.TUNE_CONV3_WS, 2)
+    C_.set_tune(C_.TUNE_CONV3_WS_GRID, grid)
+    try:
+        test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
+    finally:
+        C_.set_tune(C_.TUNE_CONV3_WS, 0)
+        C_.set_tune(C_.TUNE_CONV3_WS_GRID, 0)
+
+
+def test_conv3x3_weight_stationary_node_epilogue():
+    """The BN-node gradient epilogue (dgrad producer) on the weight-stationary kernel == the per-tile kernel."""
+    torch.manual_seed(23)
+    C_ = hip()
+    B, H, Cin, N = 2, 16, 32, 64
+    xb, _ = bf(torch.randn(B, H, H, Cin))
+    yb, _ = bf(torch.randn(B, H, H, N))
+    wb = pack(PK_CONVT_DGRAD, torch.randn(3, 3, Cin, N) * 0.05, 3, N, Cin)
+    ab, _, _ = ab_for(N, 24)
+    ab[2 * N:3 * N] = torch.randn(N) * 0.1
+    ab[3 * N:] = torch.rand(N) + 0.5
+    outs = []
+    for v in (1, 2):
+        C_.set_tune(C_.TUNE_CONV3_WS, v)
+        try:
+            g = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            sums = torch.zeros(4 * 2 * N, device=DEV)
+            C_.conv_igemm(xb, wb, None, g, None, None, 0, B, H, H, Cin, 0, H, H, N, 3, 1, 1, 1, None, 0,
+                          node_y=yb, node_ab=ab.to(DEV), node_sums=sums, node_reps=4, node_relu=1)
+            outs.append((from_bits(g), sums.view(4, 2, N).sum(0).cpu()))
+        finally:
+            C_.set_tune(C_.TUNE_CONV3_WS, 0)
+    (g1, s1), (g2, s2) = outs
+    assert rel(g2, g1) < 5e-3 and (g1 == 0).sum() == (g2 == 0).sum()
+    assert torch.allclose(s2, s1, rtol=2e-3, atol=5e-2)
+
+
 def test_evaluator_engine_matches_per_batch_eval():
     """UNetEngine.evaluator(k*B): the same held-out images evaluated k batches per launch over the SHARED
     parameters give the same per-pixel loss / accuracy as the reference's B-image batches."""

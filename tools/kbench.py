@@ -66,6 +66,9 @@ def main():
     ap.add_argument("--variants", action="store_true", help="also time algo variants of conv_wgrad / conv_igemm")
     ap.add_argument("--tune", default="", help="launch knobs, e.g. 3=256,4=2 (see TuneKey in launch.h)")
     ap.add_argument("--quiet", action="store_true", help="totals only")
+    ap.add_argument("--roofline", action="store_true",
+                    help="per call: minimum HBM bytes (every tensor argument read or written once), MFMA flops, "
+                         "achieved GB/s / TF/s and the roofline floor max(bytes / 6.3 TB/s, flops / 2.5 PF/s)")
     args = ap.parse_args()
     table = ParamTable()
     data = make_synthetic_device(64, args.img, seed=0)
@@ -86,6 +89,9 @@ def main():
         kk, v = kv.split("=")
         C.set_tune(int(kk), int(v))
     want = set(args.ops.split(",")) if args.ops else None
+    roof = defaultdict(float)
+    if args.roofline:
+        print(f"{'us':>8}  {'floor':>7} {'eff':>5}   {'min bytes':>11} {'achieved':>10}  {'MFMA':>12}  op(shape ints)")
     tot = defaultdict(float)
     n = defaultdict(int)
     print(f"{'us':>8}  op(shape ints)")
@@ -100,6 +106,15 @@ def main():
         tot[name] += t
         n[name] += 1
         line = f"{t:8.1f}  {shape_key(name, a, k)}"
+        if args.roofline:
+            by, fl = min_bytes(eng, name, a, k), conv_flops(name, a)
+            floor = max(by / HBM_BPS, fl / MFMA_FPS) * 1e6
+            roof["bytes"] += by
+            roof["flops"] += fl
+            roof["floor"] += floor
+            roof["time"] += t
+            line = (f"{t:8.1f}  {floor:7.1f} {100 * floor / max(t, 1e-9):5.0f}%  {by / 1e6:8.2f} MB {by / t / 1e3:6.2f} "
+                    f"TB/s  {fl / t / 1e6:7.1f} TF/s  {shape_key(name, a, k)}")
         if args.variants and name in ("conv_wgrad", "conv_igemm", "dw_fwd", "dw_dgrad", "dw_wgrad"):
             for algo in ((1, 2, 0) if name.startswith("dw_") else (1, 0)):
                 a2, kk = list(a), dict(k)
@@ -119,6 +134,48 @@ def main():
     for name in sorted(tot, key=lambda x: -tot[x]):
         print(f"{tot[name]:9.1f}  {n[name]:3d} calls  {name}")
     print(f"{sum(tot.values()):9.1f}  total")
+    if args.roofline and roof["time"]:
+        print(f"\nwhole step (isolated replays, L2/Infinity-Cache warm): {roof['time']:.1f} us measured, minimum "
+              f"{roof['bytes'] / 1e6:.1f} MB + {roof['flops'] / 1e9:.1f} GFLOP -> roofline floor {roof['floor']:.1f} us "
+              f"({100 * roof['floor'] / roof['time']:.0f}% of measured; {roof['bytes'] / roof['time'] / 1e3:.2f} TB/s "
+              f"average over the step)")
+
+
+HBM_BPS = 6.3e12          # achievable HBM3E streaming rate on MI355X (MI355X_MICROARCH.md: 8 TB/s spec, ~6.3 achievable)
+MFMA_FPS = 2.5e15         # dense bf16 MFMA peak
+
+
+def min_bytes(eng, name, a, k):
+    """Bytes the call must move at least: every tensor argument read or written once (the dataset arguments count
+    only the batch's images / masks; packed weights and tables are small)."""
+    tot = 0
+    scratch = [eng.ws, eng.gws] + list(eng._wslabs.values())   # split-K workspace / weight-gradient slab rows: design
+    spans = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in scratch if t.numel()]
+    for x in list(a) + list(k.values()):
+        if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
+            continue
+        if any(lo <= x.data_ptr() < hi for lo, hi in spans):
+            continue                     # scratch of this design, not a minimum (the weight gradient itself is small)
+        if eng.images is not None and x.data_ptr() == eng.images.data_ptr():
+            tot += eng.B * eng.S * eng.S * 3
+        elif eng.masks is not None and x.data_ptr() == eng.masks.data_ptr():
+            tot += eng.B * eng.S * eng.S
+        else:
+            tot += x.numel() * x.element_size()
+    return tot
+
+
+def conv_flops(name, a):
+    """2*M*N*K of the conv_igemm / conv_wgrad calls (positional ints: B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, ...)."""
+    if name not in ("conv_igemm", "conv_wgrad", "conv3x3_fp8"):
+        return 0.0
+    ints = [x for x in a if isinstance(x, int) and not isinstance(x, bool)]
+    i0 = 1 if name == "conv_igemm" or name == "conv3x3_fp8" else 1    # relu flag precedes B
+    try:
+        B, Hin, Win, Cin, up, Ho, Wo, N, ks = ints[i0:i0 + 9]
+    except ValueError:
+        return 0.0
+    return 2.0 * B * Ho * Wo * N * ks * ks * Cin
 
 
 if __name__ == "__main__":
