@@ -256,8 +256,14 @@ class UNetEngine:
         self._finish_dyn: List[tuple] = []
         self._wslabs: Dict[str, torch.Tensor] = {}
         self._build_finish()
+        # CFL_BN_TAIL=1: in-launch BN finalize (launch.h BnFinal; one ticket counter per BN layer, the producer's last
+        # block computes the coefficients). Off by default: the per-block ticket round trip (atomics drained, then a
+        # returning atomic) delays every block's retirement - measured 7.5% SLOWER per step than the 15 separate
+        # 1-block bn_finalize launches (8,730 -> 8,076 img/s, profiles/README.md)
+        self.bn_tail = os.environ.get("CFL_BN_TAIL", "0") == "1"
+        self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
         # per-step zeroing of gradients / statistics in one launch
-        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10]]
+        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10], self.bn_ctr]
         self.zero_table = self.C.make_zero_table(spans)
         self.n_zero, self.max_zero = len(spans), max(t.numel() * t.element_size() for t in spans)
         # inference BN coefficients of every layer (one launch per eval forward)
@@ -348,10 +354,20 @@ class UNetEngine:
             ev.bind_data(self.images, self.masks)
 
     # ------------------------------------------------------------------------------------------------ schedule
+    def _fin(self, name: str, train: bool) -> Dict[str, object]:
+        """Producer kwargs that make the launch accumulating BN layer ``name``'s batch statistics also finalize
+        them (in its last block); empty in inference mode or with the tail disabled."""
+        if not train or not self.bn_tail:
+            return {}
+        b = self.bn[name]
+        i = self.bn_names.index(name)
+        return dict(fin_ab=b["ab"], fin_gamma=self.P(name, "gamma"), fin_beta=self.P(name, "beta"),
+                    fin_ctr=self.bn_ctr[i:i + 1], fin_count=float(self.bn_count(name)), fin_eps=self.bn_eps)
+
     def _bn_final(self, name: str, train: bool) -> torch.Tensor:
         b = self.bn[name]
-        if not train:
-            return b["ab"]                     # inference: all coefficients written by forward()'s bn_eval_coefs
+        if not train or self.bn_tail:
+            return b["ab"]          # inference: written by forward()'s bn_eval_coefs; train: by the producer's tail
         self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
                            self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
                            float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
@@ -359,7 +375,7 @@ class UNetEngine:
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
-               join: Optional[Dict[str, object]] = None) -> None:
+               join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
 
         ``node`` = (y, bn, relu): the output is the incoming gradient of that BN node; the kernel's epilogue writes
@@ -376,16 +392,18 @@ class UNetEngine:
             kw = dict(node_y=ny, node_ab=bn["ab"], node_sums=bn["sums"], node_reps=self.RS, node_relu=nrelu)
         if join:
             kw.update(join)
+        if fin:
+            kw.update(fin)
         self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                           pad_l, self.ws if need > 1 else None, **kw)
 
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
               Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor],
-              join: Optional[Dict[str, object]] = None) -> None:
+              join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None) -> None:
         pad = (ks - 1) // 2 if stride == 1 else 0
         B = self.B
         self._igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
-                    N, ks, stride, pad, pad, join=join)
+                    N, ks, stride, pad, pad, join=join, fin=fin)
 
     def forward(self, train: bool = True) -> None:
         C, B, r, A = self.C, self.B, self.r, self.act
@@ -397,7 +415,7 @@ class UNetEngine:
         e_conv, e_bn = next(n), next(n)
         st = self.bn[e_bn]["stats"] if train else None
         C.entry_fwd(self.images, self.idx, self.P(e_conv, "kernel"), self.P(e_conv, "bias"), A["y0"], st, B, self.S,
-                    ENTRY_FILTERS)
+                    ENTRY_FILTERS, **self._fin(e_bn, train))
         ab0 = self._bn_final(e_bn, train)
         x = Lazy(A["y0"], ab0, 1, r[0], ENTRY_FILTERS)     # a0 = relu(BN0(y0))
         for k, F in enumerate(ENC_FILTERS):
@@ -405,11 +423,11 @@ class UNetEngine:
             H = r[k]
             C.dw_fwd(x.t, self.P(s1, "depthwise_kernel"), A[f"e{k}_d1"], x.ab, 1, B, H, H, x.C)
             self._conv(Lazy(A[f"e{k}_d1"], None, 0, H, x.C), s1, PK_PW, A[f"e{k}_y1"], F, 1, 1, 0, H,
-                       self.P(s1, "bias"), self.bn[b1]["stats"] if train else None)
+                       self.P(s1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
             ab1 = self._bn_final(b1, train)
             C.dw_fwd(A[f"e{k}_y1"], self.P(s2, "depthwise_kernel"), A[f"e{k}_d2"], ab1, 1, B, H, H, F)
             self._conv(Lazy(A[f"e{k}_d2"], None, 0, H, F), s2, PK_PW, A[f"e{k}_y2"], F, 1, 1, 0, H,
-                       self.P(s2, "bias"), self.bn[b2]["stats"] if train else None)
+                       self.P(s2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train))
             ab2 = self._bn_final(b2, train)
             if self.fuse_join:   # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
                 self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
@@ -425,10 +443,10 @@ class UNetEngine:
             Rk = r[3] << k
             up = 0 if k == 0 else 1
             self._convt(Lazy(prev.t, None, 1, prev.H, prev.C), t1, A[f"d{k}_c1"], F, up, Rk,
-                        self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
+                        self.P(t1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
             abA = self._bn_final(b1, train)
             self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
-                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None)
+                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train))
             abB = self._bn_final(b2, train)
             if self.fuse_join:   # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
                 self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None,
@@ -587,11 +605,11 @@ class UNetEngine:
                             self.amax8 if step else None, self.n_views8)
 
     def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
-               bias: torch.Tensor, stats: Optional[torch.Tensor]) -> None:
+               bias: torch.Tensor, stats: Optional[torch.Tensor], fin: Optional[Dict[str, object]] = None) -> None:
         """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled (maps of at least 8x8; smaller ones - only
         at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel."""
         if not self.fp8 or Ho < 8:
-            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats)
+            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, fin=fin)
             return
         B = self.B
         need = self.C.conv_splits_fp8(B, Ho, Ho, N, x.C)
@@ -605,7 +623,7 @@ class UNetEngine:
             self._await_all()                # the fp8 copies are repacked after the LAST FedAvg bucket
         self.C.conv3x3_fp8(x.t, self.packed8[off8:off8 + n8], self.scales8[soff:soff + cout], self.amax8[i],
                            bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho, N,
-                           self.ws if need > 1 else None)
+                           self.ws if need > 1 else None, **(fin or {}))
 
     def _fp8_calibrate(self) -> None:
         """Seed the delayed activation scales: one training-mode forward records every fp8 conv input's amax,

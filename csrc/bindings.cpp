@@ -39,6 +39,24 @@ void ok(int rc, const char* what) {
 
 InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(ab, "ab"), C, relu}; }
 
+// in-launch BN finalize arguments (launch.h BnFinal); fin_ab = None -> off (the engine launches nothing else then)
+BnFinal fin_args(const OptT& fin_ab, const OptT& fin_gamma, const OptT& fin_beta, const OptT& fin_ctr, double count,
+                 double eps, int C, bool has_stats) {
+  BnFinal f{};
+  if (!fin_ab) return f;
+  TORCH_CHECK(has_stats && fin_gamma && fin_beta && fin_ctr, "BN finalize: needs stats, fin_gamma, fin_beta, fin_ctr");
+  TORCH_CHECK(fin_ab->numel() >= 4 * C && fin_gamma->numel() >= C && fin_beta->numel() >= C &&
+              fin_ctr->numel() >= 1 && fin_ctr->element_size() == 4 && count > 0 && C <= 256,
+              "BN finalize: argument sizes");
+  f.ab = ptr<float>(*fin_ab, "fin_ab");
+  f.gamma = ptr<const float>(*fin_gamma, "fin_gamma");
+  f.beta = ptr<const float>(*fin_beta, "fin_beta");
+  f.counter = ptr<unsigned>(*fin_ctr, "fin_ctr");
+  f.count = (float)count;
+  f.eps = (float)eps;
+  return f;
+}
+
 // fused BN-node gradient epilogue arguments (launch.h BnNodeEpi); node_y = None -> off
 BnNodeEpi node_epi_args(const OptT& node_y, const OptT& node_ab, const OptT& node_sums, int reps, int relu,
                         int64_t out_numel, int C) {
@@ -59,7 +77,8 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
                    int node_relu, int join_mode, OptT join_y, OptT join_ab, OptT join_out, OptT join_argmax,
-                   int join_H, int join_W) {
+                   int join_H, int join_W, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
+                   double fin_eps) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -80,6 +99,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
   p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, y.numel(), N);
   TORCH_CHECK(!p.node.y || (!p.stats && !p.bias), "conv_igemm: the node epilogue excludes stats and bias");
+  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, N, p.stats != nullptr);
   if (join_mode) {
     TORCH_CHECK(join_mode >= JOIN_POOL && join_mode <= JOIN_ADD_UP && join_y && join_ab && join_out,
                 "conv_igemm: join needs join_y, join_ab, join_out");
@@ -202,7 +222,8 @@ void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, 
 }
 
 void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bias, at::Tensor y, OptT stats, int B,
-                  int S, int Cout) {
+                  int S, int Cout, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
+                  double fin_eps) {
   EntryParams p{};
   p.images = ptr<const uint8_t>(images, "images");
   p.idx = ptr<const int32_t>(idx, "idx");
@@ -212,6 +233,7 @@ void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bi
   p.stats = optr<float>(stats, "stats");
   p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
   TORCH_CHECK(idx.numel() == B && y.numel() == (int64_t)B * p.Ho * p.Wo * Cout && w.numel() == 27 * Cout, "entry_fwd sizes");
+  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, Cout, p.stats != nullptr);
   ok(entry_fwd(p, stream()), "entry_fwd");
 }
 
@@ -511,7 +533,8 @@ void pack_fp8_op(at::Tensor flat, at::Tensor packed8, at::Tensor scales, at::Ten
 
 void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor amax, OptT bias, at::Tensor y,
                     OptT stats, OptT ab, int relu, int B, int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N,
-                    OptT ws) {
+                    OptT ws, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
+                    double fin_eps) {
   Conv8Params q{};
   ConvParams& p = q.c;
   p.x = ptr<const bf16_t>(x, "x");
@@ -532,6 +555,7 @@ void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor 
   TORCH_CHECK(wt8.numel() >= (int64_t)N * p.K && wscale.numel() >= N && amax.numel() >= 2, "conv3x3_fp8: w sizes");
   TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv3x3_fp8: y size");
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv3x3_fp8: stats size");
+  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, N, p.stats != nullptr);
   const int rc = conv3x3_fp8(q, stream());
   TORCH_CHECK(rc <= 0, "conv3x3_fp8 failed (code ", rc, ")");
   if (rc < 0) ok(splitk_epilogue(p, -rc, stream()), "conv3x3_fp8 split-K epilogue");
@@ -565,7 +589,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,
         py::arg("node_relu") = 1, py::arg("join_mode") = 0, py::arg("join_y") = py::none(),
         py::arg("join_ab") = py::none(), py::arg("join_out") = py::none(), py::arg("join_argmax") = py::none(),
-        py::arg("join_H") = 0, py::arg("join_W") = 0);
+        py::arg("join_H") = 0, py::arg("join_W") = 0, py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
+        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
@@ -589,7 +614,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_relu") = 1);
   m.def("dw_wgrad", &dw_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1, py::arg("algo") = 0);
-  m.def("entry_fwd", &entry_fwd_op);
+  m.def("entry_fwd", &entry_fwd_op, py::arg("images"), py::arg("idx"), py::arg("w"), py::arg("bias"), py::arg("y"),
+        py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
+        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
   m.def("entry_wgrad", &entry_wgrad_op, py::arg("images"), py::arg("idx"), py::arg("dy"), py::arg("dw"), py::arg("B"),
         py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1);
   m.def("make_grad_finish_table", &make_grad_finish_table);
@@ -635,7 +662,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv3x3_fp8", &conv3x3_fp8_op, py::arg("x"), py::arg("wt8"), py::arg("wscale"), py::arg("amax"),
         py::arg("bias"), py::arg("y"), py::arg("stats"), py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"),
         py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"),
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
+        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
         py::arg("max_elems"), py::arg("step") = py::none());
   m.def("render_cracks", &render_cracks_op);

@@ -343,6 +343,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
+    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -564,6 +565,7 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
+    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 

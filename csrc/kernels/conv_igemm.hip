@@ -323,6 +323,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
       atomicAdd(&rep[st * p.N + nBlock + cc], v);
     }
+    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -388,6 +389,7 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
     for (int w = 0; w < NT / 64; ++w) v += red[st][w][cc];
     atomicAdd(&rep[st * p.N + cc], v);
   }
+  if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x);
 }
 
 template <int BM_, int BN_, int WM, int WN>

@@ -77,7 +77,10 @@ __global__ __launch_bounds__(NT) void entry_fwd_kernel(EntryParams p) {
       }
     }
   }
-  if (p.stats) block_channel_atomics<2>(s, G, p.Cout, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.Cout, red);
+  if (p.stats) {
+    block_channel_atomics<2>(s, G, p.Cout, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.Cout, red);
+    bn_final_tail(p.fin, p.stats, p.Cout, gridDim.x * gridDim.y * gridDim.z);
+  }
 }
 
 // dW[ky][kx][ci][co] = sum_pix x[2oh+ky][2ow+kx][ci] * dy[pix][co]; blockIdx.y = ky, thread = (pixel, 8 outputs).
@@ -273,7 +276,10 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
     __syncthreads();
     buf ^= 1;
   }
-  if (p.stats) block_channel_atomics<2>(s, 4, 32, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 64, red);
+  if (p.stats) {
+    block_channel_atomics<2>(s, 4, 32, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 64, red);
+    bn_final_tail(p.fin, p.stats, 32, gridDim.x * gridDim.y * gridDim.z);
+  }
 }
 
 __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int nch, int steps, int replicas) {

@@ -10,6 +10,21 @@
 // per-block atomics of thousands of workgroups do not all hit the same 2*C words; bn_finalize sums the replicas.
 #define STAT_REPLICAS 32
 
+// In-launch BatchNorm finalize ("last workgroup done"): the producer of a BN layer's batch statistics turns them into
+// the layer's (a, b, mean, rstd) rows itself instead of a separate 1-block bn_finalize launch (15 per step). Every
+// block adds its statistics with agent-scope float atomics (executed memory-side, never cached in an XCD's L2),
+// waits for them (vmcnt 0), then one lane draws a ticket from `counter`; the block that draws the last ticket reads
+// the replica rows with sc1 loads (L1 bypass) and writes ab (cdna_hip_programming.md §6 Guideline 16: counter form
+// with write-through payload). The last block re-zeroes the counter (the engine also zeroes it every step).
+struct BnFinal {
+  const float* gamma;      // nullptr = off
+  const float* beta;
+  float* ab;               // [4][C]
+  unsigned* counter;
+  float count;             // pixels per channel
+  float eps;
+};
+
 // ---------------------------------------------------------------- implicit-GEMM conv (conv_igemm.hip)
 // BN-node gradient epilogue (backward). The kernel's output o is the incoming gradient of a BatchNorm node whose
 // forward input was `y` (ab rows: a, b, mean, rstd). Instead of o the kernel writes the node gradient
@@ -53,6 +68,7 @@ struct ConvParams {
   int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
   BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
   ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
+  BnFinal fin;         // optional in-launch finalize of `stats` (run by the launch that completes them)
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
@@ -122,6 +138,7 @@ struct EntryParams {
   float* dw;               // wgrad destination (3,3,3,Cout) fp32: [replicas][27*Cout]
   int B, S, Cout, Ho, Wo;
   int replicas;            // wgrad: >1 = spread block atomics over that many row copies (summed by grad_finish)
+  BnFinal fin;             // forward: in-launch finalize of `stats`
 };
 int entry_fwd(const EntryParams& p, hipStream_t st);
 int entry_wgrad(const EntryParams& p, hipStream_t st);
@@ -303,3 +320,59 @@ int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int row
                    hipStream_t st);
 int render_cracks(const float* segs, const float* params, uint8_t* images, uint8_t* masks, int n, int img,
                   int max_seg, hipStream_t st);
+
+// Tail of a statistics producer (see BnFinal). EVERY thread of EVERY block of the launch calls it after issuing its
+// block's statistics atomics into stats[STAT_REPLICAS][2][C] (C <= 256, blockDim.x <= 256); `nblocks` = the
+// launch's grid size. The last block computes ab.
+__device__ __forceinline__ void bn_final_tail(const BnFinal& f, const float* stats, int C, int nblocks) {
+  __shared__ float spart[2 * 256];
+  __shared__ int sflag[1];
+  if (f.gamma == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's atomics have completed
+  __syncthreads();                                          // ... and every other wave's
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(f.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sflag = old == (unsigned)nblocks - 1;
+  }
+  __syncthreads();
+  if (!*sflag) return;
+  // thread -> (channel c, replica phase j): all of a channel's 2 * STAT_REPLICAS loads in one round
+  const int nt = blockDim.x, per = nt >= C ? nt / C : 1;
+  const int c = threadIdx.x % C, j = threadIdx.x / C;
+  float a = 0.f, b = 0.f;
+  if (j < per) {
+    float va[STAT_REPLICAS], vb[STAT_REPLICAS];
+#pragma unroll
+    for (int k = 0; k < STAT_REPLICAS; ++k) {
+      const int r = j + k * per;
+      va[k] = r < STAT_REPLICAS ? __hip_atomic_load(stats + (size_t)r * 2 * C + c, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      vb[k] = r < STAT_REPLICAS ? __hip_atomic_load(stats + (size_t)r * 2 * C + C + c, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < STAT_REPLICAS; ++k) {
+      a += va[k];
+      b += vb[k];
+    }
+  }
+  spart[threadIdx.x] = a;
+  spart[nt + threadIdx.x] = b;
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += nt) {
+    float s = 0.f, s2 = 0.f;
+    for (int k = 0; k < per; ++k) {
+      s += spart[k * C + cc];
+      s2 += spart[nt + k * C + cc];
+    }
+    const float mean = s / f.count;
+    const float var = fmaxf(s2 / f.count - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + f.eps);
+    const float sa = f.gamma[cc] * rstd;
+    f.ab[cc] = sa;
+    f.ab[C + cc] = f.beta[cc] - mean * sa;
+    f.ab[2 * C + cc] = mean;
+    f.ab[3 * C + cc] = rstd;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(f.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -951,3 +951,43 @@ def test_head_loss_metrics_and_gradients_match_autograd(dice):
     assert float(m[6]) == float(t.sum())
     assert rel(from_bits(dx), gx) < 1e-2
     assert rel(dw.cpu(), gw) < 1e-3 and rel(db.cpu(), gb) < 1e-3
+
+
+@pytest.mark.parametrize("ks,H,Cin,N,B,tune", [
+    (1, 32, 32, 64, 4, ""),          # generic implicit GEMM (pointwise conv)
+    (3, 16, 64, 32, 2, ""),          # per-tile conv3x3 kernel
+    (3, 16, 64, 32, 2, "ws"),        # weight-stationary persistent conv3x3 kernel
+    (3, 8, 256, 256, 4, "split"),    # split-K: the tail runs in the split-K epilogue launch
+])
+def test_in_launch_bn_finalize_matches_bn_finalize(ks, H, Cin, N, B, tune):
+    """launch.h BnFinal: the statistics producer's last block writes the BN coefficients (a, b, mean, rstd) exactly
+    as a separate bn_finalize launch over the same replica rows would, and re-arms its ticket counter (two calls)."""
+    torch.manual_seed(31)
+    C_ = hip()
+    xb, _ = bf(torch.randn(B, H, H, Cin))
+    wb = pack(PK_CONV, torch.randn(ks, ks, Cin, N) * 0.05, ks, Cin, N)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    gamma, beta = (torch.rand(N) + 0.5).to(DEV), (torch.randn(N) * 0.2).to(DEV)
+    mm, mv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int32, device=DEV)
+    if tune == "ws":
+        C_.set_tune(C_.TUNE_CONV3_WS, 2)
+    if tune == "split":
+        C_.set_tune(C_.TUNE_CONV3_SMALL, 1)
+    try:
+        for _ in range(2):
+            y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            stats = torch.zeros(C_.STAT_REPLICAS * 2 * N, device=DEV)
+            ab_tail = torch.zeros(4 * N, device=DEV)
+            ws = torch.zeros(16 * B * H * H * N, device=DEV)
+            C_.conv_igemm(xb, wb, bias, y, stats, None, 0, B, H, H, Cin, 0, H, H, N, ks, 1, (ks - 1) // 2,
+                          (ks - 1) // 2, ws, 0, fin_ab=ab_tail, fin_gamma=gamma, fin_beta=beta, fin_ctr=ctr,
+                          fin_count=float(B * H * H), fin_eps=1e-3)
+            ab_ref = torch.zeros(4 * N, device=DEV)
+            C_.bn_finalize(stats, gamma, beta, mm, mv, ab_ref, N, float(B * H * H), 1e-3, 1)
+            torch.cuda.synchronize()
+            assert int(ctr.item()) == 0                                   # re-armed by the last block
+            assert torch.allclose(ab_tail, ab_ref, rtol=1e-5, atol=1e-6), (ab_tail - ab_ref).abs().max()
+    finally:
+        C_.set_tune(C_.TUNE_CONV3_WS, 0)
+        C_.set_tune(C_.TUNE_CONV3_SMALL, 0)
