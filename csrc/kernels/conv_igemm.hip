@@ -26,8 +26,14 @@
 namespace {
 
 constexpr int BK = 32;
-constexpr int LDK = BK + 8;   // padded LDS row (bf16 elements)
+constexpr int LDK = BK;       // dense 64-byte LDS rows, XOR-swizzled 16-byte quarters (swz below)
 constexpr int NT = 256;
+
+// bf16 offset of 16-byte quarter q of row r in a dense swizzled [rows][32] tile: quarter q stored at slot
+// q ^ ((r >> 1) & 3). A ds_read_b128 fragment read (16 lanes = 16 consecutive rows, one quarter) then covers all 64
+// banks, and a ds_write_b128 group (8 lanes = 2 rows x 4 quarters) 32 banks. (The previous 80-byte padded rows left
+// 2-4-way conflicts: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 29-43 % on these kernels, profiles/r2_pmc.)
+CFL_DEVICE int swz(int r, int q) { return r * BK + ((q ^ ((r >> 1) & 3)) << 3); }
 
 // Residual join (ConvJoin) of output pixel m, channels c..c+7, given the rounded conv output r (bias included).
 CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv) {
@@ -100,12 +106,12 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   constexpr int B_PER_T = (B_CHUNKS + NT - 1) / NT;
   constexpr int SA = 2 * BM_ * LDK, SB = 2 * BN_ * LDK;  // bf16 elements
   constexpr int LDC = BN_ + 8;
-  static_assert(BM_ * LDC <= SA + SB, "C staging tile must fit in the operand buffers");
+  constexpr int SMEM = SA + SB > BM_ * LDC ? SA + SB : BM_ * LDC;   // the C staging tile reuses the operands
 
-  __shared__ __attribute__((aligned(16))) bf16_t smem[SA + SB];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
   __shared__ float sred[2][NT / 64][BN_];
-  bf16_t (*sA)[BM_][LDK] = reinterpret_cast<bf16_t (*)[BM_][LDK]>(smem);
-  bf16_t (*sB)[BN_][LDK] = reinterpret_cast<bf16_t (*)[BN_][LDK]>(smem + SA);
+  bf16_t* sA = smem;                 // [2][BM_][32] swizzled
+  bf16_t* sB = smem + SA;            // [2][BN_][32] swizzled
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -142,17 +148,15 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   const bool has_ab = p.xf.ab != nullptr;
   const int relu = p.xf.relu;
 
+  // The next K-tile's operands are loaded RAW into registers (ra / rb) and only transformed (producer BN-apply +
+  // ReLU) in store_tiles, after the current tile's MFMAs: nothing consumes the loads early, so they stay in flight
+  // across the MFMAs (a transform right after the load made every K-step wait for its own loads first).
   uint4 ra[A_PER_T], rb[B_PER_T];
+  uint32_t avalid = 0;                 // bit i: A chunk i lies inside the (padded) input
+  int c_ld = 0;                        // channel of the chunks in ra (their BN coefficients)
   auto load_tiles = [&](int kt) {
-    float ca[8], cb[8];
-    if (has_ab) {
-      const float4 a0 = *reinterpret_cast<const float4*>(p.xf.ab + c);
-      const float4 a1 = *reinterpret_cast<const float4*>(p.xf.ab + c + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(p.xf.ab + p.xf.C + c);
-      const float4 b1 = *reinterpret_cast<const float4*>(p.xf.ab + p.xf.C + c + 4);
-      ca[0] = a0.x; ca[1] = a0.y; ca[2] = a0.z; ca[3] = a0.w; ca[4] = a1.x; ca[5] = a1.y; ca[6] = a1.z; ca[7] = a1.w;
-      cb[0] = b0.x; cb[1] = b0.y; cb[2] = b0.z; cb[3] = b0.w; cb[4] = b1.x; cb[5] = b1.y; cb[6] = b1.z; cb[7] = b1.w;
-    }
+    c_ld = c;
+    avalid = 0;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int ih = a_ih[i] + ky, iw = a_iw[i] + kx;
@@ -160,19 +164,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
         const size_t off = ((size_t)a_off[i] + (size_t)(ih >> p.up_in) * p.Win + (iw >> p.up_in)) * p.Cin + c;
         v = *reinterpret_cast<const uint4*>(p.x + off);
-        if (has_ab || relu) {
-          float f[8];
-          unpack8(v, f);
-          if (has_ab) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaf(ca[j], f[j], cb[j]);
-          }
-          if (relu) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-          }
-          v = pack8(f);
-        }
+        avalid |= 1u << i;
       }
       ra[i] = v;
     }
@@ -198,12 +190,29 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   };
 
   auto store_tiles = [&](int buf) {
+    if (has_ab || relu) {
+      float ca[8], cb[8];
+      load_f8_or(p.xf.ab + c_ld, has_ab, 1.f, ca);
+      load_f8_or(p.xf.ab + p.xf.C + c_ld, has_ab, 0.f, cb);
 #pragma unroll
-    for (int i = 0; i < A_PER_T; ++i) *reinterpret_cast<uint4*>(&sA[buf][(tid >> 2) + i * 64][kq * 8]) = ra[i];
+      for (int i = 0; i < A_PER_T; ++i) {
+        float f[8];
+        unpack8(ra[i], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          f[j] = fmaf(ca[j], f[j], cb[j]);
+          if (relu) f[j] = fmaxf(f[j], 0.f);
+        }
+        ra[i] = ((avalid >> i) & 1u) ? pack8(f) : make_uint4(0, 0, 0, 0);   // padding stays exactly 0
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i)
+      *reinterpret_cast<uint4*>(sA + buf * BM_ * LDK + swz((tid >> 2) + i * 64, kq)) = ra[i];
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int ch = tid + i * NT;
-      if (ch < B_CHUNKS) *reinterpret_cast<uint4*>(&sB[buf][ch >> 2][(ch & 3) * 8]) = rb[i];
+      if (ch < B_CHUNKS) *reinterpret_cast<uint4*>(sB + buf * BN_ * LDK + swz(ch >> 2, ch & 3)) = rb[i];
     }
   };
 
@@ -219,16 +228,18 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   }
   __syncthreads();
 
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int fr = lane & 15, fq = lane >> 4;
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) load_tiles(kt + 1);
     s8v af[FM], bfg[FN];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const s8v*>(&sA[cur][wm * TM + i * 16 + fr][fk]);
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const s8v*>(sA + cur * BM_ * LDK + swz(wm * TM + i * 16 + fr, fq));
 #pragma unroll
-    for (int j = 0; j < FN; ++j) bfg[j] = *reinterpret_cast<const s8v*>(&sB[cur][wn * TN + j * 16 + fr][fk]);
+    for (int j = 0; j < FN; ++j)
+      bfg[j] = *reinterpret_cast<const s8v*>(sB + cur * BN_ * LDK + swz(wn * TN + j * 16 + fr, fq));
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
