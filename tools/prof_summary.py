@@ -1,28 +1,42 @@
-"""Summarise a rocprofv3 --kernel-trace --stats run: per-kernel time per training step."""
+"""Summarise a rocprofv3 --kernel-trace run of ``bench.py --profile-steps N``: per-kernel time per STEADY-STATE step.
+
+The trace holds the dataset render kernels, the eager warm-up step that precedes graph capture and N graph replays.
+Steps are delimited by ``zero_spans_kernel`` (the first kernel of every training step); the summary drops everything
+before the second step start (render + eager warm-up) and averages over the remaining graph-replayed steps only:
+kernel time per step by kernel, step wall-clock (zero_spans start to the next one) and the idle share between kernels.
+
+    python tools/prof_summary.py gpurun_out/prof [top]
+"""
+import collections
 import csv
+import os
 import sys
 
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 21.0
-rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
-skip = ("render_kernel",)
-rows = [r for r in rows if not any(s in r["Name"] for s in skip)]
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
-print(f"GPU kernel time per step: {tot / 1e6 / steps:.3f} ms  ({steps:.0f} steps)")
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:22]:
-    t = float(r["TotalDurationNs"])
-    print(f"{t / 1e6 / steps:8.3f} ms/step {100 * t / tot:6.2f}%  calls/step {int(r['Calls']) / steps:6.1f}  "
-          f"avg {float(r['AverageNs']) / 1e3:8.1f} us  {r['Name'][:80]}")
-
-# busy vs wall over the graph-replayed steps (kernel trace): the gap share is launch/dependency overhead
-import os  # noqa: E402
-tp = f"{d}/run_kernel_trace.csv"
-if os.path.exists(tp):
-    tr = [r for r in csv.DictReader(open(tp)) if not any(s in r["Kernel_Name"] for s in skip)]
-    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    n = len(tr)
-    tail = tr[n // 2:]                       # second half: steady-state replays
-    wall = int(tail[-1]["End_Timestamp"]) - int(tail[0]["Start_Timestamp"])
-    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tail)
-    print(f"steady state (last {len(tail)} kernels): wall {wall / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms, "
-          f"idle {100 * (1 - busy / max(wall, 1)):.1f}%  (avg gap {(wall - busy) / 1e3 / max(len(tail) - 1, 1):.2f} us)")
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+path = os.path.join(d, "run_kernel_trace.csv")
+tr = list(csv.DictReader(open(path)))
+tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+starts = [i for i, r in enumerate(tr) if "zero_spans_kernel" in r["Kernel_Name"]]
+if len(starts) < 3:
+    sys.exit(f"{path}: fewer than 3 training steps in the trace")
+steady = tr[starts[1]:]                     # from the first graph replay on (step 0 = eager warm-up)
+nsteps = len(starts) - 1
+bounds = [int(tr[i]["Start_Timestamp"]) for i in starts[1:]] + [int(tr[-1]["End_Timestamp"])]
+walls = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
+per = collections.defaultdict(lambda: [0, 0])
+busy = 0
+for r in steady:
+    t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    per[name][0] += t
+    per[name][1] += 1
+    busy += t
+wall = bounds[-1] - bounds[0]
+print(f"steady state: {nsteps} graph-replayed steps (eager warm-up + dataset render excluded)")
+print(f"step wall-clock {wall / nsteps / 1e3:.1f} us (min {min(walls) / 1e3:.1f}, max {max(walls) / 1e3:.1f}); "
+      f"kernel busy {busy / nsteps / 1e3:.1f} us/step; idle between kernels {100 * (1 - busy / wall):.1f}%; "
+      f"{len(steady) / nsteps:.0f} kernels/step")
+print(f"{'us/step':>9} {'share':>6} {'calls':>6} {'avg us':>8}  kernel")
+for name, (t, n) in sorted(per.items(), key=lambda kv: -kv[1][0])[:top]:
+    print(f"{t / nsteps / 1e3:9.1f} {100 * t / busy:5.1f}% {n / nsteps:6.1f} {t / n / 1e3:8.1f}  {name[:90]}")
