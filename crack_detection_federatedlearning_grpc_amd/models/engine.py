@@ -261,6 +261,12 @@ class UNetEngine:
         # returning atomic) delays every block's retirement - measured 7.5% SLOWER per step than the 15 separate
         # 1-block bn_finalize launches (8,730 -> 8,076 img/s, profiles/README.md)
         self.bn_tail = os.environ.get("CFL_BN_TAIL", "0") == "1"
+        # weight gradients (off the backward critical path: they read forward activations and incoming gradients
+        # that are never overwritten within a step) deferred to the end of backward and issued as ONE batch, the 3x3
+        # halo ones grouped per tile config into shared launches (conv_wgrad_batch) so their latency-bound grids
+        # co-run (CFL_WGRAD_DEFER=0: each issued where it is computed)
+        self.defer_wgrad = os.environ.get("CFL_WGRAD_DEFER", "1") != "0"
+        self._wq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
         # per-step zeroing of gradients / statistics in one launch
         spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10], self.bn_ctr]
@@ -302,8 +308,12 @@ class UNetEngine:
             self._finish_dyn = [e for e in self._finish_dyn if e[1].data_ptr() != dst.data_ptr()]
             self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
             self._finish_dirty = True
-        self.C.conv_wgrad(x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l,
-                          dst_mode, 0, 0, rows)
+        args = (x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l, dst_mode, 0, 0,
+                rows)
+        if self._wq is not None:
+            self._wq.append(args)          # deferred: issued as one batch at the end of backward
+        else:
+            self.C.conv_wgrad(*args)
 
     def _side(self, fn) -> None:
         """Launch ``fn``'s kernels on the weight-gradient stream after everything issued so far on the current
@@ -461,6 +471,21 @@ class UNetEngine:
                    self.metrics if train else self.eval_metrics, B, r[0], DEC_FILTERS[-1], self.dice)
 
     def backward(self) -> None:
+        self._wq = [] if self.defer_wgrad else None
+        try:
+            self._backward()
+        finally:
+            wq, self._wq = self._wq, None
+        if wq:
+            self.C.conv_wgrad_batch(wq)
+        self._join_side()
+        if self._finish_dirty:
+            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("grad_finish table changed during graph capture")
+            self._build_finish()
+        self.C.grad_finish(self.finish_table, self.n_finish, self.finish_work)
+
+    def _backward(self) -> None:
         C, B, r, A, D = self.C, self.B, self.r, self.act, self.dg
         names = self.names
         hl = names[-1]
@@ -582,12 +607,6 @@ class UNetEngine:
                                self.G(names[1], "beta"), B * H * H, cin, self.RS)
                 C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
                               ENTRY_FILTERS, self.C.STAT_REPLICAS)
-        self._join_side()
-        if self._finish_dirty:
-            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("grad_finish table changed during graph capture")
-            self._build_finish()
-        C.grad_finish(self.finish_table, self.n_finish, self.finish_work)
 
     def optimizer_step(self) -> None:
         self._await_all()

@@ -141,9 +141,9 @@ int conv_splits_op(int B, int Ho, int Wo, int N, int ks, int stride, int pad, in
   return conv_igemm_splits(p);
 }
 
-void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win, int Cin,
-                   int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t, int pad_l, int dst_mode,
-                   int m_chunk, int algo, int slabs) {
+WgradParams wgrad_params(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win,
+                         int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t, int pad_l,
+                         int dst_mode, int m_chunk, int algo, int slabs) {
   WgradParams p{};
   p.x = ptr<const bf16_t>(x, "x");
   p.dy = ptr<const bf16_t>(dy, "dy");
@@ -163,7 +163,33 @@ void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu
   TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv_wgrad: x size");
   TORCH_CHECK(dy.numel() == (int64_t)p.M * N, "conv_wgrad: dy size");
   TORCH_CHECK(dw.numel() >= (int64_t)(slabs > 0 ? slabs : 1) * p.K * N, "conv_wgrad: dw size");
+  return p;
+}
+
+void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int Hin, int Win, int Cin,
+                   int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t, int pad_l, int dst_mode,
+                   int m_chunk, int algo, int slabs) {
+  const WgradParams p = wgrad_params(x, dy, dw, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l,
+                                     dst_mode, m_chunk, algo, slabs);
   ok(conv_wgrad(p, stream()), "conv_wgrad");
+}
+
+// calls: a list of conv_wgrad argument tuples (x, dy, dw, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride,
+// pad_t, pad_l, dst_mode, m_chunk, algo, slabs) -> one batch (3x3 halo wgrads grouped into shared launches)
+void conv_wgrad_batch_op(py::list calls) {
+  std::vector<WgradParams> ps;
+  for (auto h : calls) {
+    auto t = h.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 21, "conv_wgrad_batch: each call needs the 21 conv_wgrad arguments");
+    OptT ab = t[3].is_none() ? OptT() : OptT(t[3].cast<at::Tensor>());
+    ps.push_back(wgrad_params(t[0].cast<at::Tensor>(), t[1].cast<at::Tensor>(), t[2].cast<at::Tensor>(), ab,
+                              t[4].cast<int>(), t[5].cast<int>(), t[6].cast<int>(), t[7].cast<int>(),
+                              t[8].cast<int>(), t[9].cast<int>(), t[10].cast<int>(), t[11].cast<int>(),
+                              t[12].cast<int>(), t[13].cast<int>(), t[14].cast<int>(), t[15].cast<int>(),
+                              t[16].cast<int>(), t[17].cast<int>(), t[18].cast<int>(), t[19].cast<int>(),
+                              t[20].cast<int>()));
+  }
+  ok(conv_wgrad_batch(ps.data(), (int)ps.size(), stream()), "conv_wgrad_batch");
 }
 
 // (slab rows, rows are plain-stored (sum without re-zeroing) rather than atomic replicas)
@@ -600,6 +626,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),
         py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("dst_mode"),
         py::arg("m_chunk") = 0, py::arg("algo") = 0, py::arg("slabs") = 0);
+  m.def("conv_wgrad_batch", &conv_wgrad_batch_op, py::arg("calls"));
   m.def("conv_wgrad_slabs", &conv_wgrad_slabs_op, py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"),
         py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"),
         py::arg("pad_t"), py::arg("pad_l"), py::arg("algo") = 0);
@@ -637,6 +664,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_ENTRY_ALGO") = (int)TUNE_ENTRY_ALGO;
   m.attr("TUNE_CONV3_WS") = (int)TUNE_CONV3_WS;
   m.attr("TUNE_CONV3_WS_GRID") = (int)TUNE_CONV3_WS_GRID;
+  m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

@@ -37,7 +37,7 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
 // addresses of the destination layout (c for the Conv2DTranspose (kh,kw,out,in) layout, n for HWIO): each atomic
 // wave-instruction then adds 4 x 64 B segments instead of 64 scattered dwords.
 template <int BNO, bool TR>
-__global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int tiles_total, int splits) {
+CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, int bx, int by, int bz) {
   constexpr int NF = BNO / 16;              // n fragments
   constexpr int COMBOS = 2 * NF;            // (c fragment, n fragment) pairs per tap
   constexpr int CPW = COMBOS / 4;           // combos per wave
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
   __shared__ __attribute__((aligned(16))) bf16_t sD[2][TP][LDD];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cbase = blockIdx.x * CB, nBlock = blockIdx.y * BNO;
+  const int cbase = bx * CB, nBlock = by * BNO;
   const int tiles_w = (p.Wo + TW - 1) / TW, tiles_h = (p.Ho + TH - 1) / TH;
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
   const bool has_ab = p.xf.ab != nullptr;
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
     for (int u = 0; u < CPW; ++u) acc[t][u] = f4v{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
-  int t = blockIdx.z;
+  int t = bz;
   if (t < tiles_total) {
     load(t);
     store(0);
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
   // Slab mode: this split's own row of the slab, plain stores (each element has exactly one writer); otherwise
   // fp32 atomics into the destination.
   const bool slab = p.slabs > 0;
-  float* dwb = slab ? p.dw + (size_t)blockIdx.z * 9 * p.Cin * p.N : p.dw;
+  float* dwb = slab ? p.dw + (size_t)bz * 9 * p.Cin * p.N : p.dw;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
@@ -191,6 +191,34 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int
         else atomicAdd(&dwb[dst], acc[tap][u][r]);
       }
     }
+}
+
+template <int BNO, bool TR>
+__global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int tiles_total, int splits) {
+  wgrad3_body<BNO, TR>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Grouped launch: several independent weight gradients (different layers, same tile config) in ONE grid. Every
+// layer's wgrad is off the backward critical path and, alone, a latency-bound grid of a few hundred blocks; the
+// engine defers them to the end of backward and issues one launch per tile config, so their blocks co-run.
+constexpr int WG_MAX = 8;
+struct Wgrad3Item {
+  WgradParams p;
+  int tiles, splits, gx, gy, block0;
+};
+struct Wgrad3Group {
+  Wgrad3Item it[WG_MAX];
+  int n;
+};
+
+template <int BNO, bool TR>
+__global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_group_kernel(const Wgrad3Group g) {
+  int k = 0;
+  while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
+  const Wgrad3Item& I = g.it[k];
+  const int local = blockIdx.x - I.block0;
+  const int bx = local % I.gx, r = local / I.gx;
+  wgrad3_body<BNO, TR>(I.p, I.tiles, I.splits, bx, r % I.gy, r / I.gy);
 }
 
 }  // namespace
@@ -216,6 +244,47 @@ int conv3x3_wgrad_splits(const WgradParams& p) {
   int bno, tiles, splits;
   wgrad3_shape(p, bno, tiles, splits);
   return splits;
+}
+
+// tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>
+int conv3x3_wgrad_config(const WgradParams& p) {
+  int bno, tiles, splits;
+  wgrad3_shape(p, bno, tiles, splits);
+  return (bno == 64 ? 0 : 2) + (p.dst_mode == 1 ? 0 : 1);
+}
+
+// n problems of ONE tile config (conv3x3_wgrad_config) in grouped launches of up to WG_MAX
+int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += WG_MAX) {
+    Wgrad3Group g{};
+    int blocks = 0, cfg = -1;
+    for (int i = i0; i < n && i < i0 + WG_MAX; ++i) {
+      const WgradParams& p = ps[i];
+      if (!conv3x3_wgrad_supported(p)) return 1;
+      int bno, tiles, splits;
+      wgrad3_shape(p, bno, tiles, splits);
+      if (p.slabs > 0 && p.slabs != splits) return 2;
+      const int c = conv3x3_wgrad_config(p);
+      if (cfg >= 0 && c != cfg) return 4;
+      cfg = c;
+      Wgrad3Item& it = g.it[g.n++];
+      it.p = p;
+      it.tiles = tiles;
+      it.splits = splits;
+      it.gx = p.Cin / CB;
+      it.gy = p.N / bno;
+      it.block0 = blocks;
+      blocks += it.gx * it.gy * splits;
+    }
+    switch (cfg) {
+      case 0: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<64, true>), dim3(blocks), dim3(NT), 0, st, g); break;
+      case 1: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<64, false>), dim3(blocks), dim3(NT), 0, st, g); break;
+      case 2: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<32, true>), dim3(blocks), dim3(NT), 0, st, g); break;
+      default: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<32, false>), dim3(blocks), dim3(NT), 0, st, g); break;
+    }
+    if (hipGetLastError() != hipSuccess) return 3;
+  }
+  return 0;
 }
 
 int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {

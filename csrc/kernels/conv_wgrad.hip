@@ -222,6 +222,32 @@ int conv_wgrad_slabs(const WgradParams& p) {
 
 bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x3_wgrad_supported(p); }
 
+int conv3x3_wgrad_config(const WgradParams& p);
+int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st);
+
+int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
+  WgradParams by_cfg[4][16];
+  int cnt[4] = {0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    const WgradParams& p = ps[i];
+    if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
+    if (p.algo != 1 && conv3x3_wgrad_supported(p) && cfl_tune(TUNE_WGRAD_GROUP) != 1) {
+      const int c = conv3x3_wgrad_config(p);
+      if (cnt[c] == 16) return 5;
+      by_cfg[c][cnt[c]++] = p;
+    } else {
+      const int rc = conv_wgrad(p, st);
+      if (rc) return rc;
+    }
+  }
+  for (int c = 0; c < 4; ++c)
+    if (cnt[c]) {
+      const int rc = conv3x3_wgrad_grouped(by_cfg[c], cnt[c], st);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
 int conv_wgrad(const WgradParams& p, hipStream_t st) {
   if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
   if (p.algo != 1 && conv3x3_wgrad_supported(p)) return conv3x3_wgrad(p, st);

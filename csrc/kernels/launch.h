@@ -105,6 +105,9 @@ struct WgradParams {
                        //    (halo kernel: one plain-stored row per pixel split; generic: atomic replica rows)
 };
 int conv_wgrad(const WgradParams& p, hipStream_t st);
+// several independent weight gradients: the 3x3 halo ones grouped by tile config into shared launches
+// (conv3x3_wgrad.hip conv3x3_wgrad_group_kernel), the rest launched one by one
+int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st);
 int conv_wgrad_slabs(const WgradParams& p);
 bool conv_wgrad_plain_slabs(const WgradParams& p);   // slab rows are plain-stored (else atomic replica rows)
 #define WGRAD_REPLICAS 16
@@ -309,7 +312,8 @@ enum TuneKey {
   TUNE_HEAD_BLOCKS = 13,       // head fwd / bwd grid cap (default 512)
   TUNE_CONV3_WS = 14,          // conv3x3 Cin <= 64: 0 = weight-stationary persistent kernel, 1 = per-tile kernel
   TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
-  TUNE_N = 16
+  TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every 3x3 wgrad on its own (no grouping)
+  TUNE_N = 20
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -1077,3 +1077,29 @@ def test_training_parity_vs_plain_fp32():
     assert abs(me["iou"] - iou_ref) < 0.1
     for k, v in cos_eng.items():                                            # gradient fidelity >= bf16 autocast's
         assert v >= min(0.85, cos_ac[k] - 0.05), (k, v, cos_ac[k])
+
+
+def test_conv_wgrad_batch_grouped_equals_individual():
+    """conv_wgrad_batch (the engine's deferred weight gradients): 3x3 halo wgrads of different layers grouped into
+    shared launches per tile config, plus a 1x1 one launched alone, give bit-identical slabs to one call each."""
+    torch.manual_seed(41)
+    C_ = hip()
+    shapes = [  # (B, Hin, Cin, up, Ho, N, ks, dst_mode)
+        (2, 16, 64, 0, 16, 32, 3, 1), (2, 8, 64, 1, 16, 32, 3, 1), (2, 16, 32, 0, 16, 64, 3, 1),
+        (2, 16, 64, 0, 16, 64, 3, 1), (2, 16, 32, 0, 16, 64, 1, 0), (3, 8, 32, 0, 8, 32, 3, 0)]
+    calls = []
+    for B, Hin, Cin, up, Ho, N, ks, dm in shapes:
+        x, _ = bf(torch.randn(B, Hin, Hin, Cin))
+        dy, _ = bf(torch.randn(B, Ho, Ho, N))
+        ab = ab_for(Cin, 42)[0].to(DEV)
+        pad = 1 if ks == 3 else 0
+        rows, _plain = C_.conv_wgrad_slabs(B, Hin, Hin, Cin, up, Ho, Ho, N, ks, 1, pad, pad)
+        slab = torch.zeros(rows * ks * ks * Cin * N, device=DEV)
+        calls.append((x, dy, slab, ab, 1, B, Hin, Hin, Cin, up, Ho, Ho, N, ks, 1, pad, pad, dm, 0, 0, rows))
+    C_.conv_wgrad_batch(calls)
+    batched = [c[2].clone() for c in calls]
+    for c in calls:
+        c[2].zero_()
+        C_.conv_wgrad(*c)
+    for a, c in zip(batched, calls):
+        assert torch.equal(a, c[2])
