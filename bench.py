@@ -35,7 +35,8 @@ def main() -> int:
                     help="per-client batch (reference: 16; 0 = HBM planner, models/memplan.py)")
     ap.add_argument("--hbm-fraction", type=float, default=0.85, help="HBM share the batch planner may fill")
     ap.add_argument("--epochs", type=int, default=10, help="local epochs per FL round (client_fit_model.py:166)")
-    ap.add_argument("--local-steps", type=int, default=388, help="iterations per epoch (reference: 6213 // 16)")
+    ap.add_argument("--local-steps", type=int, default=0,
+                    help="iterations per epoch (0: the reference's Sequence length, 6213 // batch = 388 at batch 16)")
     ap.add_argument("--val-steps", type=int, default=-1,
                     help="validation batches per epoch (-1: the whole held-out split, as Keras fit(validation_data))")
     ap.add_argument("--samples", type=int, default=8000, help="synthetic images per client")
@@ -90,9 +91,12 @@ def main() -> int:
         from crack_detection_federatedlearning_grpc_amd.models.memplan import plan_batch
         plan = plan_batch(args.img, None, args.hbm_fraction, args.samples)
         args.batch = plan.batch
-        if args.local_steps == 388:                        # reference epoch = 6213 // batch iterations
-            args.local_steps = max(1, min(6213, args.samples) // args.batch)
+    if args.local_steps <= 0:                              # reference epoch = 6213 // batch iterations
+        args.local_steps = max(1, min(6213, args.samples) // args.batch)
     # reference split: the first 6213 of the ~8k images train, the rest validate (kept in proportion for small sets)
+    if rank == 0:
+        print(f"[bench] rendering {args.samples} synthetic {args.img}^2 images on the device", file=sys.stderr,
+              flush=True)
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank,
                                  split=min(6213, max(args.batch, int(args.samples * 0.7766))))
     eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
@@ -146,16 +150,27 @@ def main() -> int:
         else:
             eng.pack()
 
-    for _ in range(args.warmup):
+    def note(msg: str) -> None:                           # progress on stderr (the JSON result stays on stdout)
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    note(f"engine ready: batch {args.batch} @ {args.img}^2, {args.epochs} x {args.local_steps} steps per round, "
+         f"{val_steps} validation batches per epoch")
+    for w in range(args.warmup):
+        tw = time.perf_counter()
         fl_round()
+        torch.cuda.synchronize()
+        note(f"warm-up round {w + 1}/{args.warmup}: {time.perf_counter() - tw:.2f} s")
     eng.read_metrics("train")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         fl_round()
+        if args.steps > 1 and args.img >= 512:
+            note(f"timed round {i + 1}/{args.steps} issued")  # (no sync: timing unaffected)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -7,9 +7,12 @@ packed weights, BN statistics, weight-gradient slabs) or small (the split-K work
 low-M layers use and which shrinks as the batch grows).
 
 ``plan_batch`` picks the largest per-client batch whose footprint (engine + the client's resident uint8 dataset
-shard) fits a fraction of HBM, subject to the kernels' 32-bit pixel indexing (every tensor <= 2^30 elements, half
-the int32 range). The reference trains at a fixed batch 16 (client_fit_model.py:56); the planner is the MI355X-side
-answer to SURVEY.md §7.5 item 6.
+shard) fits a fraction of HBM. Index widths: every kernel forms ELEMENT offsets in 64 bits (``(size_t)pixel * C``;
+audited over csrc/kernels for round 2), and keeps 32-bit only the pixel index (B*H*W) and the elementwise kernels'
+work-item counters (pixels x channel groups of >= 4 channels, plus one grid stride) - so the index bound is
+numel / 4 < 2^31 - 2^24 per tensor, which at 512^2 allows batches up to 2,040: HBM, not the index width, bounds
+the 512^2 plan (58 GB at the old 2^30-element bound). The reference trains at a fixed batch 16
+(client_fit_model.py:56); the planner is the MI355X-side answer to SURVEY.md §7.5 item 6.
 """
 from __future__ import annotations
 
@@ -19,8 +22,9 @@ from typing import Dict, Optional, Tuple
 from .spec import DEC_FILTERS, ENC_FILTERS, ENTRY_FILTERS
 
 BF16, U8, F32 = 2, 1, 4
-MAX_ELEMS = 2**30              # kernels index pixels (B*H*W) and grid-stride counters in 32 bits: keep every
-                               # tensor at half the int32 range
+MAX_ITEMS = 2**31 - 2**24      # 32-bit work-item counters (>= 4 channels per item) plus one grid stride
+ITEM_CHANNELS = 4
+MAX_ELEMS = MAX_ITEMS * ITEM_CHANNELS   # largest tensor (elements) the kernels index; element offsets are 64-bit
 
 
 def _qres(k: int, Rk: int) -> int:
@@ -117,7 +121,7 @@ class Plan:
     engine_bytes: int
     dataset_bytes: int
     budget_bytes: int
-    limit: str                       # "hbm" | "int32-index" | "max_batch"
+    limit: str                       # "hbm" | "index" (32-bit work-item counters) | "max_batch"
 
     @property
     def total_bytes(self) -> int:
@@ -150,7 +154,7 @@ def plan_batch(img: int, hbm_bytes: Optional[int] = None, fraction: float = 0.85
     b_hbm = avail // per
     b_idx = MAX_ELEMS // largest_tensor_elems(1, img)
     b = min(b_hbm, b_idx, max_batch)
-    limit = "hbm" if b == b_hbm else ("int32-index" if b == b_idx else "max_batch")
+    limit = "hbm" if b == b_hbm else ("index" if b == b_idx else "max_batch")
     if b >= multiple:
         b -= b % multiple
     return Plan(int(b), img, engine_bytes(int(b), img), data, budget, limit)

@@ -26,7 +26,16 @@ def test_plan_respects_hbm_and_index_limits(S):
     assert p.batch % 8 == 0 and p.batch > 16
     assert p.total_bytes <= p.budget_bytes
     assert M.largest_tensor_elems(p.batch, S) <= M.MAX_ELEMS
-    assert p.limit in ("hbm", "int32-index", "max_batch")
+    assert p.limit in ("hbm", "index", "max_batch")
+
+
+def test_512_plan_is_hbm_bound_on_mi355x():
+    """With 64-bit element offsets the 512^2 plan on a 288 GB MI355X is bounded by HBM (batch ~1000), not by the
+    kernels' index width (the old 2^30-element bound stopped at batch 256 / 58 GB)."""
+    p = M.plan_batch(512, 288 * 10**9, 0.85, samples=8000)
+    assert p.limit == "hbm" and p.batch >= 512, p.as_dict()
+    assert M.largest_tensor_elems(p.batch, 512) > 2**30               # past the old bound
+    assert M.largest_tensor_elems(p.batch, 512) <= M.MAX_ELEMS
 
 
 def test_plan_hbm_bound_when_small():
