@@ -52,6 +52,10 @@ def main() -> int:
                     help="also run the FL product path (FLServer + one FLClient per rank over real gRPC, HIP engine, "
                          "RCCL data plane for N>1) for warmup+steps rounds and print a SECOND JSON line: wall-clock "
                          "per round from server release to next release, vs the engine-only round above")
+    ap.add_argument("--fedavg-1rank", action="store_true",
+                    help="N=1 only: run the overlapped FedAvg path anyway over a 1-rank RCCL group (bucketed "
+                         "all-reduce + per-bucket repack on the side stream, first step of the next round waiting "
+                         "per layer) - for kernel traces of the overlap (tools/overlap_summary.py)")
     ap.add_argument("--verify-fedavg", action="store_true",
                     help="after the timed rounds, check one weighted FedAvg against an all-gathered reference")
     args = ap.parse_args()
@@ -69,6 +73,12 @@ def main() -> int:
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(local % ndev)               # local % ndev: a gloo rehearsal may share one GPU
     dev = torch.device("cuda", local % ndev)
+    if world == 1 and args.fedavg_1rank:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            fport = so.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{fport}", rank=0, world_size=1, device_id=dev)
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -102,7 +112,7 @@ def main() -> int:
     eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
-    agg = FedAvgAllReduce(eng.flat, table, world) if world > 1 else None
+    agg = FedAvgAllReduce(eng.flat, table, world) if world > 1 or args.fedavg_1rank else None
     n_local = len(data.train_idx)
     batches = torch.as_tensor(epoch_batches(data.train_idx, args.batch, args.local_steps, seed=rank),
                               dtype=torch.int32, device=dev)
@@ -231,7 +241,7 @@ def main() -> int:
         fl_line = run_fl_bench(args, world, rank, round_s)
         if rank == 0:
             print(json.dumps(fl_line), flush=True)
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

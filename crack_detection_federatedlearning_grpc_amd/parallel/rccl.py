@@ -81,7 +81,10 @@ class FedAvgAllReduce:
             return []
         w = self._weight(n_local, weighted)
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.flat.device)
+            # high priority: HIP gives it its own hardware queue (a default-priority stream may be multiplexed onto
+            # the compute stream's queue - GPU_MAX_HW_QUEUES=4 - and then cannot overlap it; measured with
+            # tools/overlap_summary.py), and the per-bucket repack that gates the next round's layers goes first
+            self._side = torch.cuda.Stream(device=self.flat.device, priority=-1)
         out = []
         for sl in self.buckets:
             b = self.flat[sl]
