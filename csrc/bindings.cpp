@@ -665,6 +665,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_CONV3_WS") = (int)TUNE_CONV3_WS;
   m.attr("TUNE_CONV3_WS_GRID") = (int)TUNE_CONV3_WS_GRID;
   m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
+  m.attr("TUNE_CONV3_DEEP") = (int)TUNE_CONV3_DEEP;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

@@ -633,7 +633,11 @@ static bool small_tiles(const ConvParams& p) {
   return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
 }
 
-int conv3x3_splits(const ConvParams& p) { return small_tiles(p) || ws_eligible(p) ? 1 : conv3x3_split_k(p); }
+bool conv3x3_deep_eligible(const ConvParams& p);
+int conv3x3_splits(const ConvParams& p) {
+  return small_tiles(p) || ws_eligible(p) || (conv3x3_deep_eligible(p) && p.fin.gamma == nullptr)
+             ? 1 : conv3x3_split_k(p);
+}
 
 // K splits of the 8x16 / 16x8-pixel tiles (the fp8 kernel has no small-tile variant and always uses this)
 int conv3x3_split_k(const ConvParams& p) {
@@ -654,8 +658,13 @@ bool conv3x3_supported(const ConvParams& p) {
          p.Wo >= 8 && p.Ho >= 8 && (p.N % 128 == 0 || p.N == 64 || p.N == 32);
 }
 
+bool conv3x3_deep_eligible(const ConvParams& p);
+int conv3x3_deep(const ConvParams& p, hipStream_t st);
+
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
+  // LDS-DMA ring, no split-K (it has no in-launch BN-finalize tail: a BnFinal request keeps the other kernels)
+  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr) return conv3x3_deep(p, st);
   if (ws_eligible(p)) {                     // weight-stationary persistent tiles (no split-K)
     const bool w16 = p.Wo >= 16;
     if (p.Cin == 32) {

@@ -313,6 +313,7 @@ enum TuneKey {
   TUNE_CONV3_WS = 14,          // conv3x3 Cin <= 64: 0 = weight-stationary persistent kernel, 1 = per-tile kernel
   TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
   TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every 3x3 wgrad on its own (no grouping)
+  TUNE_CONV3_DEEP = 17,        // conv3x3 Cin >= 128: 0 = LDS-DMA 3-stage deep-K kernel, 1 = off, 2 = force (any Cin)
   TUNE_N = 20
 };
 int cfl_tune(int key);

@@ -378,7 +378,16 @@ def test_conv_igemm_big_m_tiles(N):
 
 
 def test_conv_igemm_split_k_with_stats():
-    """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue."""
+    """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue (the LDS-DMA deep-K kernel, which
+    takes such shapes by default, is switched off here)."""
+    hip().set_tune(hip().TUNE_CONV3_DEEP, 1)
+    try:
+        _split_k_with_stats()
+    finally:
+        hip().set_tune(hip().TUNE_CONV3_DEEP, 0)
+
+
+def _split_k_with_stats():
     torch.manual_seed(9)
     B, H, Cin, N = 4, 8, 256, 256
     assert hip().conv_splits(B, H, H, N, 3, 1, 1, Cin) > 1
@@ -787,7 +796,38 @@ def test_conv3x3_weight_stationary_forced(B, Hs, Cin, N, up, use_ab, grid):
         C_.set_tune(C_.TUNE_CONV3_WS_GRID, 0)
 
 
-def test_conv3x3_weight_stationary_node_epilogue():
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [
+    (2, 16, 128, 64, 0, True),       # 4 chunks: the 3-stage LDS-DMA ring wraps
+    (4, 8, 256, 256, 0, True),       # the 16x16-level shape family (8 chunks, 8 column blocks)
+    (2, 8, 128, 32, 1, False),       # upsampled input, ReLU-only producer transform
+    (2, 8, 64, 32, 0, True),         # 2 chunks (shorter than the ring)
+    (3, 8, 32, 64, 0, False),        # 1 chunk
+])
+def test_conv3x3_deep_dma_forced(B, Hs, Cin, N, up, use_ab):
+    """TUNE_CONV3_DEEP=2 forces the LDS-DMA deep-K kernel (conv3x3_deep.hip: global_load_lds into a 3-stage ring,
+    swizzle via source addresses, in-place producer transform) on every shape it accepts; output and BN statistics
+    vs the generic implicit GEMM and the fp32 reference."""
+    C_ = hip()
+    C_.set_tune(C_.TUNE_CONV3_DEEP, 2)
+    C_.set_tune(C_.TUNE_CONV3_WS, 1)
+    try:
+        test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
+    finally:
+        C_.set_tune(C_.TUNE_CONV3_DEEP, 0)
+        C_.set_tune(C_.TUNE_CONV3_WS, 0)
+
+
+@pytest.mark.parametrize("deep", [False, True])
+def test_conv3x3_weight_stationary_node_epilogue(deep):
+    if deep:
+        hip().set_tune(hip().TUNE_CONV3_DEEP, 2)
+    try:
+        _node_epilogue_ws_vs_tile()
+    finally:
+        hip().set_tune(hip().TUNE_CONV3_DEEP, 0)
+
+
+def _node_epilogue_ws_vs_tile():
     """The BN-node gradient epilogue (dgrad producer) on the weight-stationary kernel == the per-tile kernel."""
     torch.manual_seed(23)
     C_ = hip()
@@ -976,6 +1016,7 @@ def test_in_launch_bn_finalize_matches_bn_finalize(ks, H, Cin, N, B, tune):
         C_.set_tune(C_.TUNE_CONV3_WS, 2)
     if tune == "split":
         C_.set_tune(C_.TUNE_CONV3_SMALL, 1)
+        C_.set_tune(C_.TUNE_CONV3_DEEP, 1)
     try:
         for _ in range(2):
             y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
@@ -993,6 +1034,7 @@ def test_in_launch_bn_finalize_matches_bn_finalize(ks, H, Cin, N, B, tune):
     finally:
         C_.set_tune(C_.TUNE_CONV3_WS, 0)
         C_.set_tune(C_.TUNE_CONV3_SMALL, 0)
+        C_.set_tune(C_.TUNE_CONV3_DEEP, 0)
 
 
 def _first_layer_cos(g_a, g_b, table, names=("conv2d", "separable_conv2d", "conv2d_transpose_7", "conv2d_8")):
