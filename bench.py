@@ -130,7 +130,12 @@ def main() -> int:
     # the reference's 16-image validation batches, evaluated 3-8 at a time by an inference engine sharing the
     # weights (per-pixel means are batching-invariant: models/engine.py UNetEngine.evaluator)
     vimg = epoch_batches(data.val_idx, args.batch, 0, 0)[:val_steps].reshape(-1) if val_steps else None
-    ev = eng.evaluator(eng.eval_batch_for(len(vimg))) if val_steps else None
+    # CFL_OVERLAP_VAL=1: each epoch's validation pass runs on its own stream (parameter snapshot) while the next
+    # epoch trains (UNetEngine.overlapped_validation)
+    overlap_val = os.environ.get("CFL_OVERLAP_VAL", "0") == "1" and use_graph
+    ev = eng.evaluator(eng.eval_batch_for(len(vimg)), snapshot=overlap_val) if val_steps else None
+    ev_stream = torch.cuda.Stream(device=dev, priority=int(os.environ.get("CFL_VAL_PRIORITY", "0"))) \
+        if overlap_val else None
     vbatches = torch.as_tensor(vimg.reshape(-1, ev.B), dtype=torch.int32, device=dev) if val_steps else None
 
     if args.profile_eval_steps and val_steps:
@@ -150,9 +155,14 @@ def main() -> int:
                     eng.idx.copy_(batches[s])
                     eng.train_step(use_graph)
             with phase("bench/validate"):
-                for v in range(vbatches.shape[0] if val_steps else 0):
-                    ev.idx.copy_(vbatches[v])
-                    ev.eval_step(use_graph)
+                if overlap_val and val_steps:
+                    eng.overlapped_validation(ev, vbatches, ev_stream, use_graph)
+                else:
+                    for v in range(vbatches.shape[0] if val_steps else 0):
+                        ev.idx.copy_(vbatches[v])
+                        ev.eval_step(use_graph)
+        if ev_stream is not None:
+            torch.cuda.current_stream(dev).wait_stream(ev_stream)   # the round's last validation pass
         if agg is not None:
             # weighted FedAvg over RCCL/xGMI, bucketed in layer order on a side stream; each bucket's layers are
             # repacked to bf16 there and the next round waits per bucket (engine.defer_until)

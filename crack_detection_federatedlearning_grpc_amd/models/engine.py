@@ -754,22 +754,50 @@ class UNetEngine:
             out["dice"] = 2.0 * tp / (pp + t) if pp + t > 0 else 1.0
         return out
 
-    def evaluator(self, batch: int) -> "UNetEngine":
+    def evaluator(self, batch: int, snapshot: bool = False) -> "UNetEngine":
         """An inference-only engine of batch ``batch`` over THIS engine's parameters, packed weights and dataset.
         Validation loss / accuracy are per-pixel means over the whole held-out split (head.hip sums, normalised by
         the pixel count), so evaluating the same images in larger batches gives the same numbers - and larger
         batches fill the GPU (the 16-image eval forward is launch/latency-bound). Not used for the fp8 path (its
-        activation scales are calibrated per engine) or with the per-batch Dice term."""
-        if batch == self.B or self.fp8 or self.dice:
+        activation scales are calibrated per engine) or with the per-batch Dice term.
+
+        ``snapshot``: the evaluator reads its OWN copy of the fp32 parameters and packed weights (``ParamSnapshot``,
+        refreshed from this engine by ``snap.refresh()``), so a validation pass can run on another stream while the
+        next epoch trains (``overlapped_validation``)."""
+        if (batch == self.B and not snapshot) or self.fp8 or self.dice:
             return self
-        ev = self._evaluators.get(batch)
+        key = (batch, snapshot)
+        ev = self._evaluators.get(key)
         if ev is None:
+            share = ParamSnapshot(self) if snapshot else self
             ev = UNetEngine(self.table, batch, self.S, self.dev, "bce", self.lr, self.b1, self.b2, self.adam_eps,
-                            self.momentum, self.bn_eps, share=self)
+                            self.momentum, self.bn_eps, share=share)
+            ev.snap = share if snapshot else None
             if self.images is not None:
                 ev.bind_data(self.images, self.masks)
-            self._evaluators[batch] = ev
+            self._evaluators[key] = ev
         return ev
+
+    def overlapped_validation(self, ev: "UNetEngine", batches: torch.Tensor, stream: torch.cuda.Stream,
+                              use_graph: bool = True) -> torch.cuda.Event:
+        """Validation of the CURRENT parameters on ``stream``, concurrent with whatever the caller issues next on
+        the current (training) stream: the snapshot evaluator ``ev`` copies the parameters first (the training
+        stream waits only for that 12 MB copy), then replays its inference graph over ``batches`` [n, ev.B].
+        Keras semantics hold: the pass sees exactly the epoch-end weights. Returns the event marking the pass's
+        end (join it before reading ``ev.eval_metrics``)."""
+        main = torch.cuda.current_stream(self.dev)
+        stream.wait_stream(main)
+        with torch.cuda.stream(stream):
+            ev.snap.refresh()
+            copied = torch.cuda.Event()
+            copied.record(stream)
+            for v in range(batches.shape[0]):
+                ev.idx.copy_(batches[v])
+                ev.eval_step(use_graph)
+            done = torch.cuda.Event()
+            done.record(stream)
+        main.wait_event(copied)                 # training may overwrite the parameters once they are copied
+        return done
 
     def eval_batch_for(self, n_images: int, cap: int = 128) -> int:
         """Largest eval batch <= cap that is a multiple of B and divides ``n_images`` (a whole number of the
@@ -786,6 +814,25 @@ class UNetEngine:
         self.forward(False)
         p = torch.sigmoid(self.h)
         return p.repeat_interleave(2, 1).repeat_interleave(2, 2)
+
+
+class ParamSnapshot:
+    """The parameter-side view an inference engine shares (``UNetEngine(share=...)``): private copies of a training
+    engine's fp32 flat buffer and bf16 packed weights, refreshed on demand (the evaluator's BN tables point at these
+    copies, so the training engine may keep updating its own while a validation pass runs)."""
+
+    def __init__(self, parent: "UNetEngine"):
+        self.parent = parent
+        self.flat = parent.flat.clone()
+        self.packed = parent.packed.clone()
+
+    def refresh(self) -> None:
+        self.parent._await_all()
+        self.flat.copy_(self.parent.flat)
+        self.packed.copy_(self.parent.packed)
+
+    def _await_all(self) -> None:
+        pass
 
 
 class HipBackend:

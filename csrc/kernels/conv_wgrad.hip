@@ -30,7 +30,11 @@ template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
   constexpr int TK = BKO / 2, TN = BNO / 2;
   constexpr int FK = TK / 16, FN = TN / 16;
-  constexpr int LDX = BKO + 8, LDG = BNO + 8;
+  // LDS rows of 96 / 160 / 288 bytes (32 x odd): the 32 lanes of each ds_read_b64_tr_b16 read 8 CONSECUTIVE pixel
+  // rows x 32 bytes (k-slot order below), which then cover all 64 banks. The previous 80-144-byte rows with rows
+  // {8g+q, 8g+q+4} per lane group left 2-way conflicts: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 33-40 %
+  // (profiles/r2_step1/pmc_summary.txt) - the same fix conv3x3_wgrad.hip got in round 1.
+  constexpr int LDX = BKO + 16, LDG = BNO + 16;
   constexpr int XC = RM * BKO / 8, GC = RM * BNO / 8;   // 16-byte chunks per tile
   constexpr int XPT = (XC + NT - 1) / NT, GPT = (GC + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) bf16_t sX[2][RM][LDX];
@@ -142,20 +146,22 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
     if (more) load(m0 + RM);
 #pragma unroll
     for (int ks = 0; ks < RM / 32; ++ks) {
-      const int r0 = 32 * ks + 8 * g + q;
+      // this lane's pixel rows: r0 (elements 0-3) and r0 + 16 (elements 4-7); the same pixel -> k-slot permutation
+      // on both operands, so the reduction is unchanged
+      const int r0 = 32 * ks + 4 * g + q;
       s8v af[FK], bfg[FN];
 #pragma unroll
       for (int i = 0; i < FK; ++i) {
         const int kc = wk * TK + i * 16 + 4 * pq;
         const s4v lo = tr_read(&sX[buf][r0][kc]);
-        const s4v hi = tr_read(&sX[buf][r0 + 4][kc]);
+        const s4v hi = tr_read(&sX[buf][r0 + 16][kc]);
         af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int nc = wn * TN + j * 16 + 4 * pq;
         const s4v lo = tr_read(&sG[buf][r0][nc]);
-        const s4v hi = tr_read(&sG[buf][r0 + 4][nc]);
+        const s4v hi = tr_read(&sG[buf][r0 + 16][nc]);
         bfg[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll

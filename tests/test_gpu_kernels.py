@@ -1145,3 +1145,27 @@ def test_conv_wgrad_batch_grouped_equals_individual():
         C_.conv_wgrad(*c)
     for a, c in zip(batched, calls):
         assert torch.equal(a, c[2])
+
+
+def test_overlapped_validation_matches_sequential():
+    """UNetEngine.overlapped_validation: a validation pass on its own stream over a parameter snapshot, with the next
+    training step issued right behind it on the training stream, gives exactly the metrics of the sequential pass
+    (the training step cannot leak into the snapshot)."""
+    table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=8)
+    eng.train_step(use_graph=False)
+    vb = torch.arange(8, dtype=torch.int32, device=DEV).view(2, 4)
+    ev_seq = eng.evaluator(4)
+    ev_seq.eval_metrics.zero_()
+    for v in range(2):
+        ev_seq.idx.copy_(vb[v])
+        ev_seq.eval_step(use_graph=False)
+    m_seq = ev_seq.read_metrics("eval")
+    ev = eng.evaluator(4, snapshot=True)
+    ev.eval_metrics.zero_()
+    st = torch.cuda.Stream(device=DEV)
+    done = eng.overlapped_validation(ev, vb, st, use_graph=True)
+    for _ in range(3):
+        eng.train_step(use_graph=False)                      # modifies eng.flat / packed while the pass runs
+    torch.cuda.current_stream().wait_event(done)
+    m_ov = ev.read_metrics("eval")
+    assert m_ov == m_seq, (m_ov, m_seq)

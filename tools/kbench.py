@@ -34,7 +34,11 @@ class Recorder:
             return f
 
         def wrap(*a, **k):
-            self.calls.append((name, a, k))
+            if name == "conv_wgrad_batch":       # the engine's deferred weight gradients: time each one alone
+                for c in a[0]:
+                    self.calls.append(("conv_wgrad", tuple(c), {}))
+            else:
+                self.calls.append((name, a, k))
             return f(*a, **k)
         return wrap
 
