@@ -35,7 +35,7 @@ def make_dataset(cfg: FLConfig, rank: int = 0, device: str = "cpu") -> CrackData
     if cfg.data == "folder":
         from ..data.folder import load_folder_dataset
         return load_folder_dataset(cfg.train_image_dir, cfg.train_mask_dir, cfg.img_size, cfg.val_samples,
-                                   cfg.shuffle_seed)
+                                   cfg.shuffle_seed, device=device)
     seed = cfg.data_seed * 7919 + rank
     if device == "cuda":
         from ..data.device import make_synthetic_device

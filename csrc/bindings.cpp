@@ -557,6 +557,18 @@ void pack_fp8_op(at::Tensor flat, at::Tensor packed8, at::Tensor scales, at::Ten
      "pack_fp8");
 }
 
+// src: uint8 device bytes of n decoded images back to back; offs: int64 [n] byte offsets; dims: int32 [n, 2] (h, w);
+// dst: uint8 [n, dh, dw, c] or [n, dh, dw] (c = 1)
+void resize_batch_op(at::Tensor src, at::Tensor offs, at::Tensor dims, at::Tensor dst, int binarize) {
+  TORCH_CHECK(src.scalar_type() == at::kByte && dst.scalar_type() == at::kByte, "resize_batch: uint8 tensors");
+  TORCH_CHECK(offs.scalar_type() == at::kLong && dims.scalar_type() == at::kInt, "resize_batch: offs int64, dims int32");
+  const int n = (int)offs.numel();
+  TORCH_CHECK(dims.numel() == 2 * n && dst.dim() >= 3 && dst.size(0) == n, "resize_batch: shapes");
+  const int dh = (int)dst.size(1), dw = (int)dst.size(2), c = dst.dim() == 4 ? (int)dst.size(3) : 1;
+  ok(resize_batch(ptr<const uint8_t>(src, "src"), ptr<const int64_t>(offs, "offs"), ptr<const int>(dims, "dims"),
+                  ptr<uint8_t>(dst, "dst"), n, dh, dw, c, binarize, stream()), "resize_batch");
+}
+
 void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor amax, OptT bias, at::Tensor y,
                     OptT stats, OptT ab, int relu, int B, int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N,
                     OptT ws, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
@@ -696,5 +708,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
         py::arg("max_elems"), py::arg("step") = py::none());
   m.def("render_cracks", &render_cracks_op);
+  m.def("resize_batch", &resize_batch_op, py::arg("src"), py::arg("offs"), py::arg("dims"), py::arg("dst"),
+        py::arg("binarize") = 0);
   m.def("gather_rows_u8", &gather_rows_u8_op);
 }

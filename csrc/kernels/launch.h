@@ -325,6 +325,10 @@ int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int row
                    hipStream_t st);
 int render_cracks(const float* segs, const float* params, uint8_t* images, uint8_t* masks, int n, int img,
                   int max_seg, hipStream_t st);
+// n decoded images (src bytes at offs[i], dims[i] = {h, w}, c channels) bilinearly resized into dst [n, dh, dw, c]
+// (binarize: masks -> {0, 1}); datagen.hip
+int resize_batch(const uint8_t* src, const int64_t* offs, const int* dims, uint8_t* dst, int n, int dh, int dw, int c,
+                 int binarize, hipStream_t st);
 
 // Tail of a statistics producer (see BnFinal). EVERY thread of EVERY block of the launch calls it after issuing its
 // block's statistics atomics into stats[STAT_REPLICAS][2][C] (C <= 256, blockDim.x <= 256); `nblocks` = the

@@ -1169,3 +1169,28 @@ def test_overlapped_validation_matches_sequential():
     torch.cuda.current_stream().wait_event(done)
     m_ov = ev.read_metrics("eval")
     assert m_ov == m_seq, (m_ov, m_seq)
+
+
+def test_folder_dataset_device_resize_matches_host(tmp_path):
+    """Folder data path (client_fit_model.py:34-40): images / masks decoded on the host and resized + binarised by
+    the HIP batch kernel (datagen.hip resize_batch) match the host resize (_native.resize_bilinear): bit-exact when
+    down-scaling, at most 1 LSB on < 1 % of the values when up-scaling (float rounding of the host build); the split
+    semantics are the same."""
+    from PIL import Image
+    from crack_detection_federatedlearning_grpc_amd.data.folder import load_folder_dataset
+    rng = np.random.default_rng(3)
+    (tmp_path / "img").mkdir()
+    (tmp_path / "mask").mkdir()
+    for i, (h, w) in enumerate([(227, 227), (100, 140), (64, 64), (300, 180), (50, 77), (128, 128)]):
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(tmp_path / "img" / f"{i:03d}.jpg")
+        m = (rng.random((h, w)) > 0.9).astype(np.uint8) * 255
+        Image.fromarray(m).save(tmp_path / "mask" / f"{i:03d}.jpg")
+    host = load_folder_dataset(str(tmp_path / "img"), str(tmp_path / "mask"), 96, split=4)
+    dev = load_folder_dataset(str(tmp_path / "img"), str(tmp_path / "mask"), 96, split=4, device="cuda")
+    assert isinstance(dev.images, torch.Tensor) and dev.images.is_cuda and tuple(dev.images.shape) == (6, 96, 96, 3)
+    di = np.abs(dev.images.cpu().numpy().astype(int) - host.images.astype(int))
+    assert di.max() <= 1 and (di > 0).mean() < 0.01, (di.max(), (di > 0).mean())
+    assert np.array_equal(dev.images.cpu().numpy()[0], host.images[0]) or di[0].max() <= 1
+    dm = dev.masks.cpu().numpy() != host.masks
+    assert dm.mean() < 0.01 and set(np.unique(dev.masks.cpu().numpy())) <= {0, 1}
+    assert np.array_equal(dev.train_idx, host.train_idx) and np.array_equal(dev.val_idx, host.val_idx)
