@@ -58,6 +58,9 @@ def main() -> int:
                          "per layer) - for kernel traces of the overlap (tools/overlap_summary.py)")
     ap.add_argument("--verify-fedavg", action="store_true",
                     help="after the timed rounds, check one weighted FedAvg against an all-gathered reference")
+    ap.add_argument("--tune", default="",
+                    help="launch-shape knobs for A/B sweeps, 'KEY=V,...' (csrc/kernels/launch.h TuneKey names without "
+                         "the TUNE_ prefix, e.g. WGRAD3_BLOCKS=256); default: the built-in heuristics")
     args = ap.parse_args()
 
     import numpy as np
@@ -95,6 +98,12 @@ def main() -> int:
     from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
     from crack_detection_federatedlearning_grpc_amd.utils.trace import phase
 
+    if args.tune:
+        from crack_detection_federatedlearning_grpc_amd._native_loader import hip
+        C = hip()
+        for kv in args.tune.split(","):
+            k, v = kv.split("=")
+            C.set_tune(getattr(C, "TUNE_" + k.strip().upper()), int(v))
     table = ParamTable()
     plan = None
     if args.batch <= 0:

@@ -266,6 +266,10 @@ class UNetEngine:
         # halo ones grouped per tile config into shared launches (conv_wgrad_batch) so their latency-bound grids
         # co-run (CFL_WGRAD_DEFER=0: each issued where it is computed)
         self.defer_wgrad = os.environ.get("CFL_WGRAD_DEFER", "1") != "0"
+        # BN-backward apply folded into the operand load of the data-gradient conv that consumes it (conv_igemm
+        # bwd=...; 14 of the 15 bn_bwd_apply passes - the entry BN's feeds only the entry weight gradient), which
+        # also stores dx for the weight gradient (CFL_BNB_FOLD=0: separate bn_bwd_apply launches)
+        self.fold_bnb = os.environ.get("CFL_BNB_FOLD", "0") == "1"
         self._wq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
         # per-step zeroing of gradients / statistics in one launch
@@ -385,11 +389,15 @@ class UNetEngine:
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
-               join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None) -> None:
+               join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None,
+               bwd: Optional[Tuple[torch.Tensor, str, torch.Tensor]] = None) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
 
         ``node`` = (y, bn, relu): the output is the incoming gradient of that BN node; the kernel's epilogue writes
-        the masked node gradient and accumulates the BN-backward sums (fused node_bwd)."""
+        the masked node gradient and accumulates the BN-backward sums (fused node_bwd).
+        ``bwd`` = (y, bn name, dx): x is the gradient w.r.t. that BN layer's output and the conv's operand is the
+        BN-backward apply of it (the kernel folds bn_bwd_apply into its operand load and also stores dx, for the
+        weight gradient, and the layer's dgamma / dbeta)."""
         need = self.C.conv_splits(B, Ho, Wo, N, ks, stride, pad_t, Cin)
         if need > 1 and need * B * Ho * Wo * N > self.ws.numel():
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
@@ -404,6 +412,11 @@ class UNetEngine:
             kw.update(join)
         if fin:
             kw.update(fin)
+        if bwd is not None:
+            by, bname, bdx = bwd
+            bb = self.bn[bname]
+            kw.update(bwd_y=by, bwd_ab=bb["ab"], bwd_sums=bb["sums"], bwd_reps=self.RS, bwd_dx=bdx,
+                      bwd_dgamma=self.G(bname, "gamma"), bwd_dbeta=self.G(bname, "beta"))
         self.C.conv_igemm(x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                           pad_l, self.ws if need > 1 else None, **kw)
 
@@ -487,6 +500,7 @@ class UNetEngine:
 
     def _backward(self) -> None:
         C, B, r, A, D = self.C, self.B, self.r, self.act, self.dg
+        fold = self.fold_bnb
         names = self.names
         hl = names[-1]
         C.head_bwd(A["d3_xlo"], self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
@@ -506,13 +520,16 @@ class UNetEngine:
             # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. For k < 3 the BN-backward sums
             # were accumulated by the plain node pass of level k+1 that produced dxlo (node_bwd sy/sab).
             if k == 3:
-                C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, D[f"d{k}_g"],
+                # folded: g_B is parked in dc2, which is free until convT1's dgrad stores its dx there (after the
+                # convT2 dgrad below has consumed g_B); d3_g is that dgrad's own output
+                gB = D[f"d{k}_dc2"] if fold else D[f"d{k}_g"]
+                C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, gB,
                            bnB["sums"], B, Rk, Rk, F, self.RS)
-                gB = D[f"d{k}_g"]
             else:
                 gB = dxlo
-            C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
-                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
+            if not fold:
+                C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
+                               self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
             if k == 0:
                 dq = dxlo
@@ -524,19 +541,23 @@ class UNetEngine:
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
+            # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue; folded: its operand is
+            # BN_B's backward apply of g_B (it stores dc = that dx for the weight gradient)
+            self._igemm(gB if fold else D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None,
+                        0, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1),
+                        bwd=(A[f"d{k}_c2"], b2, D[f"d{k}_dc"]) if fold else None)
             # convT2: input relu(BN_A(c1))
             self._side(lambda: self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
                                            F, 3, 1, 1, 1, 1))
-            # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
-            self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None, 0, B, Rk, Rk, F,
-                        0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1))
-            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
-                           self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
+            if not fold:
+                C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
+                               self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
+            self._igemm(D[f"d{k}_g"] if fold else D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None,
+                        D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1,
+                        bwd=(A[f"d{k}_c1"], b1, D[f"d{k}_dc2"]) if fold else None)
             # convT1: input relu(up?(prev))
             self._side(lambda: self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
                                            Rk, F, 3, 1, 1, 1, 1))
-            self._igemm(D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None, D[f"d{k}_dxin"], None, None, 0, B, Rk,
-                         Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
             # for k > 0 this gradient is also BN_B(k-1)'s node gradient: accumulate that BN's backward sums here
             if k > 0:
@@ -564,13 +585,15 @@ class UNetEngine:
             # BN_b node: routed through the max-pool (no ReLU)
             C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
                        bnb["sums"], B, H, H, F, self.RS)
-            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"], self.G(b2, "gamma"),
-                           self.G(b2, "beta"), B * H * H, F, self.RS)
-            # pointwise 2
+            if not fold:
+                C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"],
+                               self.G(b2, "gamma"), self.G(b2, "beta"), B * H * H, F, self.RS)
+            # pointwise 2 (folded: its dgrad applies BN_b's backward on load and stores dy)
+            self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None,
+                        None, 0, B, H, H, F, 0, H, H, F, 1, 1, 0, 0,
+                        bwd=(A[f"e{k}_y2"], b2, D[f"e{k}_dy"]) if fold else None)
             self._side(lambda: self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
                                            F, 0, H, H, F, 1, 1, 0, 0, 0))
-            self._igemm(D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None, None, 0, B, H, H, F, 0,
-                         H, H, F, 1, 1, 0, 0)
             # depthwise 2 on relu(BN_a(y1))
             self._side(lambda: C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")],
                                           bna["ab"], 1, B, H, H, F, self.C.STAT_REPLICAS))
@@ -578,13 +601,15 @@ class UNetEngine:
             C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
                        node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
                        node_relu=1)
-            C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy2"], self.G(b1, "gamma"),
-                           self.G(b1, "beta"), B * H * H, F, self.RS)
+            if not fold:
+                C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy2"],
+                               self.G(b1, "gamma"), self.G(b1, "beta"), B * H * H, F, self.RS)
             # pointwise 1
+            self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy2"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"],
+                        None, None, 0, B, H, H, F, 0, H, H, cin, 1, 1, 0, 0,
+                        bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]) if fold else None)
             self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
                                            H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
-            self._igemm(D[f"e{k}_dy2"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"], None, None, 0, B, H, H, F, 0,
-                         H, H, cin, 1, 1, 0, 0)
             # depthwise 1 on relu(x_in)
             self._side(lambda: C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B,
                                           H, H, cin, self.C.STAT_REPLICAS))

@@ -78,7 +78,8 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
                    int node_relu, int join_mode, OptT join_y, OptT join_ab, OptT join_out, OptT join_argmax,
                    int join_H, int join_W, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
-                   double fin_eps) {
+                   double fin_eps, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
+                   OptT bwd_dbeta) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -121,6 +122,23 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
     p.join.argmax = optr<uint8_t>(join_argmax, "join_argmax");
     p.join.H = join_H;
     p.join.W = join_W;
+  }
+  if (bwd_y) {                      // BN-backward apply folded into the operand load (common.h BnBwdIn)
+    TORCH_CHECK(bwd_ab && bwd_sums && bwd_dx, "conv_igemm: bwd_y needs bwd_ab, bwd_sums, bwd_dx");
+    TORCH_CHECK(!ab && !relu && !up_in && !join_mode && Cin <= BNB_MAX_C && bwd_reps >= 1 &&
+                bwd_reps <= BNB_MAX_REPS, "conv_igemm: the folded BN backward excludes ab / relu / up_in / join");
+    TORCH_CHECK(bwd_y->numel() == x.numel() && bwd_dx->numel() == x.numel() && bwd_ab->numel() >= 4 * Cin &&
+                bwd_sums->numel() >= (int64_t)bwd_reps * 2 * Cin, "conv_igemm: bwd tensor sizes");
+    TORCH_CHECK((!bwd_dgamma || bwd_dgamma->numel() >= Cin) && (!bwd_dbeta || bwd_dbeta->numel() >= Cin),
+                "conv_igemm: bwd_dgamma / bwd_dbeta sizes");
+    p.bwd.y = ptr<const bf16_t>(*bwd_y, "bwd_y");
+    p.bwd.ab = ptr<const float>(*bwd_ab, "bwd_ab");
+    p.bwd.sums = ptr<const float>(*bwd_sums, "bwd_sums");
+    p.bwd.reps = bwd_reps;
+    p.bwd.invM = 1.f / (float)((int64_t)B * Hin * Win);
+    p.bwd.dx = ptr<bf16_t>(*bwd_dx, "bwd_dx");
+    p.bwd.dgamma = optr<float>(bwd_dgamma, "bwd_dgamma");
+    p.bwd.dbeta = optr<float>(bwd_dbeta, "bwd_dbeta");
   }
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
@@ -628,7 +646,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_relu") = 1, py::arg("join_mode") = 0, py::arg("join_y") = py::none(),
         py::arg("join_ab") = py::none(), py::arg("join_out") = py::none(), py::arg("join_argmax") = py::none(),
         py::arg("join_H") = 0, py::arg("join_W") = 0, py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
-        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
+        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3,
+        py::arg("bwd_y") = py::none(), py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(),
+        py::arg("bwd_reps") = 1, py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(),
+        py::arg("bwd_dbeta") = py::none());
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
@@ -678,6 +699,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_CONV3_WS_GRID") = (int)TUNE_CONV3_WS_GRID;
   m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
   m.attr("TUNE_CONV3_DEEP") = (int)TUNE_CONV3_DEEP;
+  m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

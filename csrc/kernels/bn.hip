@@ -299,66 +299,38 @@ __global__ __launch_bounds__(NT) void node_pool_bwd_kernel(NodeBwdParams p) {
 constexpr int BBA_IPT = 4;
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
-  __shared__ float ssum[2 * 256];
+  __shared__ float co[5 * BNB_MAX_C];
   __shared__ float part[NT];
   const int G = p.C >> 3, lg = ilog2(G);
-  const float invM = 1.f / (float)p.M;
   const int total = p.M << lg;
   // grid stride is a multiple of G, so a thread's channel group never changes
   const int c0 = (threadIdx.x & (G - 1)) * 8;
   const int S = gridDim.x * NT;
-  // the first BBA_IPT items and the BN coefficients are loaded BEFORE the replica reduction below, so their latency
-  // overlaps it (the low-resolution layers run one iteration per thread: prologue and loads were two serial
-  // memory round trips)
-  float a[8], mean[8], rstd[8], g[BBA_IPT][8], y[BBA_IPT][8];
-  load_f8(p.ab + c0, a);
-  load_f8(p.ab + 2 * p.C + c0, mean);
-  load_f8(p.ab + 3 * p.C + c0, rstd);
+  // the first BBA_IPT items are loaded BEFORE the replica reduction below, so their latency overlaps it (the
+  // low-resolution layers run one iteration per thread: prologue and loads were two serial memory round trips)
+  uint4 g[BBA_IPT], y[BBA_IPT];
   auto load_items = [&](int t0) {
 #pragma unroll
     for (int u = 0; u < BBA_IPT; ++u) {
       const int t = t0 + u * S;
       const size_t m = (size_t)(t < total ? t : (t0 < total ? t0 : 0)) >> lg;   // clamped: loads unconditional
-      load8(p.g + m * p.C + c0, g[u]);
-      load8(p.y + m * p.C + c0, y[u]);
+      g[u] = *reinterpret_cast<const uint4*>(p.g + m * p.C + c0);
+      y[u] = *reinterpret_cast<const uint4*>(p.y + m * p.C + c0);
     }
   };
   int t0 = blockIdx.x * NT + threadIdx.x;
   load_items(t0);
-  // sum the node_bwd replica rows [reps][2][C] once per block (L2-resident, 2*C*reps floats)
-  // (all threads load in parallel: thread -> (element, replica subset), partials combined through LDS)
-  const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
-  const int C2 = 2 * p.C;                                  // power of two (C / 8 is)
-  if (C2 <= NT) {
-    const int per = NT / C2, e = threadIdx.x & (C2 - 1), jj = threadIdx.x / C2;
-    float v = 0.f;
-    for (int r = jj; r < reps; r += per) v += p.sums[(size_t)r * C2 + e];
-    part[threadIdx.x] = v;
-    __syncthreads();
-    if (threadIdx.x < C2) {
-      float t = 0.f;
-      for (int k = 0; k < per; ++k) t += part[k * C2 + threadIdx.x];
-      ssum[threadIdx.x] = t;
-    }
-  } else {
-    for (int e = threadIdx.x; e < C2; e += NT) {
-      float v = 0.f;
-      for (int r = 0; r < reps; ++r) v += p.sums[(size_t)r * C2 + e];
-      ssum[e] = v;
-    }
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < p.C; c += NT) {
-      if (p.dbeta) p.dbeta[c] = ssum[c];
-      if (p.dgamma) p.dgamma[c] = ssum[p.C + c];
-    }
-  }
-  float k1[8], k2[8];
+  // the same prologue and element arithmetic as the conv operands that fold this pass (common.h BnBwdIn)
+  const BnBwdIn q{p.y, p.ab, p.sums, p.sum_reps, 1.f / (float)p.M, p.dy, p.dgamma, p.dbeta};
+  bnb_prologue<NT>(q, p.C, co, part, blockIdx.x == 0);
+  float a[8], mean[8], rstd[8], k1[8], k2[8];        // this thread's channel group: constant over its items
 #pragma unroll
-  for (int jj = 0; jj < 8; ++jj) {
-    k1[jj] = ssum[c0 + jj] * invM;
-    k2[jj] = ssum[p.C + c0 + jj] * invM;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = co[c0 + j];
+    mean[j] = co[p.C + c0 + j];
+    rstd[j] = co[2 * p.C + c0 + j];
+    k1[j] = co[3 * p.C + c0 + j];
+    k2[j] = co[4 * p.C + c0 + j];
   }
   // BBA_IPT items per thread per iteration, all loads issued before any math (memory-level parallelism: the small
   // layers launch few blocks, so one item in flight per thread would leave HBM latency-bound)
@@ -366,13 +338,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
 #pragma unroll
     for (int u = 0; u < BBA_IPT; ++u) {
       const int t = t0 + u * S;
-      float o[8];
+      float gf[8], yf[8], of[8];
+      unpack8(g[u], gf);
+      unpack8(y[u], yf);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const float xhat = (y[u][jj] - mean[jj]) * rstd[jj];
-        o[jj] = a[jj] * (g[u][jj] - k1[jj] - xhat * k2[jj]);
-      }
-      if (t < total) *reinterpret_cast<uint4*>(p.dy + (size_t)(t >> lg) * p.C + c0) = pack8(o);
+      for (int j = 0; j < 8; ++j) of[j] = bnb_apply(gf[j], yf[j], a[j], mean[j], rstd[j], k1[j], k2[j]);
+      const uint4 o = pack8(of);
+      if (t < total) *reinterpret_cast<uint4*>(p.dy + (size_t)(t >> lg) * p.C + c0) = o;
     }
     if (t0 + BBA_IPT * S < total) load_items(t0 + BBA_IPT * S);
   }
@@ -431,7 +403,7 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
 
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
   if (p.C % 8 || !pow2(p.C / 8)) return 1;
-  if (p.C > 256) return 1;
+  if (p.C > BNB_MAX_C || p.sum_reps > BNB_MAX_REPS) return 1;
   int blocks = (int)(((int64_t)p.M * (p.C / 8) + BBA_IPT * NT - 1) / (BBA_IPT * NT));
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;

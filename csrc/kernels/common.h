@@ -187,6 +187,100 @@ CFL_DEVICE uint4 node_epi(uint4 o_bits, const bf16_t* yp, const NodeCoef& k, int
   return pack8(o);
 }
 
+// BatchNorm backward "apply" folded into the operand load of the data-gradient conv that consumes it (launch.h
+// ConvParams::bwd). The conv input x is then the gradient g w.r.t. the BN output, and the operand is
+//   dx = a * (g - s0 / M - xhat * s1 / M),  xhat = (y - mean) * rstd
+// with s0 = sum(g), s1 = sum(g * xhat) the node sums (replica rows accumulated by the producer of g). dx is also
+// stored (each input pixel once) for the weight gradient that reads it later, and one block writes dgamma = s1 /
+// dbeta = s0. This replaces the separate bn_bwd_apply pass: one launch and one write + read of dx fewer.
+struct BnBwdIn {
+  const bf16_t* y;     // raw BN input (same layout as x); nullptr = off
+  const float* ab;     // 4 rows: a, b, mean, rstd
+  const float* sums;   // [reps][2][C]
+  int reps;            // 1..16
+  float invM;          // 1 / pixels per channel
+  bf16_t* dx;          // side store of dx (nullptr = none)
+  float* dgamma;       // flat-grad slots, written (not accumulated) by one block; nullptr = none
+  float* dbeta;
+};
+#define BNB_MAX_C 256
+#define BNB_MAX_REPS 16
+
+// One element of the BN-backward apply (shared by bn_bwd_apply and the folded conv operands: same arithmetic,
+// bit-identical results).
+CFL_DEVICE float bnb_apply(float g, float y, float a, float mean, float rstd, float k1, float k2) {
+  const float xhat = (y - mean) * rstd;
+  return a * (g - k1 - xhat * k2);
+}
+
+// Block prologue of a BN-backward consumer (NTH threads; C <= BNB_MAX_C, C % 8 == 0): sums the replica rows of the
+// node sums - every load of the block issued in one round - and stages the per-channel coefficients in LDS:
+//   co[0..C) a, co[C..2C) mean, co[2C..3C) rstd, co[3C..4C) k1 = s0/M, co[4C..5C) k2 = s1/M
+// `part`: NTH floats of LDS. write_grads: this block writes dgamma / dbeta. Ends with a barrier.
+template <int NTH>
+CFL_DEVICE void bnb_prologue(const BnBwdIn& q, int C, float* co, float* part, bool write_grads) {
+  const int C2 = 2 * C, t = threadIdx.x;
+  const int reps = q.reps > 1 ? q.reps : 1;
+  float am = 0.f, mm = 0.f, rm = 0.f;
+  const bool coef = t < C;
+  if (coef) {                                   // BN coefficients: issued with the replica loads below
+    am = q.ab[t];
+    mm = q.ab[2 * C + t];
+    rm = q.ab[3 * C + t];
+  }
+  float s_lo = 0.f, s_hi = 0.f;                 // sums of element t (and t + NTH when C2 > NTH)
+  if (C2 <= NTH) {
+    const int per = NTH / C2, e = t % C2, j = t / C2;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < BNB_MAX_REPS; ++k) {
+      const int r = j + k * per;
+      if (r < reps) v += q.sums[(size_t)r * C2 + e];
+    }
+    part[t] = v;
+    __syncthreads();
+    if (t < C2)
+      for (int k = 0; k < per; ++k) s_lo += part[k * C2 + t];
+  } else {                                      // C2 == 2 * NTH at most (C <= 256, NTH = 256)
+#pragma unroll
+    for (int r = 0; r < BNB_MAX_REPS; ++r)
+      if (r < reps) {
+        s_lo += q.sums[(size_t)r * C2 + t];
+        s_hi += q.sums[(size_t)r * C2 + t + NTH];
+      }
+  }
+  // element e < C is s0[e], e >= C is s1[e - C]
+  if (t < C2) {
+    co[3 * C + t] = s_lo * q.invM;              // k1 for t < C, k2 (= co[4C + t - C]) for t >= C
+    if (write_grads) {
+      if (t < C) { if (q.dbeta) q.dbeta[t] = s_lo; }
+      else if (q.dgamma) q.dgamma[t - C] = s_lo;
+    }
+  }
+  if (C2 > NTH) {
+    co[3 * C + t + NTH] = s_hi * q.invM;
+    if (write_grads && q.dgamma) q.dgamma[t + NTH - C] = s_hi;
+  }
+  if (coef) {
+    co[t] = am;
+    co[C + t] = mm;
+    co[2 * C + t] = rm;
+  }
+  __syncthreads();
+}
+
+// dx of 8 channels c0..c0+7 from 8 g and 8 y values (coefficients from bnb_prologue's LDS block)
+CFL_DEVICE uint4 bnb_apply8(const uint4& gv, const uint4& yv, const float* co, int C, int c0) {
+  float g[8], y[8], o[8];
+  unpack8(gv, g);
+  unpack8(yv, y);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    o[j] = bnb_apply(g[j], y[j], co[c0 + j], co[C + c0 + j], co[2 * C + c0 + j], co[3 * C + c0 + j],
+                     co[4 * C + c0 + j]);
+  return pack8(o);
+}
+
 CFL_DEVICE float xform1(float v, const InXform& t, int c) {
   if (t.ab) v = fmaf(t.ab[c], v, t.ab[t.C + c]);
   if (t.relu) v = fmaxf(v, 0.f);

@@ -33,7 +33,9 @@ __device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r
 // WB ("whole-chunk B"): the block stages all 9 taps' weight tiles of a chunk at once ([tap][n][LDB], single LDS
 // buffer, next chunk register-prefetched during the current chunk's 9 x FMxFN MFMAs): two barriers per CHUNK
 // instead of one per tap, and no per-tap global-load latency on the critical path. Used for BN <= 64.
-template <int TH, int TW, int BN_, int WM, int WN, bool WB>
+// BWD (WB only): the halo is the BN-backward apply of (x = g, p.bwd.y) (common.h BnBwdIn), loaded raw and applied
+// after the previous chunk's MFMAs; the N-block-0 blocks store the tile's interior dx (each input pixel once).
+template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
@@ -49,6 +51,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SH + SB];
   __shared__ float sred[2][4][BN_];
+  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];
+  static_assert(!BWD || WB, "folded BN backward: whole-chunk path only");
   bf16_t* sH = smem;              // [2][HP][LDH]
   bf16_t* sB = smem + SH;         // [2][BN_][LDB]
 
@@ -73,17 +77,19 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   const int relu = p.xf.relu;
 
   // ---- halo loading: piece e -> halo pixel e/4, channel quarter e%4 ----
-  uint4 rh[H_PER_T];
+  uint4 rh[H_PER_T], ryh[BWD ? H_PER_T : 1];
+  uint32_t hvalid = 0;                                  // BWD: bit i = piece i inside the image
   auto load_halo = [&](int chunk) {
     const int cbase = chunk * BK;
     // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
     float a8[8], b8[8];
     load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
     load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
+    uint32_t hv = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
+      uint4 v = make_uint4(0, 0, 0, 0), yv = v;
       if (e < HALO_CHUNKS) {
         const int hp = e >> 2, q = e & 3;
         const int hy = hp / HW, hx = hp - hy * HW;
@@ -92,7 +98,11 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
           const int c = cbase + q * 8;
           v = *reinterpret_cast<const uint4*>(
               p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + c);
-          if (has_ab || relu) {
+          if constexpr (BWD) {
+            yv = *reinterpret_cast<const uint4*>(p.bwd.y + (((size_t)b * p.Hin + iy) * p.Win + ix) * p.Cin + c);
+            hv |= 1u << i;
+          }
+          if (!BWD && (has_ab || relu)) {
             float f[8];
             unpack8(v, f);
             if (has_ab) {
@@ -108,6 +118,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
         }
       }
       rh[i] = v;
+      if constexpr (BWD) ryh[i] = yv;
+    }
+    hvalid = hv;
+  };
+  // BWD: dx of the raw halo of `chunk` in place (+ the interior's side store)
+  auto bwd_halo = [&](int chunk) {
+    const bool side = bn_idx == 0 && p.bwd.dx != nullptr;
+    const int c = chunk * BK + (tid & 3) * 8;
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      if (!((hvalid >> i) & 1u)) continue;
+      const int e = tid + i * NT, hp = e >> 2;
+      const int hy = hp / HW, hx = hp - hy * HW;
+      rh[i] = bnb_apply8(rh[i], ryh[i], sco, p.Cin, c);
+      if (side && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW)
+        *reinterpret_cast<uint4*>(p.bwd.dx + (((size_t)b * p.Hin + ty0 + hy - 1) * p.Win + tx0 + hx - 1) * p.Cin +
+                                  c) = rh[i];
     }
   };
   auto store_halo = [&](int buf) {
@@ -184,6 +211,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
     if (ch0 < ch1) {
       load_halo(ch0);
       load_bw(ch0);
+    }
+    if constexpr (BWD) {          // the first chunk's loads are in flight during the replica reduction
+      bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
+      if (ch0 < ch1) bwd_halo(ch0);
+    }
+    if (ch0 < ch1) {
       store_halo(0);
       store_bw();
     }
@@ -212,6 +245,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
       __syncthreads();
       if (next_chunk) {
+        if constexpr (BWD) bwd_halo(ch + 1);
         store_halo(0);
         store_bw();
         __syncthreads();
@@ -357,8 +391,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 // only when it is written to LDS (after the MFMAs), so the loads are never waited for early. BN statistics /
 // BN-node sums accumulate in registers across the block's tiles: one set of channel atomics per block.
 // LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
-template <int TH, int TW, int CH>
-__global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
+template <int TH, int TW, int CH, bool BWD = false>
+__global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
   constexpr int BN_ = 32, WM = 4;
   constexpr int BM = TH * TW;
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
@@ -372,6 +406,7 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SW + SH + BM * LDC];
   __shared__ float sred[2][4][BN_];
+  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];   // BN-backward coefficients (BWD: see conv3x3_kernel)
   bf16_t* sB = smem;                 // [CH][9][BN_][32]
   bf16_t* sH = smem + SW;            // [CH][HP][32]
   bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem + SW + SH);
@@ -407,11 +442,15 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
     tx0 = (t % tiles_w) * TW;
   };
   // raw halo of a tile into registers (no use of the values here: the loads stay in flight)
-  uint4 rh[CH][H_PER_T];
+  uint4 rh[CH][H_PER_T], ry[BWD ? CH : 1][BWD ? H_PER_T : 1];
   uint32_t rvalid = 0;                                  // bit i: piece i lies inside the image
+  int hb = 0, hty0 = 0, htx0 = 0;                       // tile of the halo in rh (BWD side store)
   auto load_halo = [&](int item) {
     int b, ty0, tx0;
     tile_of(item, b, ty0, tx0);
+    hb = b;
+    hty0 = ty0;
+    htx0 = tx0;
     rvalid = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
@@ -424,9 +463,13 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
       const bf16_t* src = p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + q * 8;
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ok) v = *reinterpret_cast<const uint4*>(src + ch * BK);
+        uint4 v = make_uint4(0, 0, 0, 0), yv = v;
+        if (ok) {
+          v = *reinterpret_cast<const uint4*>(src + ch * BK);
+          if constexpr (BWD) yv = *reinterpret_cast<const uint4*>(p.bwd.y + (src - p.x) + ch * BK);
+        }
         rh[ch][i] = v;
+        if constexpr (BWD) ry[ch][i] = yv;
       }
     }
   };
@@ -437,10 +480,19 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
       const int e = tid + i * NT;
       if (e >= HALO_CHUNKS) continue;
       const bool ok = (rvalid >> i) & 1u;
+      const int hp = e >> 2, hy = hp / HW, hx = hp - hy * HW;
+      const bool side = BWD && ok && nBlock == 0 && p.bwd.dx != nullptr && hy >= 1 && hy <= TH && hx >= 1 &&
+                        hx <= TW;
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
         uint4 v = rh[ch][i];
-        if (has_ab || relu) {
+        if constexpr (BWD) {
+          const int c = ch * BK + (e & 3) * 8;
+          v = ok ? bnb_apply8(v, ry[ch][i], sco, p.Cin, c) : make_uint4(0, 0, 0, 0);
+          if (side)
+            *reinterpret_cast<uint4*>(p.bwd.dx + (((size_t)hb * p.Hin + hty0 + hy - 1) * p.Win + htx0 + hx - 1) *
+                                      p.Cin + c) = v;
+        } else if (has_ab || relu) {
           float f[8];
           unpack8(v, f);
           if (has_ab) {
@@ -477,10 +529,9 @@ __global__ __launch_bounds__(NT, CH == 1 ? 3 : 2) void conv3x3_ws_kernel(ConvPar
   for (int q = 0; q < 8; ++q) s[0][q] = s[1][q] = 0.f;
 
   int item = blockIdx.x;
-  if (item < n_items) {
-    load_halo(item);
-    store_halo();
-  }
+  if (item < n_items) load_halo(item);
+  if constexpr (BWD) bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, blockIdx.x == 0);
+  if (item < n_items) store_halo();
   __syncthreads();
   for (; item < n_items; item += gridDim.x) {
     const int next = item + gridDim.x;
@@ -591,7 +642,8 @@ void launch_ws(const ConvParams& p, hipStream_t st) {
   grid = grid / nb * nb;
   if (grid < nb) grid = nb;
   if (grid > items) grid = items;
-  hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
+  if (p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  else hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
 }
 
 template <int TH, int TW, int BN_, int WM, int WN, bool WB = false>
@@ -601,6 +653,13 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
   splits = (chunks + per - 1) / per;
   const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   dim3 grid(tiles, p.N / BN_, splits);
+  if constexpr (WB) {
+    if (p.bwd.y) {
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per,
+                         splits > 1 ? p.ws : nullptr);
+      return splits;
+    }
+  }
   hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, WB>), grid, dim3(NT), 0, st, p, per,
                      splits > 1 ? p.ws : nullptr);
   return splits;
@@ -635,7 +694,7 @@ static bool small_tiles(const ConvParams& p) {
 
 bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_splits(const ConvParams& p) {
-  return small_tiles(p) || ws_eligible(p) || (conv3x3_deep_eligible(p) && p.fin.gamma == nullptr)
+  return small_tiles(p) || ws_eligible(p) || (conv3x3_deep_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y)
              ? 1 : conv3x3_split_k(p);
 }
 
@@ -661,10 +720,15 @@ bool conv3x3_supported(const ConvParams& p) {
 bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_deep(const ConvParams& p, hipStream_t st);
 
+bool conv3x3_bwd_foldable(const ConvParams& p) {
+  return conv3x3_supported(p) && !p.up_in && (ws_eligible(p) || use_wb(p));
+}
+
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
   // LDS-DMA ring, no split-K (it has no in-launch BN-finalize tail: a BnFinal request keeps the other kernels)
-  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr) return conv3x3_deep(p, st);
+  // (the folded BN backward, p.bwd, runs on the whole-chunk / weight-stationary kernels: conv3x3_bwd_foldable)
+  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y) return conv3x3_deep(p, st);
   if (ws_eligible(p)) {                     // weight-stationary persistent tiles (no split-K)
     const bool w16 = p.Wo >= 16;
     if (p.Cin == 32) {

@@ -96,7 +96,9 @@ CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv) {
   }
 }
 
-template <int BM_, int BN_, int WM, int WN, bool JN = false>
+// BWD: the operand is the BN-backward apply of (x = g, p.bwd.y) (common.h BnBwdIn; 1x1 / stride 1 only, so every
+// A chunk is one input pixel and the N-block-0 blocks store each dx element exactly once).
+template <int BM_, int BN_, int WM, int WN, bool JN = false, bool BWD = false>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_per_split, float* __restrict__ ws) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM_ / WM, TN = BN_ / WN;
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
   __shared__ float sred[2][NT / 64][BN_];
+  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];   // BN-backward coefficients (bnb_prologue)
   bf16_t* sA = smem;                 // [2][BM_][32] swizzled
   bf16_t* sB = smem + SA;            // [2][BN_][32] swizzled
 
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   // The next K-tile's operands are loaded RAW into registers (ra / rb) and only transformed (producer BN-apply +
   // ReLU) in store_tiles, after the current tile's MFMAs: nothing consumes the loads early, so they stay in flight
   // across the MFMAs (a transform right after the load made every K-step wait for its own loads first).
-  uint4 ra[A_PER_T], rb[B_PER_T];
+  uint4 ra[A_PER_T], rb[B_PER_T], ry[BWD ? A_PER_T : 1];
   uint32_t avalid = 0;                 // bit i: A chunk i lies inside the (padded) input
   int c_ld = 0;                        // channel of the chunks in ra (their BN coefficients)
   auto load_tiles = [&](int kt) {
@@ -164,6 +167,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
         const size_t off = ((size_t)a_off[i] + (size_t)(ih >> p.up_in) * p.Win + (iw >> p.up_in)) * p.Cin + c;
         v = *reinterpret_cast<const uint4*>(p.x + off);
+        if constexpr (BWD) ry[i] = *reinterpret_cast<const uint4*>(p.bwd.y + off);
         avalid |= 1u << i;
       }
       ra[i] = v;
@@ -190,7 +194,17 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   };
 
   auto store_tiles = [&](int buf) {
-    if (has_ab || relu) {
+    if constexpr (BWD) {
+      const bool side = blockIdx.y == 0 && p.bwd.dx != nullptr;
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i) {
+        if ((avalid >> i) & 1u) {
+          ra[i] = bnb_apply8(ra[i], ry[i], sco, p.Cin, c_ld);
+          if (side)        // 1x1 / stride 1: input pixel == output pixel m
+            *reinterpret_cast<uint4*>(p.bwd.dx + (size_t)(mBlock + (tid >> 2) + i * 64) * p.Cin + c_ld) = ra[i];
+        }
+      }
+    } else if (has_ab || relu) {
       float ca[8], cb[8];
       load_f8_or(p.xf.ab + c_ld, has_ab, 1.f, ca);
       load_f8_or(p.xf.ab + p.xf.C + c_ld, has_ab, 0.f, cb);
@@ -222,10 +236,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
-    load_tiles(kt0);
-    store_tiles(0);
-  }
+  if (kt0 < kt1) load_tiles(kt0);
+  if constexpr (BWD)                   // the first tile's loads are in flight during the replica reduction
+    bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
+  if (kt0 < kt1) store_tiles(0);
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -408,7 +422,10 @@ void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
   const int KT = p.K / BK;
   const int per = (KT + splits - 1) / splits;
   dim3 grid((p.M + BM_ - 1) / BM_, p.N / BN_, splits);
-  if (p.join.mode)   // separate instantiation: the join epilogue's registers must not cost the plain convs occupancy
+  if (p.bwd.y)
+    hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN, false, true>), grid, dim3(NT), 0, st, p, per,
+                       splits > 1 ? ws : nullptr);
+  else if (p.join.mode)   // separate instantiation: the join epilogue's registers must not cost the plain convs occupancy
     hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN, true>), grid, dim3(NT), 0, st, p, per, nullptr);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? ws : nullptr);
@@ -420,6 +437,35 @@ bool conv3x3_supported(const ConvParams& p);
 int conv3x3(const ConvParams& p, hipStream_t st);
 
 static bool use3x3(const ConvParams& p) { return p.algo != 1 && conv3x3_supported(p); }
+bool conv3x3_bwd_foldable(const ConvParams& p);
+
+// Can the kernel that serves p fold its BN-backward operand (p.bwd)? 1x1 / stride 1 generic tiles (default tile
+// configs) and the 3x3 halo kernels (conv3x3_bwd_foldable).
+static bool bwd_foldable(const ConvParams& p) {
+  if (use3x3(p)) return conv3x3_bwd_foldable(p);
+  return p.ks == 1 && p.stride == 1 && p.pad_t == 0 && p.pad_l == 0 && !p.up_in && p.Ho == p.Hin &&
+         p.Wo == p.Win && cfl_tune(TUNE_IGEMM_CFG) == 0;
+}
+
+// Unfolded form of a p.bwd request: bn_bwd_apply into bwd.dx, then the plain conv of dx (identical results).
+static int bwd_unfolded(ConvParams p, hipStream_t st) {
+  BnBwdApplyParams a{};
+  a.g = p.x;
+  a.y = p.bwd.y;
+  a.ab = p.bwd.ab;
+  a.sums = p.bwd.sums;
+  a.dy = p.bwd.dx;
+  a.dgamma = p.bwd.dgamma;
+  a.dbeta = p.bwd.dbeta;
+  a.M = p.B * p.Hin * p.Win;
+  a.C = p.Cin;
+  a.sum_reps = p.bwd.reps;
+  const int rc = bn_bwd_apply(a, st);
+  if (rc) return rc;
+  p.x = p.bwd.dx;
+  p.bwd = BnBwdIn{};
+  return conv_igemm(p, st);
+}
 
 int splitk_epilogue(const ConvParams& p, int splits, hipStream_t st) {
   const int G = p.N / 8, lanes = NT / G;
@@ -446,6 +492,10 @@ int conv_igemm_splits(const ConvParams& p) {
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
   if (p.join.mode && (p.ks != 1 || p.stats || p.node.y || p.N % 8)) return 5;   // joins: 1x1 residual convs only
+  if (p.bwd.y) {
+    if (p.xf.ab || p.xf.relu || p.up_in || p.join.mode || p.Cin > BNB_MAX_C || p.bwd.dx == nullptr) return 6;
+    if (!bwd_foldable(p)) return bwd_unfolded(p, st);
+  }
   if (use3x3(p)) {                       // halo-tile kernel for every 3x3 / stride-1 conv (conv3x3.hip)
     const int rc = conv3x3(p, st);
     if (rc > 0) return rc;

@@ -27,7 +27,7 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
 // RM: pixels per pipeline stage (32 = one MFMA k-step; 128 = four k-steps per barrier and 4x the bytes in flight
 // per stage for the small K x N tiles, which are latency-bound at 32)
 template <int BKO, int BNO, int RM>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
+CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int bz) {
   constexpr int TK = BKO / 2, TN = BNO / 2;
   constexpr int FK = TK / 16, FN = TN / 16;
   // LDS rows of 96 / 160 / 288 bytes (32 x odd): the 32 lanes of each ds_read_b64_tr_b16 read 8 CONSECUTIVE pixel
@@ -42,8 +42,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid >> 1, wn = wid & 1;
-  const int kBlock = blockIdx.x * BKO, nBlock = blockIdx.y * BNO;
-  const int m_begin = blockIdx.z * chunk;
+  const int kBlock = bx * BKO, nBlock = by * BNO;
+  const int m_begin = bz * chunk;
   const int m_end = imin(p.M, m_begin + chunk);
   if (m_begin >= m_end) return;
   const int HWo = p.Ho * p.Wo;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
 
   // epilogue: D[k][n], col n = lane&15, row k = (lane>>4)*4 + r; slab mode spreads the split blocks' atomics
   // over replica rows (every block adding into ONE row serialises at the memory-side atomic units)
-  float* dwb = p.slabs > 0 ? p.dw + (size_t)(blockIdx.z % p.slabs) * p.K * p.N : p.dw;
+  float* dwb = p.slabs > 0 ? p.dw + (size_t)(bz % p.slabs) * p.K * p.N : p.dw;
 #pragma unroll
   for (int i = 0; i < FK; ++i)
 #pragma unroll
@@ -198,10 +198,15 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int ch
     }
 }
 
-template <int BKO, int BNO, int RM = 32>
-void launch(const WgradParams& p, hipStream_t st) {
-  const int tiles = (p.K / BKO) * (p.N / BNO);
-  int chunk = p.m_chunk;
+template <int BKO, int BNO, int RM>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
+  wgrad_body<BKO, BNO, RM>(p, chunk, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// pixels per block (multiple of rm) and M splits of a generic weight gradient with a bko x bno output tile
+void wgrad_shape(const WgradParams& p, int bko, int bno, int rm, int& chunk, int& zs) {
+  const int tiles = (p.K / bko) * (p.N / bno);
+  chunk = p.m_chunk;
   if (chunk <= 0) {
     int splits = (512 + tiles - 1) / tiles;
     const int max_splits = (p.M + 511) / 512;   // keep >= 512 pixels (16 reduction steps) per block
@@ -209,10 +214,73 @@ void launch(const WgradParams& p, hipStream_t st) {
     if (splits < 1) splits = 1;
     chunk = (p.M + splits - 1) / splits;
   }
-  chunk = (chunk + RM - 1) / RM * RM;
-  const int zs = (p.M + chunk - 1) / chunk;
+  chunk = (chunk + rm - 1) / rm * rm;
+  zs = (p.M + chunk - 1) / chunk;
+}
+
+template <int BKO, int BNO, int RM = 32>
+void launch(const WgradParams& p, hipStream_t st) {
+  int chunk, zs;
+  wgrad_shape(p, BKO, BNO, RM, chunk, zs);
   dim3 grid(p.K / BKO, p.N / BNO, zs);
   hipLaunchKernelGGL((conv_wgrad_kernel<BKO, BNO, RM>), grid, dim3(NT), 0, st, p, chunk);
+}
+
+// Grouped launch of several independent generic (1x1 / strided) weight gradients of ONE tile config: the deferred
+// pointwise and residual-conv wgrads of a step are latency-bound grids of 64-512 blocks each (the low-resolution
+// layers hold few pixels per block), so issued together their blocks co-run (the 3x3 halo ones are grouped the same
+// way in conv3x3_wgrad.hip).
+constexpr int WG1_MAX = 16;
+struct WgradItem {
+  WgradParams p;
+  int chunk, gx, gy, block0;
+};
+struct WgradGroup {
+  WgradItem it[WG1_MAX];
+  int n;
+};
+
+template <int BKO, int BNO, int RM>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_group_kernel(const WgradGroup g) {
+  int k = 0;
+  while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
+  const WgradItem& I = g.it[k];
+  const int local = blockIdx.x - I.block0;
+  const int bx = local % I.gx, r = local / I.gx;
+  wgrad_body<BKO, BNO, RM>(I.p, I.chunk, bx, r % I.gy, r / I.gy);
+}
+
+// tile config of a generic weight gradient (see conv_wgrad) and its (BKO, BNO, RM)
+int wgrad_config(const WgradParams& p, int& bko, int& bno, int& rm) {
+  const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
+  if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) { bko = 128; bno = 128; rm = 32; return 0; }
+  rm = 128;
+  if (p.K % 64 == 0 && p.N % 64 == 0) { bko = 64; bno = 64; return 1; }
+  if (p.K % 64 == 0) { bko = 64; bno = 32; return 2; }
+  if (p.N % 64 == 0) { bko = 32; bno = 64; return 3; }
+  bko = 32; bno = 32;
+  return 4;
+}
+
+template <int BKO, int BNO, int RM>
+int launch_group(const WgradParams* ps, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += WG1_MAX) {
+    WgradGroup g{};
+    int blocks = 0;
+    for (int i = i0; i < n && i < i0 + WG1_MAX; ++i) {
+      WgradItem& it = g.it[g.n++];
+      it.p = ps[i];
+      int zs;
+      wgrad_shape(ps[i], BKO, BNO, RM, it.chunk, zs);
+      it.gx = ps[i].K / BKO;
+      it.gy = ps[i].N / BNO;
+      it.block0 = blocks;
+      blocks += it.gx * it.gy * zs;
+    }
+    hipLaunchKernelGGL((conv_wgrad_group_kernel<BKO, BNO, RM>), dim3(blocks), dim3(NT), 0, st, g);
+    if (hipGetLastError() != hipSuccess) return 3;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -231,20 +299,43 @@ bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x
 int conv3x3_wgrad_config(const WgradParams& p);
 int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st);
 
+static bool generic_ok(const WgradParams& p) {
+  return p.Cin % 8 == 0 && p.K == p.ks * p.ks * p.Cin && p.K % 32 == 0 && p.N % 32 == 0;
+}
+
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
-  WgradParams by_cfg[4][16];
-  int cnt[4] = {0, 0, 0, 0};
+  static thread_local WgradParams by_cfg[4][16], gen_cfg[5][32];
+  int cnt[4] = {0, 0, 0, 0}, gcnt[5] = {0, 0, 0, 0, 0};
+  const bool group = cfl_tune(TUNE_WGRAD_GROUP) != 1;
+  const bool group1 = group && cfl_tune(TUNE_WGRAD_GROUP) != 2;
   for (int i = 0; i < n; ++i) {
     const WgradParams& p = ps[i];
     if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
-    if (p.algo != 1 && conv3x3_wgrad_supported(p) && cfl_tune(TUNE_WGRAD_GROUP) != 1) {
+    if (p.algo != 1 && conv3x3_wgrad_supported(p) && group) {
       const int c = conv3x3_wgrad_config(p);
       if (cnt[c] == 16) return 5;
       by_cfg[c][cnt[c]++] = p;
+    } else if (!(p.algo != 1 && conv3x3_wgrad_supported(p)) && group1 && generic_ok(p)) {
+      int bko, bno, rm;
+      const int c = wgrad_config(p, bko, bno, rm);
+      if (gcnt[c] == 32) return 5;
+      gen_cfg[c][gcnt[c]++] = p;
     } else {
       const int rc = conv_wgrad(p, st);
       if (rc) return rc;
     }
+  }
+  for (int c = 0; c < 5; ++c) {
+    if (!gcnt[c]) continue;
+    int rc;
+    switch (c) {
+      case 0: rc = launch_group<128, 128, 32>(gen_cfg[c], gcnt[c], st); break;
+      case 1: rc = launch_group<64, 64, 128>(gen_cfg[c], gcnt[c], st); break;
+      case 2: rc = launch_group<64, 32, 128>(gen_cfg[c], gcnt[c], st); break;
+      case 3: rc = launch_group<32, 64, 128>(gen_cfg[c], gcnt[c], st); break;
+      default: rc = launch_group<32, 32, 128>(gen_cfg[c], gcnt[c], st); break;
+    }
+    if (rc) return rc;
   }
   for (int c = 0; c < 4; ++c)
     if (cnt[c]) {
@@ -257,12 +348,14 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
 int conv_wgrad(const WgradParams& p, hipStream_t st) {
   if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
   if (p.algo != 1 && conv3x3_wgrad_supported(p)) return conv3x3_wgrad(p, st);
-  if (p.Cin % 8 != 0 || p.K != p.ks * p.ks * p.Cin || p.K % 32 != 0 || p.N % 32 != 0) return 1;
-  const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
-  if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) launch<128, 128>(p, st);
-  else if (p.K % 64 == 0 && p.N % 64 == 0) launch<64, 64, 128>(p, st);
-  else if (p.K % 64 == 0) launch<64, 32, 128>(p, st);
-  else if (p.N % 64 == 0) launch<32, 64, 128>(p, st);
-  else launch<32, 32, 128>(p, st);
+  if (!generic_ok(p)) return 1;
+  int bko, bno, rm;
+  switch (wgrad_config(p, bko, bno, rm)) {
+    case 0: launch<128, 128>(p, st); break;
+    case 1: launch<64, 64, 128>(p, st); break;
+    case 2: launch<64, 32, 128>(p, st); break;
+    case 3: launch<32, 64, 128>(p, st); break;
+    default: launch<32, 32, 128>(p, st); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

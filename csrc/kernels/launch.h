@@ -69,6 +69,9 @@ struct ConvParams {
   BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
   ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
   BnFinal fin;         // optional in-launch finalize of `stats` (run by the launch that completes them)
+  BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;
+                       // common.h). Data-gradient convs only: 1x1/s1 or 3x3/s1, no upsample, no xf; shapes a kernel
+                       // does not fold fall back to bn_bwd_apply into bwd.dx + the plain conv (same results)
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
@@ -312,7 +315,7 @@ enum TuneKey {
   TUNE_HEAD_BLOCKS = 13,       // head fwd / bwd grid cap (default 512)
   TUNE_CONV3_WS = 14,          // conv3x3 Cin <= 64: 0 = weight-stationary persistent kernel, 1 = per-tile kernel
   TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
-  TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every 3x3 wgrad on its own (no grouping)
+  TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every wgrad on its own, 2 = group the 3x3 ones only
   TUNE_CONV3_DEEP = 17,        // conv3x3 Cin >= 128: 0 = LDS-DMA 3-stage deep-K kernel, 1 = off, 2 = force (any Cin)
   TUNE_N = 20
 };
