@@ -271,6 +271,7 @@ class UNetEngine:
         # also stores dx for the weight gradient (CFL_BNB_FOLD=0: separate bn_bwd_apply launches)
         self.fold_bnb = os.environ.get("CFL_BNB_FOLD", "0") == "1"
         self._wq: Optional[List[tuple]] = None
+        self._dwq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
         # per-step zeroing of gradients / statistics in one launch
         spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10], self.bn_ctr]
@@ -483,12 +484,25 @@ class UNetEngine:
         C.head_fwd(prev.t, self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics if train else self.eval_metrics, B, r[0], DEC_FILTERS[-1], self.dice)
 
+    def _dw_wgrad(self, *args) -> None:
+        """Depthwise weight gradient: deferred with the conv weight gradients (its inputs - a forward activation and
+        the depthwise dgrad's incoming gradient - are not rewritten later in backward) and issued in one grouped
+        launch with the other depthwise layers' (dw_wgrad_batch)."""
+        if self._dwq is not None:
+            self._dwq.append(args + (0,))
+        else:
+            self._side(lambda: self.C.dw_wgrad(*args))
+
     def backward(self) -> None:
         self._wq = [] if self.defer_wgrad else None
+        self._dwq = [] if self.defer_wgrad else None
         try:
             self._backward()
         finally:
             wq, self._wq = self._wq, None
+            dwq, self._dwq = self._dwq, None
+        if dwq:
+            self.C.dw_wgrad_batch(dwq)
         if wq:
             self.C.conv_wgrad_batch(wq)
         self._join_side()
@@ -595,8 +609,8 @@ class UNetEngine:
             self._side(lambda: self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
                                            F, 0, H, H, F, 1, 1, 0, 0, 0))
             # depthwise 2 on relu(BN_a(y1))
-            self._side(lambda: C.dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")],
-                                          bna["ab"], 1, B, H, H, F, self.C.STAT_REPLICAS))
+            self._dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B, H,
+                           H, F, self.C.STAT_REPLICAS)
             # depthwise dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
             C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
                        node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
@@ -611,8 +625,8 @@ class UNetEngine:
             self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
                                            H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
             # depthwise 1 on relu(x_in)
-            self._side(lambda: C.dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B,
-                                          H, H, cin, self.C.STAT_REPLICAS))
+            self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H, cin,
+                           self.C.STAT_REPLICAS)
             C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._side(lambda: self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,

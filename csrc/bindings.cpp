@@ -251,8 +251,8 @@ void dw_dgrad_op(at::Tensor dy, at::Tensor w, at::Tensor dx, int B, int H, int W
   ok(dw_dgrad(p, stream()), "dw_dgrad");
 }
 
-void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C,
-                 int replicas, int algo) {
+DwParams dw_wgrad_params(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C,
+                         int replicas, int algo) {
   DwParams p = dwp(B, H, W, C);
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -262,7 +262,26 @@ void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, 
   p.replicas = replicas < 1 ? 1 : replicas;
   TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && dy.numel() == x.numel() &&
                   dw.numel() == (int64_t)p.replicas * 9 * C, "dw_wgrad sizes");
-  ok(dw_wgrad(p, stream()), "dw_wgrad");
+  return p;
+}
+
+void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, int B, int H, int W, int C,
+                 int replicas, int algo) {
+  ok(dw_wgrad(dw_wgrad_params(x, dy, dw, ab, relu, B, H, W, C, replicas, algo), stream()), "dw_wgrad");
+}
+
+// calls: a list of dw_wgrad argument tuples (x, dy, dw, ab, relu, B, H, W, C, replicas, algo) -> one grouped launch
+void dw_wgrad_batch_op(py::list calls) {
+  std::vector<DwParams> ps;
+  for (auto h : calls) {
+    auto t = h.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 11, "dw_wgrad_batch: each call needs the 11 dw_wgrad arguments");
+    OptT ab = t[3].is_none() ? OptT() : OptT(t[3].cast<at::Tensor>());
+    ps.push_back(dw_wgrad_params(t[0].cast<at::Tensor>(), t[1].cast<at::Tensor>(), t[2].cast<at::Tensor>(), ab,
+                                 t[4].cast<int>(), t[5].cast<int>(), t[6].cast<int>(), t[7].cast<int>(),
+                                 t[8].cast<int>(), t[9].cast<int>(), t[10].cast<int>()));
+  }
+  ok(dw_wgrad_batch(ps.data(), (int)ps.size(), stream()), "dw_wgrad_batch");
 }
 
 void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bias, at::Tensor y, OptT stats, int B,
@@ -674,6 +693,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_relu") = 1);
   m.def("dw_wgrad", &dw_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("replicas") = 1, py::arg("algo") = 0);
+  m.def("dw_wgrad_batch", &dw_wgrad_batch_op, py::arg("calls"));
   m.def("entry_fwd", &entry_fwd_op, py::arg("images"), py::arg("idx"), py::arg("w"), py::arg("bias"), py::arg("y"),
         py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
         py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
@@ -700,6 +720,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
   m.attr("TUNE_CONV3_DEEP") = (int)TUNE_CONV3_DEEP;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
+  m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;
+  m.attr("TUNE_WGRAD1_MINPIX") = (int)TUNE_WGRAD1_MINPIX;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

@@ -233,7 +233,10 @@ static void wgrad3_shape(const WgradParams& p, int& bno, int& tiles, int& splits
   tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   const int xy = (p.Cin / CB) * (p.N / bno);
   const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 512;
-  const int min_tiles = cfl_tune(TUNE_WGRAD3_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_MINTILES) : 4;
+  // >= 16 pixel tiles per block: the engine launches the decoder's halo wgrads grouped (conv3x3_wgrad_grouped), so
+  // long blocks still fill the chip, and every pixel split is one plain-stored slab row that grad_finish must read
+  // (whole-step A/B on one MI355X: 4 / 8 / 16 / 24 / 32 -> 1.733 / 1.706 / 1.691 / 1.729 / 1.782 ms/iteration)
+  const int min_tiles = cfl_tune(TUNE_WGRAD3_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_MINTILES) : 16;
   splits = (target + xy - 1) / xy;
   const int max_splits = (tiles + min_tiles - 1) / min_tiles;   // amortise each block's output write
   if (splits > max_splits) splits = max_splits;

@@ -208,8 +208,13 @@ void wgrad_shape(const WgradParams& p, int bko, int bno, int rm, int& chunk, int
   const int tiles = (p.K / bko) * (p.N / bno);
   chunk = p.m_chunk;
   if (chunk <= 0) {
-    int splits = (512 + tiles - 1) / tiles;
-    const int max_splits = (p.M + 511) / 512;   // keep >= 512 pixels (16 reduction steps) per block
+    // 256 blocks per layer: the deferred wgrads of a step are launched grouped (launch_group), so a layer's grid
+    // need not fill the chip alone - fewer, longer blocks halve the replica-row atomics (whole-step A/B: 1.691 ->
+    // 1.676 ms/iteration vs 512, profiles/README.md)
+    const int target = cfl_tune(TUNE_WGRAD1_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD1_BLOCKS) : 256;
+    const int minpix = cfl_tune(TUNE_WGRAD1_MINPIX) > 0 ? cfl_tune(TUNE_WGRAD1_MINPIX) : 512;
+    int splits = (target + tiles - 1) / tiles;
+    const int max_splits = (p.M + minpix - 1) / minpix;   // keep >= minpix pixels per block (512: 4 RM=128 stages)
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     chunk = (p.M + splits - 1) / splits;

@@ -459,8 +459,9 @@ CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0
 }
 }  // namespace dws
 
+// bid / nblocks: this block's index in, and the size of, its launch (or its item of a grouped launch)
 template <int MODE>
-__global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replicas, int seg_rows) {
+CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, int bid, int nblocks) {
   using namespace dws;
   __shared__ __attribute__((aligned(16))) bf16_t sH[NRING * HWp * LDP];
   __shared__ __attribute__((aligned(16))) float sNode[MODE == 1 ? 4 * CT : 4];   // dgrad node coefficients
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replic
   const int tid = threadIdx.x, cg = tid % G, pt = tid / G;
   const int sr = pt / (TW / SL), sc = (pt % (TW / SL)) * SL;
   const int nslices = p.C / CT, tiles_w = (p.W + TW - 1) / TW, nseg = (p.H + seg_rows - 1) / seg_rows;
-  int lin = xcd_swizzle(blockIdx.x, gridDim.x);
+  int lin = xcd_swizzle(bid, nblocks);
   const int cs = lin % nslices;
   lin /= nslices;
   const int tw = lin % tiles_w;
@@ -653,11 +654,11 @@ __global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replic
     float* dst;
     int rstride;
     if (MODE == 2) {
-      dst = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
+      dst = p.dw + (size_t)(bid % replicas) * 9 * p.C;
       rstride = p.C;
     } else {
       const int reps = p.node.reps > 1 ? p.node.reps : 1;
-      dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * p.C;
+      dst = p.node.sums + (size_t)(bid % reps) * 2 * p.C;
       rstride = p.C;
     }
     for (int e = tid; e < NS * CT; e += NT) {
@@ -669,15 +670,48 @@ __global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replic
 }
 
 template <int MODE>
-int launch_stream(const DwParams& p, int replicas, hipStream_t st) {
+__global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replicas, int seg_rows) {
+  dw_stream_body<MODE>(p, replicas, seg_rows, blockIdx.x, gridDim.x);
+}
+
+// Grouped launch of the deferred depthwise weight gradients of a step (the engine's 6 SeparableConv depthwise
+// layers): each alone is a latency-bound row-streaming grid, so they share one launch and their blocks co-run.
+constexpr int DWG_MAX = 8;
+struct DwItem {
+  DwParams p;
+  int replicas, seg_rows, block0, nblocks;   // block0: multiple of 8 (an item's blocks keep their XCD order)
+};
+struct DwGroup {
+  DwItem it[DWG_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) {
+  int k = 0;
+  while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
+  const DwItem& I = g.it[k];
+  const int local = blockIdx.x - I.block0;
+  if (local >= I.nblocks) return;                       // alignment padding between items
+  dw_stream_body<2>(I.p, I.replicas, I.seg_rows, local, I.nblocks);
+}
+
+// (grid size, rows per segment) of the row-streaming kernels
+void stream_shape(const DwParams& p, int& blocks, int& seg_rows) {
   const int steps = (p.H + dws::SR - 1) / dws::SR;
   const int strips = p.B * ((p.W + 31) / 32) * (p.C / dws::CT);
   const int target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 768;   // A/B-measured (256 / 384 / 512 / 768 / 1024 / 2048)
   int nseg = (target + strips - 1) / strips;
   nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
-  const int seg_rows = ((steps + nseg - 1) / nseg) * dws::SR;
+  seg_rows = ((steps + nseg - 1) / nseg) * dws::SR;
   nseg = (p.H + seg_rows - 1) / seg_rows;
-  hipLaunchKernelGGL((dw_stream_kernel<MODE>), dim3(strips * nseg), dim3(NT), 0, st, p, replicas, seg_rows);
+  blocks = strips * nseg;
+}
+
+template <int MODE>
+int launch_stream(const DwParams& p, int replicas, hipStream_t st) {
+  int blocks, seg_rows;
+  stream_shape(p, blocks, seg_rows);
+  hipLaunchKernelGGL((dw_stream_kernel<MODE>), dim3(blocks), dim3(NT), 0, st, p, replicas, seg_rows);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -718,6 +752,37 @@ int dw_dgrad(const DwParams& p, hipStream_t st) {
   if (tiled(p)) return launch_tile<1>(p, 1, st);
   if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the halo-tile path only
   return launch_dw(p.dy, p.w, p.y, InXform{nullptr, p.C, 0}, p.B, p.H, p.W, p.C, 1, st);
+}
+
+int dw_wgrad_batch(const DwParams* ps, int n, hipStream_t st) {
+  DwGroup g{};
+  int blocks = 0;
+  auto flush = [&]() -> int {
+    if (g.n == 0) return 0;
+    hipLaunchKernelGGL(dw_wgrad_group_kernel, dim3(blocks), dim3(NT), 0, st, g);
+    g = DwGroup{};
+    blocks = 0;
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  };
+  for (int i = 0; i < n; ++i) {
+    const DwParams& p = ps[i];
+    if (!streamed(p) || cfl_tune(TUNE_WGRAD_GROUP) == 1) {   // other paths: one launch each
+      const int rc = dw_wgrad(p, st);
+      if (rc) return rc;
+      continue;
+    }
+    if (g.n == DWG_MAX) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    DwItem& it = g.it[g.n++];
+    it.p = p;
+    it.replicas = p.replicas > 1 ? p.replicas : 1;
+    stream_shape(p, it.nblocks, it.seg_rows);
+    it.block0 = blocks;
+    blocks = (blocks + it.nblocks + 7) / 8 * 8;
+  }
+  return flush();
 }
 
 int dw_wgrad(const DwParams& p, hipStream_t st) {

@@ -131,6 +131,8 @@ struct DwParams {
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);
 int dw_wgrad(const DwParams& p, hipStream_t st);
+// several independent depthwise weight gradients: the row-streaming ones in one grouped launch (dwconv.hip)
+int dw_wgrad_batch(const DwParams* ps, int n, hipStream_t st);
 
 // ---------------------------------------------------------------- entry conv 3x3 s2, Cin = 3 (entry.hip)
 struct EntryParams {
@@ -303,7 +305,7 @@ int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStrea
 enum TuneKey {
   TUNE_NODE_BWD_BLOCKS = 0, TUNE_DW_WGRAD_BLOCKS = 1, TUNE_ENTRY_WGRAD_BLOCKS = 2,
   TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 512)
-  TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 4)
+  TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 16)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
   TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 512)
@@ -317,6 +319,8 @@ enum TuneKey {
   TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
   TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every wgrad on its own, 2 = group the 3x3 ones only
   TUNE_CONV3_DEEP = 17,        // conv3x3 Cin >= 128: 0 = LDS-DMA 3-stage deep-K kernel, 1 = off, 2 = force (any Cin)
+  TUNE_WGRAD1_BLOCKS = 18,     // generic (1x1) wgrad: target blocks per layer (default 256)
+  TUNE_WGRAD1_MINPIX = 19,     // generic (1x1) wgrad: min pixels per block (default 512)
   TUNE_N = 20
 };
 int cfl_tune(int key);
