@@ -159,7 +159,10 @@ CFL_DEVICE void node_gather(const NodeBwdParams& p, int b, int h, int w, int c0,
   }
 }
 
-template <int M0, int M1>
+// IPT items (pixel, 8-channel group) per thread per iteration, all gathered before any store: the walk is
+// latency-bound (a 512-block grid leaves 8-16 items per thread at the 128^2 level), so the loads of several items
+// must be in flight together
+template <int M0, int M1, int IPT>
 __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   __shared__ float red[2][4][256];
   const int G = p.C >> 3, lg = ilog2(G);
@@ -192,24 +195,23 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
       }
     }
   };
-  // flat items (pixel, channel group), two per iteration; the grid stride is a multiple of G
+  // flat items (pixel, channel group), IPT per iteration; the grid stride is a multiple of G
   const int total = (p.B * p.H * p.W) << lg;
   const int HW = p.H * p.W;
   const int stride = gridDim.x * NT;
-  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += 2 * stride) {
-    const int it2 = it + stride;
-    const bool two = it2 < total;
-    float y0[8], v0[8], g0[8], y1[8], v1[8], g1[8];
-    const int pix0 = it >> lg, b0 = pix0 / HW, r0 = pix0 - b0 * HW, h0 = r0 / p.W;
-    node_gather<M0, M1>(p, b0, h0, r0 - h0 * p.W, c0, a, bb, y0, v0, g0);
-    int pix1 = 0;
-    if (two) {
-      pix1 = it2 >> lg;
-      const int b1 = pix1 / HW, r1 = pix1 - b1 * HW, h1 = r1 / p.W;
-      node_gather<M0, M1>(p, b1, h1, r1 - h1 * p.W, c0, a, bb, y1, v1, g1);
+  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += IPT * stride) {
+    float y[IPT][8], v[IPT][8], g[IPT][8];
+    int pix[IPT];
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+      const int itu = it + u * stride;
+      pix[u] = (itu < total ? itu : it) >> lg;            // clamped: every gather issues, only valid items store
+      const int bu = pix[u] / HW, ru = pix[u] - bu * HW, hu = ru / p.W;
+      node_gather<M0, M1>(p, bu, hu, ru - hu * p.W, c0, a, bb, y[u], v[u], g[u]);
     }
-    finish((size_t)pix0, y0, v0, g0);
-    if (two) finish((size_t)pix1, y1, v1, g1);
+#pragma unroll
+    for (int u = 0; u < IPT; ++u)
+      if (it + u * stride < total) finish((size_t)pix[u], y[u], v[u], g[u]);
   }
   if (!p.sums) return;
   // replica row of this block: every block adding into ONE row of sums serialises at the memory-side atomic units
@@ -373,6 +375,19 @@ int bn_eval_coefs(const BnEval* d_layers, int n_layers, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+template <int IPT>
+int launch_node(const NodeBwdParams& p, int blocks, hipStream_t st) {
+  const int m0 = p.src[0].mode, m1 = p.src[1].mode;
+  if (m0 == GM_SAME && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_NONE, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SUM2X2 && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_NONE, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_MAXPOOL && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_MAXPOOL, GM_NONE, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SAME && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SAME, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SUM2X2 && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_SAME, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (m0 == GM_SAME && m1 == GM_SCATTER2) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SCATTER2, IPT>), dim3(blocks), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL((node_bwd_kernel<-1, -1, 2>), dim3(blocks), dim3(NT), 0, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 int node_bwd(const NodeBwdParams& p, hipStream_t st) {
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
   const int64_t items = (int64_t)p.B * p.H * p.W * (p.C / 8);
@@ -391,14 +406,10 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   // specialised instances for the engine's source combinations (fewer live registers, no mode branches)
-  if (m0 == GM_SAME && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
-  else if (m0 == GM_SUM2X2 && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
-  else if (m0 == GM_MAXPOOL && m1 == GM_NONE) hipLaunchKernelGGL((node_bwd_kernel<GM_MAXPOOL, GM_NONE>), dim3(blocks), dim3(NT), 0, st, p);
-  else if (m0 == GM_SAME && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SAME>), dim3(blocks), dim3(NT), 0, st, p);
-  else if (m0 == GM_SUM2X2 && m1 == GM_SAME) hipLaunchKernelGGL((node_bwd_kernel<GM_SUM2X2, GM_SAME>), dim3(blocks), dim3(NT), 0, st, p);
-  else if (m0 == GM_SAME && m1 == GM_SCATTER2) hipLaunchKernelGGL((node_bwd_kernel<GM_SAME, GM_SCATTER2>), dim3(blocks), dim3(NT), 0, st, p);
-  else hipLaunchKernelGGL((node_bwd_kernel<-1, -1>), dim3(blocks), dim3(NT), 0, st, p);
-  return hipGetLastError() == hipSuccess ? 0 : 3;
+  // 2 items in flight per thread: 4 doubles the registers (occupancy 3 -> 2 waves/SIMD) and measured slower
+  // (whole step 1.684 vs 1.695 ms/iteration)
+  if (cfl_tune(TUNE_NODE_BWD_IPT) == 4) return launch_node<4>(p, blocks, st);
+  return launch_node<2>(p, blocks, st);
 }
 
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {

@@ -321,7 +321,8 @@ enum TuneKey {
   TUNE_CONV3_DEEP = 17,        // conv3x3 Cin >= 128: 0 = LDS-DMA 3-stage deep-K kernel, 1 = off, 2 = force (any Cin)
   TUNE_WGRAD1_BLOCKS = 18,     // generic (1x1) wgrad: target blocks per layer (default 256)
   TUNE_WGRAD1_MINPIX = 19,     // generic (1x1) wgrad: min pixels per block (default 512)
-  TUNE_N = 20
+  TUNE_NODE_BWD_IPT = 20,      // node_bwd: items in flight per thread (2 or 4; default 2)
+  TUNE_N = 24
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

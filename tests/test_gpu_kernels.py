@@ -1276,17 +1276,18 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-def test_engine_bnb_fold_matches_unfolded():
-    """A whole training step with the BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1) matches
-    the step with separate bn_bwd_apply launches (default): same loss, same gradients up to the run-to-run
-    atomic-order noise of the statistics (a second unfolded run bounds it)."""
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0")])
+def test_engine_switch_matches_default(var, val):
+    """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
+    issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
+    of the statistics (a second default run bounds it)."""
     import os
     grads, losses = [], []
-    for fold in ("1", "0", "0"):
-        os.environ["CFL_BNB_FOLD"] = fold
+    for v in (val, None, None):
+        if v is not None:
+            os.environ[var] = v
         try:
             _, eng, *_ = _engine_and_ref(S=128, B=4, seed=5)
-            assert eng.fold_bnb == (fold == "1")
             eng._zero_step()
             eng.forward(True)
             eng.backward()
@@ -1294,10 +1295,10 @@ def test_engine_bnb_fold_matches_unfolded():
             grads.append(eng.grad.cpu())
             losses.append(eng.read_metrics("train")["loss"])
         finally:
-            os.environ.pop("CFL_BNB_FOLD", None)
+            os.environ.pop(var, None)
     # run-to-run noise: float atomics (BN statistics, replica rows) sum in arbitrary order, and at this random init
     # the bf16 roundings / ReLU boundaries they flip move the gradients by a few percent (measured 3.7-4.9 % between
-    # identical runs); the folded step must sit inside that band
+    # identical runs); the variant must sit inside that band
     noise = max(rel(grads[2], grads[1]), 0.02)
     assert rel(grads[0], grads[1]) <= 3 * noise, (rel(grads[0], grads[1]), noise)
     assert abs(losses[0] - losses[1]) <= max(4 * abs(losses[2] - losses[1]), 2e-3), losses
