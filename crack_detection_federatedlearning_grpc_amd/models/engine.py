@@ -270,6 +270,9 @@ class UNetEngine:
         # bwd=...; 14 of the 15 bn_bwd_apply passes - the entry BN's feeds only the entry weight gradient), which
         # also stores dx for the weight gradient (CFL_BNB_FOLD=0: separate bn_bwd_apply launches)
         self.fold_bnb = os.environ.get("CFL_BNB_FOLD", "0") == "1"
+        # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
+        # dgrad launch plus a deferred, grouped wgrad)
+        self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
@@ -609,12 +612,19 @@ class UNetEngine:
             self._side(lambda: self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
                                            F, 0, H, H, F, 1, 1, 0, 0, 0))
             # depthwise 2 on relu(BN_a(y1))
-            self._dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B, H,
-                           H, F, self.C.STAT_REPLICAS)
-            # depthwise dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
-            C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
-                       node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
-                       node_relu=1)
+            # depthwise 2 on relu(BN_a(y1)): dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue,
+            # and (fused pass) the weight gradient from the same dy rows
+            if self.fuse_dw_bwd:
+                C.dw_bwd(A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"],
+                         self.gslab[(s2, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, F,
+                         node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
+                         node_relu=1)
+            else:
+                self._dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B,
+                               H, H, F, self.C.STAT_REPLICAS)
+                C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
+                           node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
+                           node_relu=1)
             if not fold:
                 C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy2"],
                                self.G(b1, "gamma"), self.G(b1, "beta"), B * H * H, F, self.RS)
@@ -625,9 +635,13 @@ class UNetEngine:
             self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
                                            H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
             # depthwise 1 on relu(x_in)
-            self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H, cin,
-                           self.C.STAT_REPLICAS)
-            C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
+            if self.fuse_dw_bwd:
+                C.dw_bwd(xin.t, xin.ab, 1, D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"],
+                         self.gslab[(s1, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, cin)
+            else:
+                self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H,
+                               cin, self.C.STAT_REPLICAS)
+                C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._side(lambda: self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                                            1, 2, 0, 0, 0))

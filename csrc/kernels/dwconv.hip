@@ -695,6 +695,195 @@ __global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) 
   dw_stream_body<2>(I.p, I.replicas, I.seg_rows, local, I.nblocks);
 }
 
+// Fused depthwise backward of one layer: dgrad and wgrad in one row-streaming pass. Both need the incoming gradient
+// dy of the same rows (dgrad as a 3x3 halo, wgrad at the centre) and the wgrad needs the layer input x as a halo, so
+// a block keeps TWO rings (dy raw, x with the producer's BN-apply + ReLU) and takes the wgrad's dy strip from the
+// centre row of the dy ring: dy and x are each read once per segment instead of dy twice + x twice (separate dgrad
+// with a BN-node epilogue reading x again, and wgrad), and one launch per layer instead of two.
+__global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int replicas, int seg_rows) {
+  using namespace dws;
+  __shared__ __attribute__((aligned(16))) bf16_t sG[NRING * HWp * LDP];   // dy rows
+  __shared__ __attribute__((aligned(16))) bf16_t sX[NRING * HWp * LDP];   // transformed x rows
+  __shared__ __attribute__((aligned(16))) float sW[9 * CT];               // flipped taps (dgrad)
+  __shared__ __attribute__((aligned(16))) float sNode[4 * CT];
+
+  const int tid = threadIdx.x, cg = tid % G, pt = tid / G;
+  const int sr = pt / (TW / SL), sc = (pt % (TW / SL)) * SL;
+  const int nslices = p.C / CT, tiles_w = (p.W + TW - 1) / TW, nseg = (p.H + seg_rows - 1) / seg_rows;
+  int lin = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int cs = lin % nslices;
+  lin /= nslices;
+  const int tw = lin % tiles_w;
+  lin /= tiles_w;
+  const int sg = lin % nseg;
+  const int b = lin / nseg;
+  const int x0 = tw * TW, cbase = cs * CT, c0 = cbase + cg * CPT;
+  const int ybeg = sg * seg_rows, yend = min(p.H, ybeg + seg_rows);
+  const int nsteps = (yend - ybeg + SR - 1) / SR;
+  const bool has_ab = p.xf.ab != nullptr;
+  const int relu = p.xf.relu;
+  const size_t img = (size_t)b * p.H * p.W * p.C + c0;
+  const bf16_t* g_b = p.dy + img;
+  const bf16_t* x_b = p.x + img;
+  float a4[4], b4[4];
+  load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
+  load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+  for (int e = tid; e < 9 * CT; e += NT) {
+    const int t = e / CT, c = e - t * CT;
+    sW[e] = p.w[(8 - t) * p.C + cbase + c];
+  }
+  const bool node = p.node.y != nullptr;
+  if (node && tid < 4 * CT) sNode[tid] = p.node.ab[(tid / CT) * p.C + cbase + tid % CT];
+  {
+    uint2 v[SR + 3], u[SR + 3];
+    uint32_t okv, oku;
+    fetch<SR + 2>(g_b, p, x0, ybeg - 1, true, v, okv);
+    fetch<SR + 2>(x_b, p, x0, ybeg - 1, true, u, oku);
+    put<SR + 2>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
+    put<SR + 2>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);
+  }
+  __syncthreads();
+
+  float accw[9][4], s0[4], s1[4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accw[t][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s0[j] = s1[j] = 0.f;
+  uint2 rg[SR + 1], rx[SR + 1];
+  uint32_t okg = 0, okx = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    const int a = ybeg + s * SR;
+    const bool more = s + 1 < nsteps;
+    fetch<SR>(g_b, p, x0, a + SR + 1, more, rg, okg);       // next step's rows, in flight during this step
+    fetch<SR>(x_b, p, x0, a + SR + 1, more, rx, okx);
+    const int oy = a + sr;
+    const float live = oy < yend ? 1.f : 0.f;              // rows past the segment belong to the next block
+    float acc[SL][4], g[SL][4];
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = 0.f;
+    // dgrad: flipped taps over the dy halo; the centre row's columns 1..SL are this strip's own dy (wgrad operand)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int slot = (oy - 1 + ky + NRING) % NRING;
+      const bf16_t* hrow = &sG[(slot * HWp + sc) * LDP + cg * CPT];
+      float wt[3][4];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) load_f4(&sW[(ky * 3 + kx) * CT + cg * CPT], wt[kx]);
+#pragma unroll
+      for (int cx = 0; cx < SL + 2; ++cx) {
+        float f[4];
+        unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+        if (ky == 1 && cx >= 1 && cx <= SL) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[cx - 1][j] = f[j] * live;
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SL) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[o][j] = fmaf(f[j], wt[kx][j], acc[o][j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // wgrad: dW[tap] += x[p + tap - 1] * dy[p] over the x halo
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int slot = (oy - 1 + ky + NRING) % NRING;
+      const bf16_t* hrow = &sX[(slot * HWp + sc) * LDP + cg * CPT];
+#pragma unroll
+      for (int cx = 0; cx < SL + 2; ++cx) {
+        float f[4];
+        unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SL) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) accw[ky * 3 + kx][j] = fmaf(f[j], g[o][j], accw[ky * 3 + kx][j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (oy < yend) {
+      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+#pragma unroll
+      for (int i = 0; i < SL; ++i)
+        if (x0 + sc + i < p.W) {
+          uint2 v = pack4(acc[i]);
+          if (node) {                                        // g = mask * o (o already bf16) + BN-backward sums
+            float o[4], y[4], na[4], nb[4], nmean[4], nrstd[4];
+            const float* nc = &sNode[cg * CPT];
+            load_f4(nc, na);
+            load_f4(nc + CT, nb);
+            load_f4(nc + 2 * CT, nmean);
+            load_f4(nc + 3 * CT, nrstd);
+            unpack4(v, o);
+            unpack4(*reinterpret_cast<const uint2*>(p.node.y + off0 + (size_t)i * p.C), y);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float gg = (!p.node.relu || fmaf(na[j], y[j], nb[j]) > 0.f) ? o[j] : 0.f;
+              o[j] = gg;
+              s0[j] += gg;
+              s1[j] += gg * (y[j] - nmean[j]) * nrstd[j];
+            }
+            v = pack4(o);
+          }
+          *reinterpret_cast<uint2*>(p.y + off0 + (size_t)i * p.C) = v;
+        }
+    }
+    if (more) {
+      put<SR>(sG, rg, okg, a + SR + 1, false, a4, b4, 0);
+      put<SR>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
+    }
+    __syncthreads();
+  }
+
+  // block reduction of the 9 tap sums (+ the 2 node sums), one atomic per (row, channel) into replica rows
+  const int lane = tid & 63, wid = tid >> 6;
+  constexpr int NS = 11;
+  float* red = reinterpret_cast<float*>(sG);                 // ring no longer needed (loop ended on a barrier)
+  float part[NS][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[t][j] = accw[t][j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    part[9][j] = s0[j];
+    part[10][j] = s1[j];
+  }
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = part[t][j];
+      for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      part[t][j] = v;
+    }
+  if (lane < G) {
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[(wid * NS + t) * CT + cg * CPT + j] = part[t][j];
+  }
+  __syncthreads();
+  float* dwr = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
+  const int nreps = p.node.reps > 1 ? p.node.reps : 1;
+  float* nsr = node ? p.node.sums + (size_t)(blockIdx.x % nreps) * 2 * p.C : nullptr;
+  for (int e = tid; e < (node ? NS : 9) * CT; e += NT) {
+    const int t = e / CT, c = e % CT;
+    const float v = red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] + red[(2 * NS + t) * CT + c] +
+                    red[(3 * NS + t) * CT + c];
+    atomicAdd(t < 9 ? &dwr[t * p.C + cbase + c] : &nsr[(t - 9) * p.C + cbase + c], v);
+  }
+}
+
 // (grid size, rows per segment) of the row-streaming kernels
 void stream_shape(const DwParams& p, int& blocks, int& seg_rows) {
   const int steps = (p.H + dws::SR - 1) / dws::SR;
@@ -752,6 +941,18 @@ int dw_dgrad(const DwParams& p, hipStream_t st) {
   if (tiled(p)) return launch_tile<1>(p, 1, st);
   if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the halo-tile path only
   return launch_dw(p.dy, p.w, p.y, InXform{nullptr, p.C, 0}, p.B, p.H, p.W, p.C, 1, st);
+}
+
+int dw_bwd(const DwParams& p, hipStream_t st) {
+  if (!streamed(p)) {                                       // other paths: the two passes
+    const int rc = dw_dgrad(p, st);
+    return rc ? rc : dw_wgrad(p, st);
+  }
+  int blocks, seg_rows;
+  stream_shape(p, blocks, seg_rows);
+  hipLaunchKernelGGL(dw_bwd_stream_kernel, dim3(blocks), dim3(NT), 0, st, p, p.replicas > 1 ? p.replicas : 1,
+                     seg_rows);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int dw_wgrad_batch(const DwParams* ps, int n, hipStream_t st) {

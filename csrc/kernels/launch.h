@@ -131,6 +131,9 @@ struct DwParams {
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);
 int dw_wgrad(const DwParams& p, hipStream_t st);
+// dgrad (p.dy -> p.y, optional BN-node epilogue p.node) and wgrad (p.x with p.xf, p.dy -> p.dw replicas) of one
+// layer in one fused pass (dwconv.hip dw_bwd_stream_kernel)
+int dw_bwd(const DwParams& p, hipStream_t st);
 // several independent depthwise weight gradients: the row-streaming ones in one grouped launch (dwconv.hip)
 int dw_wgrad_batch(const DwParams* ps, int n, hipStream_t st);
 

@@ -1276,7 +1276,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
@@ -1330,3 +1330,36 @@ def test_dw_wgrad_batch_grouped_equals_individual():
         assert torch.allclose(bt, c[2], rtol=1e-5, atol=1e-3)
         got = bt.view(c[9], 9, c[8]).sum(0).cpu()
         assert rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,C,node,relu", [(2, 32, 32, 64, True, 1), (2, 24, 40, 32, False, 1),
+                                               (3, 16, 16, 128, True, 0), (2, 13, 9, 32, True, 1)])
+def test_dw_bwd_fused_matches_dgrad_and_wgrad(B, H, W, C, node, relu):
+    """dw_bwd (depthwise dgrad + BN-node epilogue + wgrad of one layer in one row-streaming pass with a dy ring and an
+    x ring) equals dw_dgrad (bit for bit: same arithmetic) and dw_wgrad (up to float atomic order), on ragged maps
+    (segments / strips that end inside a step) and with / without the node epilogue."""
+    torch.manual_seed(47)
+    C_ = hip()
+    xb, _ = bf(torch.randn(B, H, W, C))
+    gb, _ = bf(torch.randn(B, H, W, C))
+    w = (torch.randn(9 * C) * 0.2).to(DEV)
+    ab = ab_for(C, 48)[0].to(DEV)
+    nab = ab_for(C, 49)[0]
+    nab[2 * C:3 * C], nab[3 * C:] = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    nab = nab.to(DEV)
+    reps = 32
+    kw = lambda sums: dict(node_y=xb, node_ab=nab, node_sums=sums, node_reps=4, node_relu=relu) if node else {}
+    dx_ref = torch.zeros_like(gb)
+    sums_ref = torch.zeros(4 * 2 * C, device=DEV)
+    C_.dw_dgrad(gb, w, dx_ref, B, H, W, C, 0, **kw(sums_ref))
+    dw_ref = torch.zeros(reps * 9 * C, device=DEV)
+    C_.dw_wgrad(xb, gb, dw_ref, ab, 1, B, H, W, C, reps)
+    dx = torch.zeros_like(gb)
+    sums = torch.zeros(4 * 2 * C, device=DEV)
+    dw = torch.zeros(reps * 9 * C, device=DEV)
+    C_.dw_bwd(xb, ab, 1, gb, w, dx, dw, reps, B, H, W, C, **kw(sums))
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref), int((dx != dx_ref).sum())
+    assert torch.allclose(dw.view(reps, -1).sum(0), dw_ref.view(reps, -1).sum(0), rtol=1e-4, atol=1e-3)
+    if node:
+        assert torch.allclose(sums.view(4, -1).sum(0), sums_ref.view(4, -1).sum(0), rtol=1e-4, atol=1e-3)
