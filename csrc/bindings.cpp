@@ -735,6 +735,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
   m.attr("TUNE_CONV3_DEEP") = (int)TUNE_CONV3_DEEP;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
+  m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;
   m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;
   m.attr("TUNE_WGRAD1_MINPIX") = (int)TUNE_WGRAD1_MINPIX;
   m.attr("TUNE_NODE_BWD_IPT") = (int)TUNE_NODE_BWD_IPT;

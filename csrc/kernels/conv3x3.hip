@@ -77,14 +77,17 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   const int relu = p.xf.relu;
 
   // ---- halo loading: piece e -> halo pixel e/4, channel quarter e%4 ----
+  // The halo is loaded RAW (rh) and the producer's BN-apply + ReLU applied only right before it is written to LDS,
+  // after the current chunk's MFMAs: a transform right after the load made every chunk wait for its own prefetch
+  // first (tools/conv3_probe.py at 256^2 / B16: the transformed convs ran 1.1-5.4 us slower than untransformed ones).
   uint4 rh[H_PER_T], ryh[BWD ? H_PER_T : 1];
-  uint32_t hvalid = 0;                                  // BWD: bit i = piece i inside the image
+  uint32_t hvalid = 0;                                  // bit i = piece i inside the image
+  float ha[8], hb[8];                                   // producer coefficients of the loaded chunk (quarter tid & 3)
   auto load_halo = [&](int chunk) {
     const int cbase = chunk * BK;
     // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
-    float a8[8], b8[8];
-    load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
-    load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
+    load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, ha);
+    load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, hb);
     uint32_t hv = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
@@ -98,29 +101,31 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
           const int c = cbase + q * 8;
           v = *reinterpret_cast<const uint4*>(
               p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + c);
-          if constexpr (BWD) {
+          if constexpr (BWD)
             yv = *reinterpret_cast<const uint4*>(p.bwd.y + (((size_t)b * p.Hin + iy) * p.Win + ix) * p.Cin + c);
-            hv |= 1u << i;
-          }
-          if (!BWD && (has_ab || relu)) {
-            float f[8];
-            unpack8(v, f);
-            if (has_ab) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = fmaf(a8[j], f[j], b8[j]);
-            }
-            if (relu) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-            }
-            v = pack8(f);
-          }
+          hv |= 1u << i;
         }
       }
       rh[i] = v;
       if constexpr (BWD) ryh[i] = yv;
     }
     hvalid = hv;
+  };
+  // producer BN-apply + ReLU of the raw halo in rh; padding stays exactly 0 (it is outside the transform)
+  auto xform_halo = [&]() {
+    if (BWD || !(has_ab || relu)) return;
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) {
+      if (!((hvalid >> i) & 1u)) continue;
+      float f[8];
+      unpack8(rh[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = fmaf(ha[j], f[j], hb[j]);
+        if (relu) f[j] = fmaxf(f[j], 0.f);
+      }
+      rh[i] = pack8(f);
+    }
   };
   // BWD: dx of the raw halo of `chunk` in place (+ the interior's side store)
   auto bwd_halo = [&](int chunk) {
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       if (ch0 < ch1) bwd_halo(ch0);
     }
     if (ch0 < ch1) {
+      xform_halo();
       store_halo(0);
       store_bw();
     }
@@ -246,6 +252,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       __syncthreads();
       if (next_chunk) {
         if constexpr (BWD) bwd_halo(ch + 1);
+        xform_halo();
         store_halo(0);
         store_bw();
         __syncthreads();
@@ -254,6 +261,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   } else {
   if (ch0 < ch1) {
     load_halo(ch0);
+    xform_halo();
     store_halo(0);
     load_b(ch0, 0);
     store_b(0);
@@ -285,7 +293,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
       if (more) store_b(bbuf ^ 1);
-      if (tap == 8 && next_chunk) store_halo(hbuf ^ 1);
+      if (tap == 8 && next_chunk) {
+        xform_halo();
+        store_halo(hbuf ^ 1);
+      }
       __syncthreads();
       bbuf ^= 1;
     }
