@@ -520,9 +520,12 @@ class UNetEngine:
         fold = self.fold_bnb
         names = self.names
         hl = names[-1]
+        # the head's input gradient is also the gradient of the last BN_B node (x_lo = BN_B(c2) + q, no ReLU): its
+        # BN-backward sums are accumulated in head_bwd's epilogue (no separate node pass over dxlo3)
+        bn_last = self.bn[names[17 + 5 * 3 + 3]]
         C.head_bwd(A["d3_xlo"], self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics, D["dxlo3"], self.G(hl, "kernel"), self.G(hl, "bias"), B, r[0], DEC_FILTERS[-1],
-                   self.dice)
+                   self.dice, node_y=A["d3_c2"], node_ab=bn_last["ab"], node_sums=bn_last["sums"], node_reps=self.RS)
         dxlo = D["dxlo3"]
         for k in range(3, -1, -1):
             F = DEC_FILTERS[k]
@@ -534,16 +537,9 @@ class UNetEngine:
             prevres = Rk if k == 0 else Rk // 2
             up = 0 if k == 0 else 1
             bnB, bnA = self.bn[b2], self.bn[b1]
-            # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. For k < 3 the BN-backward sums
-            # were accumulated by the plain node pass of level k+1 that produced dxlo (node_bwd sy/sab).
-            if k == 3:
-                # folded: g_B is parked in dc2, which is free until convT1's dgrad stores its dx there (after the
-                # convT2 dgrad below has consumed g_B); d3_g is that dgrad's own output
-                gB = D[f"d{k}_dc2"] if fold else D[f"d{k}_g"]
-                C.node_bwd(dxlo, GM_SAME, 0, None, 0, 0, None, A[f"d{k}_c2"], bnB["ab"], 0, gB,
-                           bnB["sums"], B, Rk, Rk, F, self.RS)
-            else:
-                gB = dxlo
+            # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. Its BN-backward sums were
+            # accumulated by the pass that produced dxlo: head_bwd (k = 3) or the plain node pass of level k+1
+            gB = dxlo
             if not fold:
                 C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
                                self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)

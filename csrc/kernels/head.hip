@@ -99,10 +99,13 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&p.metrics[2], (double)npix * 4.0);
 }
 
-template <int CIN>
+// NODE: dx is also the gradient of the decoder's last BN node (x_lo = BN_B(c2) + q, no ReLU): its BN-backward sums
+// sum(g), sum(g * xhat) are accumulated here from the stored bf16 dx (what a separate node_bwd pass would read back)
+template <int CIN, bool NODE>
 __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
   static_assert(CIN == 32, "4 lanes x 8 channels per pixel");
   __shared__ float red[CIN + 1][NT / 64];
+  __shared__ float nred[NODE ? 2 * CIN : 1][NT / 64];
   const int npix = p.B * p.R * p.R;
   const int S = 2 * p.R;
   const int q = threadIdx.x & 3;
@@ -120,9 +123,14 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) gw[k] = 0.f;
   float gb = 0.f;
+  float nmean[8], nrstd[8], ns0[8], ns1[8];
+  load_f8_or(p.node.ab + 2 * CIN + 8 * q, NODE, 0.f, nmean);
+  load_f8_or(p.node.ab + 3 * CIN + 8 * q, NODE, 0.f, nrstd);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ns0[k] = ns1[k] = 0.f;
   const int stride = gridDim.x * NT;
   for (int t0 = blockIdx.x * NT + threadIdx.x; (t0 >> 2) < npix; t0 += HPT * stride) {
-    float f[HPT][8], hv[HPT], tt[HPT];
+    float f[HPT][8], hv[HPT], tt[HPT], yn[NODE ? HPT : 1][8];
     int pix[HPT];
 #pragma unroll
     for (int u = 0; u < HPT; ++u) {     // all loads first (see head_fwd_kernel)
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
       const int pc = pix[u] < 0 ? 0 : pix[u];
       hv[u] = p.h[pc];
       load8(p.x + (size_t)pc * CIN + 8 * q, f[u]);
+      if constexpr (NODE) load8(p.node.y + (size_t)pc * CIN + 8 * q, yn[u]);
       tt[u] = mask_at(p, pc, S, q);
     }
 #pragma unroll
@@ -148,7 +157,17 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
         o[k] = dh * w[k];
         gw[k] = fmaf(dh, f[u][k], gw[k]);
       }
-      *reinterpret_cast<uint4*>(p.dx + (size_t)pix[u] * CIN + 8 * q) = pack8(o);
+      const uint4 ov = pack8(o);
+      *reinterpret_cast<uint4*>(p.dx + (size_t)pix[u] * CIN + 8 * q) = ov;
+      if constexpr (NODE) {
+        float g[8];
+        unpack8(ov, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ns0[k] += g[k];
+          ns1[k] += g[k] * (yn[u][k] - nmean[k]) * nrstd[k];
+        }
+      }
     }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -161,7 +180,31 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
     for (int k = 0; k < 8; ++k) red[8 * lane + k][wid] = gw[k];
   }
   if (lane == 0) red[CIN][wid] = gb;
+  if constexpr (NODE) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      for (int o = 4; o < 64; o <<= 1) {
+        ns0[k] += __shfl_xor(ns0[k], o, 64);
+        ns1[k] += __shfl_xor(ns1[k], o, 64);
+      }
+    if (lane < 4) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        nred[8 * lane + k][wid] = ns0[k];
+        nred[CIN + 8 * lane + k][wid] = ns1[k];
+      }
+    }
+  }
   __syncthreads();
+  if constexpr (NODE) {
+    const int reps = p.node.reps > 1 ? p.node.reps : 1;
+    float* dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * CIN;
+    if (threadIdx.x < 2 * CIN) {
+      float s = 0.f;
+      for (int w2 = 0; w2 < NT / 64; ++w2) s += nred[threadIdx.x][w2];
+      atomicAdd(&dst[threadIdx.x], s);
+    }
+  }
   if (threadIdx.x <= CIN) {
     float s = 0.f;
     for (int w2 = 0; w2 < NT / 64; ++w2) s += red[threadIdx.x][w2];
@@ -186,6 +229,7 @@ int head_fwd(const HeadParams& p, hipStream_t st) {
 
 int head_bwd(const HeadParams& p, hipStream_t st) {
   if (p.Cin != 32) return 1;
-  hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(head_blocks(p)), dim3(NT), 0, st, p);
+  if (p.node.y) hipLaunchKernelGGL((head_bwd_kernel<32, true>), dim3(head_blocks(p)), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL((head_bwd_kernel<32, false>), dim3(head_blocks(p)), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -249,6 +249,8 @@ struct HeadParams {
   float* db;
   int B, R, Cin;
   int dice;                // add the Dice loss
+  BnNodeEpi node;          // head_bwd: dx is also the (unmasked) gradient of a BN node whose input is node.y (same
+                           // layout as x): accumulate its BN-backward sums (the decoder's last BN_B; node.relu unused)
 };
 int head_fwd(const HeadParams& p, hipStream_t st);
 int head_bwd(const HeadParams& p, hipStream_t st);

@@ -993,6 +993,20 @@ def test_head_loss_metrics_and_gradients_match_autograd(dice):
     assert float(m[6]) == float(t.sum())
     assert rel(from_bits(dx), gx) < 1e-2
     assert rel(dw.cpu(), gw) < 1e-3 and rel(db.cpu(), gb) < 1e-3
+    # BN-node sums epilogue (the decoder's last BN_B): same dx, and the sums node_bwd computes from the stored dx
+    yb, _ = bf(torch.randn(B, Rr, Rr, 32, generator=g))
+    nab = ab_for(32, 51)[0]
+    nab[64:96], nab[96:] = torch.randn(32, generator=g) * 0.1, torch.rand(32, generator=g) + 0.5
+    nab = nab.to(DEV)
+    sums = torch.zeros(4 * 64, device=DEV)
+    dx2, dw2, db2 = torch.zeros_like(dx), torch.zeros_like(dw), torch.zeros_like(db)
+    met.zero_()
+    C.head_fwd(*args, B, Rr, 32, dice)
+    C.head_bwd(*args, dx2, dw2, db2, B, Rr, 32, dice, node_y=yb, node_ab=nab, node_sums=sums, node_reps=4)
+    ref_g, ref_s = _node_ref(C, dx2, yb, nab, 0, B, Rr, Rr, 32)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx) and torch.equal(ref_g, dx2)
+    assert torch.allclose(sums.view(4, 64).sum(0), ref_s, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("ks,H,Cin,N,B,tune", [
