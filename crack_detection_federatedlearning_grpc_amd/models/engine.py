@@ -630,28 +630,35 @@ class UNetEngine:
                         bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]) if fold else None)
             self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
                                            H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
-            # depthwise 1 on relu(x_in)
-            if self.fuse_dw_bwd:
-                C.dw_bwd(xin.t, xin.ab, 1, D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"],
-                         self.gslab[(s1, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, cin)
-            else:
-                self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H,
-                               cin, self.C.STAT_REPLICAS)
-                C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._side(lambda: self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                                            1, 2, 0, 0, 0))
             # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                          H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
-            if k > 0:
-                C.node_bwd(D[f"e{k}_dz0"], GM_SAME, 1, D[f"e{k}_dres"], GM_SCATTER2, 0, None, xin.t, None, 0,
-                           D[f"e{k}_dx"], None, B, H, H, cin)
-                dx_out = D[f"e{k}_dx"]
+            # depthwise 1 on relu(x_in), and the gradient of x_in itself: the depthwise branch (ReLU-masked) plus the
+            # stride-2 scatter of dres; for k = 0 x_in is relu(BN0(y0)), a BN node (mask + sums)
+            bn0 = self.bn[names[1]]
+            out = D[f"e{k}_dx"] if k > 0 else D["g0"]
+            if self.fuse_dw_bwd:                # one pass: dgrad + wgrad + the node join in the dgrad's epilogue
+                nkw = dict(node_y=A["y0"], node_ab=bn0["ab"], node_sums=bn0["sums"], node_reps=self.RS,
+                           node_relu=1) if k == 0 else dict(mask_x=1)
+                C.dw_bwd(xin.t, xin.ab, 1, D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), out,
+                         self.gslab[(s1, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, cin,
+                         add_half=D[f"e{k}_dres"], **nkw)
             else:
-                bn0 = self.bn[names[1]]
-                C.node_bwd(D["e0_dz0"], GM_SAME, 0, D["e0_dres"], GM_SCATTER2, 0, None, A["y0"], bn0["ab"], 1,
-                           D["g0"], bn0["sums"], B, H, H, cin, self.RS)
+                self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H,
+                               cin, self.C.STAT_REPLICAS)
+                C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
+                if k > 0:
+                    C.node_bwd(D[f"e{k}_dz0"], GM_SAME, 1, D[f"e{k}_dres"], GM_SCATTER2, 0, None, xin.t, None, 0,
+                               out, None, B, H, H, cin)
+                else:
+                    C.node_bwd(D["e0_dz0"], GM_SAME, 0, D["e0_dres"], GM_SCATTER2, 0, None, A["y0"], bn0["ab"], 1,
+                               out, bn0["sums"], B, H, H, cin, self.RS)
+            if k > 0:
+                dx_out = out
+            else:
                 C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
                                self.G(names[1], "beta"), B * H * H, cin, self.RS)
                 C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,

@@ -272,11 +272,16 @@ void dw_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu, 
 
 void dw_bwd_op(at::Tensor x, OptT ab, int relu, at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor dw,
                int replicas, int B, int H, int W, int C, int algo, OptT node_y, OptT node_ab, OptT node_sums,
-               int node_reps, int node_relu) {
+               int node_reps, int node_relu, OptT add_half, int mask_x) {
   DwParams p = dw_wgrad_params(x, dy, dw, ab, relu, B, H, W, C, replicas, algo);
   p.w = ptr<const float>(w, "w");
   p.y = ptr<bf16_t>(dx, "dx");
   p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, dx.numel(), C);
+  p.add_half = optr<const bf16_t>(add_half, "add_half");
+  p.mask_x = mask_x;
+  TORCH_CHECK(!p.add_half || add_half->numel() == (int64_t)B * ((H + 1) / 2) * ((W + 1) / 2) * C,
+              "dw_bwd: add_half size");
+  TORCH_CHECK(!mask_x || relu, "dw_bwd: mask_x needs the ReLU'd input");
   TORCH_CHECK(dx.numel() == dy.numel() && w.numel() == 9 * C, "dw_bwd sizes");
   ok(dw_bwd(p, stream()), "dw_bwd");
 }
@@ -710,7 +715,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dw_bwd", &dw_bwd_op, py::arg("x"), py::arg("ab"), py::arg("relu"), py::arg("dy"), py::arg("w"),
         py::arg("dx"), py::arg("dw"), py::arg("replicas"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"),
         py::arg("algo") = 0, py::arg("node_y") = py::none(), py::arg("node_ab") = py::none(),
-        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("node_relu") = 1);
+        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("node_relu") = 1,
+        py::arg("add_half") = py::none(), py::arg("mask_x") = 0);
   m.def("entry_fwd", &entry_fwd_op, py::arg("images"), py::arg("idx"), py::arg("w"), py::arg("bias"), py::arg("y"),
         py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
         py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);

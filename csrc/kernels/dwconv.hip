@@ -760,11 +760,11 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     fetch<SR>(x_b, p, x0, a + SR + 1, more, rx, okx);
     const int oy = a + sr;
     const float live = oy < yend ? 1.f : 0.f;              // rows past the segment belong to the next block
-    float acc[SL][4], g[SL][4];
+    float acc[SL][4], g[SL][4], xc[SL][4];
 #pragma unroll
     for (int i = 0; i < SL; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = 0.f;
+      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = xc[i][j] = 0.f;
     // dgrad: flipped taps over the dy halo; the centre row's columns 1..SL are this strip's own dy (wgrad operand)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
@@ -800,6 +800,10 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       for (int cx = 0; cx < SL + 2; ++cx) {
         float f[4];
         unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+        if (ky == 1 && cx >= 1 && cx <= SL) {             // centre pixels' transformed x (mask_x)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xc[cx - 1][j] = f[j];
+        }
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int o = cx - kx;
@@ -816,6 +820,24 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       for (int i = 0; i < SL; ++i)
         if (x0 + sc + i < p.W) {
           uint2 v = pack4(acc[i]);
+          if (p.add_half || p.mask_x) {                      // residual join (node_bwd semantics, one rounding)
+            float o[4];
+            unpack4(v, o);
+            if (p.mask_x) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] = xc[i][j] > 0.f ? o[j] : 0.f;
+            }
+            const int xx = x0 + sc + i;
+            if (p.add_half && ((oy | xx) & 1) == 0) {
+              const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
+              float r[4];
+              unpack4(*reinterpret_cast<const uint2*>(
+                          p.add_half + (((size_t)b * Hh + (oy >> 1)) * Wh + (xx >> 1)) * p.C + c0), r);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] += r[j];
+            }
+            v = pack4(o);
+          }
           if (node) {                                        // g = mask * o (o already bf16) + BN-backward sums
             float o[4], y[4], na[4], nb[4], nmean[4], nrstd[4];
             const float* nc = &sNode[cg * CPT];
@@ -944,7 +966,8 @@ int dw_dgrad(const DwParams& p, hipStream_t st) {
 }
 
 int dw_bwd(const DwParams& p, hipStream_t st) {
-  if (!streamed(p)) {                                       // other paths: the two passes
+  if (!streamed(p)) {                                       // other paths: the two passes (no residual join)
+    if (p.add_half || p.mask_x) return 2;
     const int rc = dw_dgrad(p, st);
     return rc ? rc : dw_wgrad(p, st);
   }

@@ -127,6 +127,10 @@ struct DwParams {
   int replicas;        // wgrad: >1 = spread block atomics over that many copies of the row (summed by grad_finish)
   int algo;            // 0 auto (C % 32 == 0 -> row-streaming LDS ring), 1 row-strip kernels, 2 LDS halo tiles
   BnNodeEpi node;      // dgrad only (halo-tile path): fused BN-node gradient epilogue
+  // dw_bwd only: the dgrad output joins the residual branch's gradient before it is stored (the encoder's input
+  // node, node_bwd(dz0 same [masked], dres stride-2 scatter) folded into the producer):
+  const bf16_t* add_half;   // dres [B, ceil(H/2), ceil(W/2), C] added at even (h, w) (before the node epilogue)
+  int mask_x;               // multiply the dgrad value (not add_half) by [x > 0] (x = the layer's transformed input)
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);

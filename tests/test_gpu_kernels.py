@@ -1377,3 +1377,37 @@ def test_dw_bwd_fused_matches_dgrad_and_wgrad(B, H, W, C, node, relu):
     assert torch.allclose(dw.view(reps, -1).sum(0), dw_ref.view(reps, -1).sum(0), rtol=1e-4, atol=1e-3)
     if node:
         assert torch.allclose(sums.view(4, -1).sum(0), sums_ref.view(4, -1).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,H,W,C,bn", [(2, 32, 32, 64, False), (2, 17, 23, 32, False), (2, 32, 32, 32, True)])
+def test_dw_bwd_residual_join_matches_node_bwd(B, H, W, C, bn):
+    """dw_bwd with the encoder input node folded into its dgrad epilogue: out = [x > 0] * dgrad + stride-2 scatter of
+    the residual gradient (add_half, mask_x), or for the BN'd entry activation the BN node (mask + sums) applied to
+    dgrad + scatter - equal to dw_dgrad into dz0 followed by node_bwd (bit for bit; odd maps included)."""
+    torch.manual_seed(53)
+    C_ = hip()
+    xb, _ = bf(torch.randn(B, H, W, C))
+    gb, _ = bf(torch.randn(B, H, W, C))
+    rb, _ = bf(torch.randn(B, (H + 1) // 2, (W + 1) // 2, C))
+    w = (torch.randn(9 * C) * 0.2).to(DEV)
+    nab = ab_for(C, 54)[0]
+    nab[2 * C:3 * C], nab[3 * C:] = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    nab = nab.to(DEV)
+    ab = nab if bn else None
+    dz0 = torch.zeros_like(gb)
+    C_.dw_dgrad(gb, w, dz0, B, H, W, C)
+    ref = torch.zeros_like(gb)
+    s_ref = torch.zeros(2 * C, device=DEV)
+    if bn:
+        C_.node_bwd(dz0, 1, 0, rb, 2, 0, None, xb, nab, 1, ref, s_ref, B, H, W, C)
+    else:
+        C_.node_bwd(dz0, 1, 1, rb, 2, 0, None, xb, None, 0, ref, None, B, H, W, C)
+    out = torch.zeros_like(gb)
+    sums = torch.zeros(4 * 2 * C, device=DEV)
+    dw = torch.zeros(16 * 9 * C, device=DEV)
+    kw = dict(node_y=xb, node_ab=nab, node_sums=sums, node_reps=4, node_relu=1) if bn else dict(mask_x=1)
+    C_.dw_bwd(xb, ab, 1, gb, w, out, dw, 16, B, H, W, C, add_half=rb, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), int((out != ref).sum())
+    if bn:
+        assert torch.allclose(sums.view(4, -1).sum(0), s_ref, rtol=1e-4, atol=1e-3)
