@@ -273,6 +273,9 @@ class UNetEngine:
         # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
         # dgrad launch plus a deferred, grouped wgrad)
         self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
+        # decoder node join (2x2 sum of the convT1 input gradient, ReLU mask, + residual gradient, BN_B(k-1) sums) in
+        # the convT1 dgrad's epilogue (CFL_POOL_JOIN=0: dxin stored + a node_bwd pass)
+        self.fuse_pool_join = os.environ.get("CFL_POOL_JOIN", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
@@ -394,7 +397,7 @@ class UNetEngine:
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
                join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None,
-               bwd: Optional[Tuple[torch.Tensor, str, torch.Tensor]] = None) -> None:
+               bwd: Optional[Tuple[torch.Tensor, str, torch.Tensor]] = None, **extra) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
 
         ``node`` = (y, bn, relu): the output is the incoming gradient of that BN node; the kernel's epilogue writes
@@ -416,6 +419,7 @@ class UNetEngine:
             kw.update(join)
         if fin:
             kw.update(fin)
+        kw.update(extra)
         if bwd is not None:
             by, bname, bdx = bwd
             bb = self.bn[bname]
@@ -565,20 +569,26 @@ class UNetEngine:
             if not fold:
                 C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
                                self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
+            # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path;
+            # for k > 0 this gradient is also BN_B(k-1)'s node gradient (its BN-backward sums accumulate here) -
+            # the join runs in the convT1 dgrad's epilogue at half resolution (dxin is never stored)
+            pjkw = {}
+            if k > 0 and self.fuse_pool_join:
+                bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
+                pjkw = dict(pj_v=prev_t, pj_add=D[f"d{k}_dres"], pj_out=D[f"d{k}_dprev"], pj_sy=A[f"d{k - 1}_c2"],
+                            pj_sab=bprev["ab"], pj_sums=bprev["sums"], pj_reps=self.RS)
             self._igemm(D[f"d{k}_g"] if fold else D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None,
                         D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1,
-                        bwd=(A[f"d{k}_c1"], b1, D[f"d{k}_dc2"]) if fold else None)
+                        bwd=(A[f"d{k}_c1"], b1, D[f"d{k}_dc2"]) if fold else None, **pjkw)
             # convT1: input relu(up?(prev))
             self._side(lambda: self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
                                            Rk, F, 3, 1, 1, 1, 1))
-            # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path
-            # for k > 0 this gradient is also BN_B(k-1)'s node gradient: accumulate that BN's backward sums here
-            if k > 0:
+            if not pjkw and k > 0:
                 bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
                 C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
                            prev_t, None, 0, D[f"d{k}_dprev"], bprev["sums"], B, prevres, prevres, cprev, self.RS,
                            sy=A[f"d{k - 1}_c2"], sab=bprev["ab"])
-            else:
+            elif not pjkw:
                 C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
                            prev_t, None, 0, D[f"d{k}_dprev"], None, B, prevres, prevres, cprev)
             dxlo = D[f"d{k}_dprev"]

@@ -79,7 +79,8 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    int node_relu, int join_mode, OptT join_y, OptT join_ab, OptT join_out, OptT join_argmax,
                    int join_H, int join_W, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
                    double fin_eps, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
-                   OptT bwd_dbeta) {
+                   OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
+                   int pj_reps) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -139,6 +140,22 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
     p.bwd.dx = ptr<bf16_t>(*bwd_dx, "bwd_dx");
     p.bwd.dgamma = optr<float>(bwd_dgamma, "bwd_dgamma");
     p.bwd.dbeta = optr<float>(bwd_dbeta, "bwd_dbeta");
+  }
+  if (pj_v) {                       // decoder node join at half resolution (launch.h PoolJoinEpi)
+    TORCH_CHECK(pj_out && ks == 3 && stride == 1 && Ho % 2 == 0 && Wo % 2 == 0 && !p.stats && !p.bias &&
+                !p.node.y && !join_mode, "conv_igemm: pj_* is a 3x3 dgrad epilogue (no stats / bias / node / join)");
+    const int64_t hn = (int64_t)B * (Ho / 2) * (Wo / 2) * N;
+    TORCH_CHECK(pj_v->numel() == hn && pj_out->numel() == hn && (!pj_add || pj_add->numel() == hn) &&
+                (!pj_sy || (pj_sy->numel() == hn && pj_sab && pj_sab->numel() >= 4 * N && pj_sums &&
+                            pj_sums->numel() >= (int64_t)(pj_reps < 1 ? 1 : pj_reps) * 2 * N)),
+                "conv_igemm: pj tensor sizes");
+    p.pj.v = ptr<const bf16_t>(*pj_v, "pj_v");
+    p.pj.add = optr<const bf16_t>(pj_add, "pj_add");
+    p.pj.out = ptr<bf16_t>(*pj_out, "pj_out");
+    p.pj.sy = optr<const bf16_t>(pj_sy, "pj_sy");
+    p.pj.sab = optr<const float>(pj_sab, "pj_sab");
+    p.pj.sums = p.pj.sy ? ptr<float>(*pj_sums, "pj_sums") : nullptr;
+    p.pj.reps = pj_reps < 1 ? 1 : pj_reps;
   }
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
@@ -686,7 +703,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3,
         py::arg("bwd_y") = py::none(), py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(),
         py::arg("bwd_reps") = 1, py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(),
-        py::arg("bwd_dbeta") = py::none());
+        py::arg("bwd_dbeta") = py::none(), py::arg("pj_v") = py::none(), py::arg("pj_add") = py::none(),
+        py::arg("pj_out") = py::none(), py::arg("pj_sy") = py::none(), py::arg("pj_sab") = py::none(),
+        py::arg("pj_sums") = py::none(), py::arg("pj_reps") = 1);
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;

@@ -281,6 +281,41 @@ CFL_DEVICE uint4 bnb_apply8(const uint4& gv, const uint4& yv, const float* co, i
   return pack8(o);
 }
 
+// One half-resolution pixel of a PoolJoinEpi (launch.h) from the four bf16 conv outputs of its 2x2 block and the
+// (prefetched) mask source vv, addend av (has_add) and sums source syv (has_sy), in node_bwd's order
+// (0 + masked((o00 + o01) + (o10 + o11)) + add, one rounding); accumulates the BN-backward sums from the rounded
+// value (mean / rstd of the sab rows in mean8 / rstd8). Returns the stored bf16 vector.
+CFL_DEVICE uint4 pool_join8(const uint4 (&o)[4], const uint4& vv, const uint4& av, const uint4& syv, bool has_add,
+                            bool has_sy, const float* mean8, const float* rstd8, float* s0, float* s1) {
+  float u[4][8], v[8], g[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) unpack8(o[q], u[q]);
+  unpack8(vv, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    g[j] = 0.f;                                   // node_bwd's accumulation, bit for bit (signed zeros included)
+    g[j] += v[j] > 0.f ? (u[0][j] + u[1][j]) + (u[2][j] + u[3][j]) : 0.f;
+  }
+  if (has_add) {
+    float a[8];
+    unpack8(av, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] += a[j];
+  }
+  const uint4 gv = pack8(g);
+  if (has_sy) {
+    float gr[8], y[8];
+    unpack8(gv, gr);
+    unpack8(syv, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0[j] += gr[j];
+      s1[j] += gr[j] * (y[j] - mean8[j]) * rstd8[j];
+    }
+  }
+  return gv;
+}
+
 CFL_DEVICE float xform1(float v, const InXform& t, int c) {
   if (t.ab) v = fmaf(t.ab[c], v, t.ab[t.C + c]);
   if (t.relu) v = fmaxf(v, 0.f);

@@ -35,7 +35,9 @@ __device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r
 // instead of one per tap, and no per-tap global-load latency on the critical path. Used for BN <= 64.
 // BWD (WB only): the halo is the BN-backward apply of (x = g, p.bwd.y) (common.h BnBwdIn), loaded raw and applied
 // after the previous chunk's MFMAs; the N-block-0 blocks store the tile's interior dx (each input pixel once).
-template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false>
+// PJ: the decoder node join epilogue (launch.h PoolJoinEpi) - its own instantiation, so the registers of its
+// prefetched operands never cost the plain convs occupancy.
+template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false, bool PJ = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
@@ -206,6 +208,26 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   const int fq = lane >> 4;
   const int brow = wn * TN + (lane & 15);
 
+  // decoder node join (PoolJoinEpi): this thread's half-resolution pixel (one per thread: HB <= rows per pass)
+  // and its mask / addend / sums-source vectors, loaded now so they are in flight during the K loop
+  constexpr bool pj = PJ;
+  static_assert(!PJ || BM / 4 <= NT / (BN_ / 8), "one half-resolution pixel per thread");
+  uint4 pjv = make_uint4(0, 0, 0, 0), pja = pjv, pjy = pjv;
+  size_t pjoff = 0;
+  bool pjok = false;
+  if constexpr (PJ) {
+    constexpr int CGp = BN_ / 8, HTW = TW / 2, HB = BM / 4;
+    const int hr = tid / CGp, hy = hr / HTW, hx = hr % HTW;
+    const int oy = ty0 + 2 * hy, ox = tx0 + 2 * hx;
+    pjok = hr < HB && oy < p.Ho && ox < p.Wo;
+    pjoff = (((size_t)b * (p.Ho >> 1) + (oy >> 1)) * (p.Wo >> 1) + (ox >> 1)) * p.N + nBlock + (tid % CGp) * 8;
+    if (pjok) {
+      pjv = *reinterpret_cast<const uint4*>(p.pj.v + pjoff);
+      if (p.pj.add) pja = *reinterpret_cast<const uint4*>(p.pj.add + pjoff);
+      if (p.pj.sy) pjy = *reinterpret_cast<const uint4*>(p.pj.sy + pjoff);
+    }
+  }
+
   f4v acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -346,6 +368,20 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   float s[2][8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) s[0][q] = s[1][q] = 0.f;
+  if constexpr (PJ) {
+    float pm[8], pr[8];
+    load_f8_or(p.pj.sab + 2 * p.N + nBlock + cg * 8, p.pj.sy != nullptr, 0.f, pm);
+    load_f8_or(p.pj.sab + 3 * p.N + nBlock + cg * 8, p.pj.sy != nullptr, 0.f, pr);
+    constexpr int HTW = TW / 2;
+    if (pjok) {
+      const int hr = tid / CG, hy = hr / HTW, hx = hr % HTW;
+      uint4 o4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o4[q] = *reinterpret_cast<const uint4*>(&sC[(2 * hy + (q >> 1)) * TW + 2 * hx + (q & 1)][cg * 8]);
+      *reinterpret_cast<uint4*>(p.pj.out + pjoff) = pool_join8(o4, pjv, pja, pjy, p.pj.add != nullptr,
+                                                               p.pj.sy != nullptr, pm, pr, s[0], s[1]);
+    }
+  } else {
 #pragma unroll
   for (int r0 = 0; r0 < BM; r0 += ROWS_PER_PASS) {
     const int row = r0 + tid / CG;
@@ -367,7 +403,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       *reinterpret_cast<uint4*>(p.y + off) = v;
     }
   }
-  if (p.stats || node) {
+  }
+  if (p.stats || node || (pj && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       for (int o = CG; o < 64; o <<= 1) {
@@ -382,13 +419,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
     }
     __syncthreads();
-    float* rep = node ? p.node.sums + (size_t)(tile_id % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+    float* rep = pj ? p.pj.sums + (size_t)(tile_id % (p.pj.reps > 1 ? p.pj.reps : 1)) * 2 * p.N
+               : node ? p.node.sums + (size_t)(tile_id % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
                       : p.stats + (size_t)(tile_id % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
-    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
+    if (!node && !pj) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -402,8 +440,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 // only when it is written to LDS (after the MFMAs), so the loads are never waited for early. BN statistics /
 // BN-node sums accumulate in registers across the block's tiles: one set of channel atomics per block.
 // LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
-template <int TH, int TW, int CH, bool BWD = false>
-__global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
+template <int TH, int TW, int CH, bool BWD = false, bool PJ = false>
+__global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
   constexpr int BN_ = 32, WM = 4;
   constexpr int BM = TH * TW;
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
@@ -530,8 +568,12 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel
   const int fq = lane >> 4;
   const int cg = tid % CG;
   const bool node = p.node.y != nullptr;
+  constexpr bool pj = PJ;
   NodeCoef nk;
   if (node) node_coef_load(p.node.ab, p.N, nBlock + cg * 8, nk);
+  float pm[8], pr[8];
+  load_f8_or(p.pj.sab + 2 * p.N + nBlock + cg * 8, pj && p.pj.sy != nullptr, 0.f, pm);
+  load_f8_or(p.pj.sab + 3 * p.N + nBlock + cg * 8, pj && p.pj.sy != nullptr, 0.f, pr);
   float biasf[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) biasf[j] = p.bias ? p.bias[nBlock + j * 16 + (lane & 15)] : 0.f;
@@ -547,6 +589,19 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel
   for (; item < n_items; item += gridDim.x) {
     const int next = item + gridDim.x;
     if (next < n_items) load_halo(next);               // in flight during this tile's MFMAs
+    // decoder node join: this tile's half-resolution vectors (one pixel per thread), in flight during the MFMAs
+    uint4 pjv = make_uint4(0, 0, 0, 0), pja = pjv, pjy = pjv;
+    size_t pjoff = 0;
+    const int pjr = tid / CG;
+    if (PJ && pjr < BM / 4) {
+      int pb, pty0, ptx0;
+      tile_of(item, pb, pty0, ptx0);
+      const int hy = pjr / (TW / 2), hx = pjr % (TW / 2);
+      pjoff = (((size_t)pb * (p.Ho >> 1) + (pty0 >> 1) + hy) * (p.Wo >> 1) + (ptx0 >> 1) + hx) * p.N + nBlock + cg * 8;
+      pjv = *reinterpret_cast<const uint4*>(p.pj.v + pjoff);
+      if (p.pj.add) pja = *reinterpret_cast<const uint4*>(p.pj.add + pjoff);
+      if (p.pj.sy) pjy = *reinterpret_cast<const uint4*>(p.pj.sy + pjoff);
+    }
     f4v acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -584,6 +639,18 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel
     if (next < n_items) store_halo();
     int b, ty0, tx0;
     tile_of(item, b, ty0, tx0);
+    if constexpr (PJ) {                                 // decoder node join at half resolution (PoolJoinEpi)
+      constexpr int HTW = TW / 2, HB = BM / 4;
+      static_assert(HB <= ROWS_PER_PASS, "one half-resolution pass");
+      if (pjr < HB) {
+        const int hy = pjr / HTW, hx = pjr % HTW;
+        uint4 o4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o4[q] = *reinterpret_cast<const uint4*>(&sC[(2 * hy + (q >> 1)) * TW + 2 * hx + (q & 1)][cg * 8]);
+        *reinterpret_cast<uint4*>(p.pj.out + pjoff) = pool_join8(o4, pjv, pja, pjy, p.pj.add != nullptr,
+                                                                 p.pj.sy != nullptr, pm, pr, s[0], s[1]);
+      }
+    } else {
 #pragma unroll
     for (int r0 = 0; r0 < BM; r0 += ROWS_PER_PASS) {
       const int row = r0 + tid / CG;
@@ -603,9 +670,10 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel
       }
       *reinterpret_cast<uint4*>(p.y + off) = v;
     }
+    }
     __syncthreads();                                    // next halo visible, C tile consumed
   }
-  if (p.stats || node) {
+  if (p.stats || node || (pj && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       for (int o = CG; o < 64; o <<= 1) {
@@ -621,13 +689,14 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD ? 3 : 2) void conv3x3_ws_kernel
     }
     __syncthreads();
     const int rb = blockIdx.x / nb;                     // replica row (blocks of one column block spread)
-    float* rep = node ? p.node.sums + (size_t)(rb % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
+    float* rep = pj ? p.pj.sums + (size_t)(rb % (p.pj.reps > 1 ? p.pj.reps : 1)) * 2 * p.N
+               : node ? p.node.sums + (size_t)(rb % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
                       : p.stats + (size_t)(rb % STAT_REPLICAS) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
-    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
+    if (!node && !pj) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -653,7 +722,9 @@ void launch_ws(const ConvParams& p, hipStream_t st) {
   grid = grid / nb * nb;
   if (grid < nb) grid = nb;
   if (grid > items) grid = items;
-  if (p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  if (p.pj.v && p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  else if (p.pj.v) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  else if (p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
   else hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
 }
 
@@ -665,6 +736,14 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
   const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   dim3 grid(tiles, p.N / BN_, splits);
   if constexpr (WB) {
+    if (p.pj.v && p.bwd.y) {
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
+      return 1;
+    }
+    if (p.pj.v) {
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, false, true>), grid, dim3(NT), 0, st, p, per, nullptr);
+      return 1;
+    }
     if (p.bwd.y) {
       hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per,
                          splits > 1 ? p.ws : nullptr);
@@ -739,7 +818,8 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
   // LDS-DMA ring, no split-K (it has no in-launch BN-finalize tail: a BnFinal request keeps the other kernels)
   // (the folded BN backward, p.bwd, runs on the whole-chunk / weight-stationary kernels: conv3x3_bwd_foldable)
-  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y) return conv3x3_deep(p, st);
+  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y && !p.pj.v)
+    return conv3x3_deep(p, st);
   if (ws_eligible(p)) {                     // weight-stationary persistent tiles (no split-K)
     const bool w16 = p.Wo >= 16;
     if (p.Cin == 32) {
@@ -751,8 +831,9 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
+  if (p.pj.v && !use_wb(p)) return 8;        // the node join needs one half-resolution pixel per thread (BN <= 64)
   int splits = conv3x3_splits(p);
-  if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
+  if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N || p.pj.v)) splits = 1;
   const bool w16 = p.Wo >= 16;
   if (small_tiles(p)) {
     splits = launch<8, 8, 32, 2, 2, true>(p, 1, st);

@@ -492,6 +492,7 @@ int conv_igemm_splits(const ConvParams& p) {
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
   if (p.join.mode && (p.ks != 1 || p.stats || p.node.y || p.N % 8)) return 5;   // joins: 1x1 residual convs only
+  if (p.pj.v && !use3x3(p)) return 7;     // the decoder node join lives in the 3x3 halo kernels' epilogues
   if (p.bwd.y) {
     if (p.xf.ab || p.xf.relu || p.up_in || p.join.mode || p.Cin > BNB_MAX_C || p.bwd.dx == nullptr) return 6;
     if (!bwd_foldable(p)) return bwd_unfolded(p, st);

@@ -53,6 +53,22 @@ struct ConvJoin {
   int H, W;
 };
 
+// Decoder node join in a 3x3 data-gradient conv's epilogue (backward of x_lo_{k-1} -> UpSampling2D -> ReLU ->
+// Conv2DTranspose, plus the residual conv's input gradient): the conv output o (full resolution, the gradient of
+// the upsampled input) is never stored; instead, at half resolution,
+//   out[h][w] = [v[h][w] > 0] * sum_{2x2} o[2h+dy][2w+dx] + add[h][w]
+// and, if sums != nullptr, the BN-backward sums of the BN node out is also the gradient of (sum g, sum g * xhat,
+// xhat from sy with the sab rows) - node_bwd(GM_SUM2X2 masked, GM_SAME, sy / sab) in the producer.
+struct PoolJoinEpi {
+  const bf16_t* v;     // nullptr = off: ReLU-mask source [B, Ho/2, Wo/2, N] (the conv's raw input)
+  const bf16_t* add;   // addend [B, Ho/2, Wo/2, N] or nullptr
+  bf16_t* out;         // [B, Ho/2, Wo/2, N]
+  const bf16_t* sy;    // BN input for the sums' xhat (same layout) or nullptr (no sums)
+  const float* sab;    // its BN rows (mean, rstd at rows 2, 3)
+  float* sums;         // [reps][2][N]
+  int reps;
+};
+
 struct ConvParams {
   const bf16_t* x;     // [B, Hin, Win, Cin] NHWC (physical; logical = upsample2 if up_in)
   const bf16_t* wt;    // [N][K] packed bf16 weights, K = ks*ks*Cin, k = (ky*ks + kx)*Cin + ci
@@ -67,6 +83,7 @@ struct ConvParams {
   int64_t ws_elems;
   int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
   BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
+  PoolJoinEpi pj;      // optional decoder node join (3x3 s1 dgrads, even tiles); excludes stats / bias / node / split
   ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
   BnFinal fin;         // optional in-launch finalize of `stats` (run by the launch that completes them)
   BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;

@@ -1290,7 +1290,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
@@ -1411,3 +1411,42 @@ def test_dw_bwd_residual_join_matches_node_bwd(B, H, W, C, bn):
     assert torch.equal(out, ref), int((out != ref).sum())
     if bn:
         assert torch.allclose(sums.view(4, -1).sum(0), s_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,H,Cin,N,tune", [(2, 32, 64, 128, ""), (2, 16, 128, 256, ""), (2, 24, 32, 64, "ws"),
+                                            (2, 16, 64, 64, "small"), (2, 20, 64, 64, "")])
+def test_conv3x3_pool_join_matches_node_bwd(B, H, Cin, N, tune):
+    """Decoder node join in the 3x3 dgrad epilogue (conv_igemm pj_*: 2x2 sum of the conv output, ReLU mask from the
+    half-resolution input, + residual gradient, BN-backward sums with xhat from another tensor) equals the conv into
+    dxin followed by node_bwd(GM_SUM2X2 masked, GM_SAME, sy / sab): output bit for bit, sums to float order, on the
+    per-tile (incl. ragged 20x20), weight-stationary and 8x8-tile kernels."""
+    torch.manual_seed(57)
+    C_ = hip()
+    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2)}
+    if tune:
+        C_.set_tune(*keys[tune])
+    try:
+        h2 = H // 2
+        xb, _ = bf(torch.randn(B, H, H, Cin))
+        wt, _ = bf(torch.randn(N, 9 * Cin) * 0.05)
+        vb, _ = bf(torch.randn(B, h2, h2, N))
+        ab_, _ = bf(torch.randn(B, h2, h2, N))
+        syb, _ = bf(torch.randn(B, h2, h2, N))
+        sab = ab_for(N, 58)[0]
+        sab[2 * N:3 * N], sab[3 * N:] = torch.randn(N) * 0.1, torch.rand(N) + 0.5
+        sab = sab.to(DEV)
+        dxin = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+        C_.conv_igemm(xb, wt, None, dxin, None, None, 0, B, H, H, Cin, 0, H, H, N, 3, 1, 1, 1)
+        ref = torch.zeros(B, h2, h2, N, dtype=torch.int16, device=DEV)
+        s_ref = torch.zeros(2 * N, device=DEV)
+        C_.node_bwd(dxin, 3, 1, ab_, 1, 0, None, vb, None, 0, ref, s_ref, B, h2, h2, N, 1, sy=syb, sab=sab)
+        out = torch.zeros_like(ref)
+        sums = torch.zeros(4 * 2 * N, device=DEV)
+        C_.conv_igemm(xb, wt, None, torch.zeros_like(dxin), None, None, 0, B, H, H, Cin, 0, H, H, N, 3, 1, 1, 1,
+                      pj_v=vb, pj_add=ab_, pj_out=out, pj_sy=syb, pj_sab=sab, pj_sums=sums, pj_reps=4)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), int((out != ref).sum())
+        assert torch.allclose(sums.view(4, -1).sum(0), s_ref, rtol=1e-4, atol=1e-3)
+    finally:
+        if tune:
+            C_.set_tune(keys[tune][0], 0)
