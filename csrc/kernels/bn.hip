@@ -23,10 +23,19 @@ constexpr int FT = 1024;
 __device__ __forceinline__ void replica_sums(const float* stats, int C, float (*part)[FT], float& s, float& s2) {
   const int per = FT / C, c = threadIdx.x % C, j = threadIdx.x / C;
   float a = 0.f, b = 0.f;
-#pragma unroll 4
-  for (int r = j; r < STAT_REPLICAS; r += per) {
-    a += stats[r * 2 * C + c];
-    b += stats[r * 2 * C + C + c];
+  // fully unrolled with a guard: a thread's (up to STAT_REPLICAS / 4 for C = 256) loads all issue before the adds
+  // (an unroll-by-4 runtime loop was two dependent memory round trips for C >= 128)
+  float va[STAT_REPLICAS / 4], vb[STAT_REPLICAS / 4];
+#pragma unroll
+  for (int k = 0; k < STAT_REPLICAS / 4; ++k) {
+    const int r = j + k * per;
+    va[k] = r < STAT_REPLICAS ? stats[r * 2 * C + c] : 0.f;
+    vb[k] = r < STAT_REPLICAS ? stats[r * 2 * C + C + c] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < STAT_REPLICAS / 4; ++k) {
+    a += va[k];
+    b += vb[k];
   }
   part[0][threadIdx.x] = a;
   part[1][threadIdx.x] = b;
@@ -358,7 +367,7 @@ bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
 int bn_finalize(const float* stats, const float* gamma, const float* beta, const float* mmean, const float* mvar,
                 float* ab, int C, float count, float eps, int train, hipStream_t st) {
-  if (C < 1 || C > FT || FT % C) return 1;
+  if (C < 1 || C > FT / 4 || FT % C) return 1;          // >= 4 replica phases per channel (replica_sums)
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(FT), 0, st, stats, gamma, beta, mmean, mvar, ab, C, count,
                      eps, train);
   return hipGetLastError() == hipSuccess ? 0 : 3;
