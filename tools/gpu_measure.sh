@@ -31,6 +31,14 @@ while read -r counters; do
       python $R/bench.py --profile-steps 6 > $O/pmc_p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $O/pmc_p$i.log; exit 1; }
 done < $R/tools/pmc_passes.txt
 python $R/tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt || exit 1
+i=0
+while read -r counters; do
+  [ -z "$counters" ] && continue
+  i=$((i+1))
+  timeout -s KILL 150 rocprofv3 --pmc $counters --output-format csv -d $O/pmc_lat/p$i -o run -- \
+      python $R/bench.py --profile-steps 6 > $O/pmc_lat_p$i.log 2>&1 || { echo "latency pass $i failed"; tail -5 $O/pmc_lat_p$i.log; exit 1; }
+done < $R/tools/pmc_latency_passes.txt
+python $R/tools/pmc_latency.py $O/pmc_lat 40 > $O/pmc_latency.txt || exit 1
 cd $R
 timeout -k 10 400 python tools/kbench.py --roofline --reps 20 > $O/roofline.txt 2>&1 || { tail -5 $O/roofline.txt; exit 1; }
 tail -2 $O/roofline.txt

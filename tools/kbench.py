@@ -34,9 +34,9 @@ class Recorder:
             return f
 
         def wrap(*a, **k):
-            if name == "conv_wgrad_batch":       # the engine's deferred weight gradients: time each one alone
+            if name in ("conv_wgrad_batch", "dw_wgrad_batch"):   # deferred weight gradients: time each one alone
                 for c in a[0]:
-                    self.calls.append(("conv_wgrad", tuple(c), {}))
+                    self.calls.append((name[:-len("_batch")], tuple(c), {}))
             else:
                 self.calls.append((name, a, k))
             return f(*a, **k)
@@ -117,7 +117,7 @@ def main():
             roof["flops"] += fl
             roof["floor"] += floor
             roof["time"] += t
-            line = (f"{t:8.1f}  {floor:7.1f} {100 * floor / max(t, 1e-9):5.0f}%  {by / 1e6:8.2f} MB {by / t / 1e3:6.2f} "
+            line = (f"{t:8.1f}  {floor:7.1f} {100 * floor / max(t, 1e-9):5.0f}%  {by / 1e6:8.2f} MB {by / t / 1e6:6.2f} "
                     f"TB/s  {fl / t / 1e6:7.1f} TF/s  {shape_key(name, a, k)}")
         if args.variants and name in ("conv_wgrad", "conv_igemm", "dw_fwd", "dw_dgrad", "dw_wgrad"):
             for algo in ((1, 2, 0) if name.startswith("dw_") else (1, 0)):

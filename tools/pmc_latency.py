@@ -1,10 +1,9 @@
 """Per-kernel memory-latency view from rocprofv3 PMC passes (tools/pmc_latency_passes.txt via gpurun):
 
-  vmem lat   SQ_INST_LEVEL_VMEM / SQ_INSTS_VMEM  - average cycles a vector-memory instruction is in flight
   L1->L2 lat TCP_TCC_READ_REQ_LATENCY_sum / TCP_TCC_READ_REQ_sum - average cycles of an L1 miss served by L2 / beyond
   L2 hit     TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
-  waves      SQ_LEVEL_WAVES / SQ_BUSY_CYCLES - average resident waves (per SE-level counter instance)
   wait       SQ_WAIT_ANY / SQ_WAVE_CYCLES - share of wave time waiting on anything (memory, barriers, dependencies)
+  vmem/wave  SQ_INSTS_VMEM / SQ_WAVES - vector-memory instructions per wave
 
     python tools/pmc_latency.py gpurun_out/pmc_lat [top]
 """
@@ -38,14 +37,13 @@ def ratio(c, a, b):
     return c[a] / c[b] if c.get(b) else float("nan")
 
 
-print(f"{'kernel':58s} {'ms':>7s} {'vmemlat':>8s} {'L1>L2lat':>9s} {'L2hit':>6s} {'waves':>6s} {'wait':>5s}")
+print(f"{'kernel':58s} {'ms':>7s} {'L1>L2lat':>9s} {'L2hit':>6s} {'wait':>5s} {'vmem/wave':>9s}")
 for k in sorted(tot, key=lambda k: -dur[k])[:top]:
     c = tot[k]
-    vm = ratio(c, "SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM")
+    vm = ratio(c, "SQ_INSTS_VMEM", "SQ_WAVES")
     l2 = ratio(c, "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum")
     hit = c.get("TCC_HIT_sum", 0.0)
     miss = c.get("TCC_MISS_sum", 0.0)
     hr = hit / (hit + miss) if hit + miss else float("nan")
-    wv = ratio(c, "SQ_LEVEL_WAVES", "SQ_BUSY_CYCLES")
     wt = ratio(c, "SQ_WAIT_ANY", "SQ_WAVE_CYCLES")
-    print(f"{k[:58]:58s} {dur[k] / 1e6:7.3f} {vm:8.0f} {l2:9.0f} {100 * hr:5.1f}% {wv:6.1f} {100 * wt:4.0f}%")
+    print(f"{k[:58]:58s} {dur[k] / 1e6:7.3f} {l2:9.0f} {100 * hr:5.1f}% {100 * wt:4.0f}% {vm:9.1f}")
