@@ -907,10 +907,12 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
 }
 
 // (grid size, rows per segment) of the row-streaming kernels
-void stream_shape(const DwParams& p, int& blocks, int& seg_rows) {
+// target: grid size to aim for (one round of resident blocks: 256 CUs x blocks per CU)
+void stream_shape(const DwParams& p, int& blocks, int& seg_rows, int target = 0) {
   const int steps = (p.H + dws::SR - 1) / dws::SR;
   const int strips = p.B * ((p.W + 31) / 32) * (p.C / dws::CT);
-  const int target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 768;   // A/B-measured (256 / 384 / 512 / 768 / 1024 / 2048)
+  if (target <= 0)
+    target = cfl_tune(TUNE_DW_STREAM_BLOCKS) > 0 ? cfl_tune(TUNE_DW_STREAM_BLOCKS) : 768;   // A/B-measured (256 / 384 / 512 / 768 / 1024 / 2048)
   int nseg = (target + strips - 1) / strips;
   nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
   seg_rows = ((steps + nseg - 1) / nseg) * dws::SR;
@@ -971,8 +973,10 @@ int dw_bwd(const DwParams& p, hipStream_t st) {
     const int rc = dw_dgrad(p, st);
     return rc ? rc : dw_wgrad(p, st);
   }
+  // two rings (56 KB LDS) and 247 VGPRs: 2 blocks per CU, so one round of resident blocks is 512 (the single-
+  // pass kernels' 768 left a half-empty second round)
   int blocks, seg_rows;
-  stream_shape(p, blocks, seg_rows);
+  stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 512);
   hipLaunchKernelGGL(dw_bwd_stream_kernel, dim3(blocks), dim3(NT), 0, st, p, p.replicas > 1 ? p.replicas : 1,
                      seg_rows);
   return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -348,6 +348,7 @@ enum TuneKey {
   TUNE_WGRAD1_BLOCKS = 18,     // generic (1x1) wgrad: target blocks per layer (default 256)
   TUNE_WGRAD1_MINPIX = 19,     // generic (1x1) wgrad: min pixels per block (default 512)
   TUNE_NODE_BWD_IPT = 20,      // node_bwd: items in flight per thread (2 or 4; default 2)
+  TUNE_DW_BWD_BLOCKS = 21,     // fused depthwise backward: target grid size (default 512)
   TUNE_N = 24
 };
 int cfl_tune(int key);

@@ -141,7 +141,7 @@ def main():
     if args.roofline and roof["time"]:
         print(f"\nwhole step (isolated replays, L2/Infinity-Cache warm): {roof['time']:.1f} us measured, minimum "
               f"{roof['bytes'] / 1e6:.1f} MB + {roof['flops'] / 1e9:.1f} GFLOP -> roofline floor {roof['floor']:.1f} us "
-              f"({100 * roof['floor'] / roof['time']:.0f}% of measured; {roof['bytes'] / roof['time'] / 1e3:.2f} TB/s "
+              f"({100 * roof['floor'] / roof['time']:.0f}% of measured; {roof['bytes'] / roof['time'] / 1e6:.2f} TB/s "
               f"average over the step)")
 
 
