@@ -409,7 +409,8 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
       ((p.H | p.W) & 1) == 0 && cfl_tune(TUNE_NODE_POOL2X2) != 1) {
     const int64_t items2 = (int64_t)p.B * (p.H / 2) * (p.W / 2) * (p.C / 8);
     int b2 = (int)((items2 + NT - 1) / NT);
-    if (b2 > cap) b2 = cap;
+    const int pcap = cfl_tune(TUNE_NODE_POOL_BLOCKS) > 0 ? cfl_tune(TUNE_NODE_POOL_BLOCKS) : cap;
+    if (b2 > pcap) b2 = pcap;
     if (b2 < 1) b2 = 1;
     hipLaunchKernelGGL(node_pool_bwd_kernel, dim3(b2), dim3(NT), 0, st, p);
     return hipGetLastError() == hipSuccess ? 0 : 3;
@@ -425,7 +426,8 @@ int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
   if (p.C % 8 || !pow2(p.C / 8)) return 1;
   if (p.C > BNB_MAX_C || p.sum_reps > BNB_MAX_REPS) return 1;
   int blocks = (int)(((int64_t)p.M * (p.C / 8) + BBA_IPT * NT - 1) / (BBA_IPT * NT));
-  if (blocks > 1024) blocks = 1024;
+  const int cap = cfl_tune(TUNE_BBA_BLOCKS) > 0 ? cfl_tune(TUNE_BBA_BLOCKS) : 1024;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
