@@ -276,6 +276,9 @@ class UNetEngine:
         # decoder node join (2x2 sum of the convT1 input gradient, ReLU mask, + residual gradient, BN_B(k-1) sums) in
         # the convT1 dgrad's epilogue (CFL_POOL_JOIN=0: dxin stored + a node_bwd pass)
         self.fuse_pool_join = os.environ.get("CFL_POOL_JOIN", "1") != "0"
+        # BN finalize done by the layer's first consumer from the replica sums (CFL_FIN_CONSUMER=0: a 1-block
+        # bn_finalize launch per BN layer)
+        self.fin_in_consumer = os.environ.get("CFL_FIN_CONSUMER", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
@@ -385,9 +388,22 @@ class UNetEngine:
         return dict(fin_ab=b["ab"], fin_gamma=self.P(name, "gamma"), fin_beta=self.P(name, "beta"),
                     fin_ctr=self.bn_ctr[i:i + 1], fin_count=float(self.bn_count(name)), fin_eps=self.bn_eps)
 
-    def _bn_final(self, name: str, train: bool) -> torch.Tensor:
+    def _xfin(self, name: str, train: bool) -> Dict[str, object]:
+        """Consumer-side BN finalize kwargs: the consumer computes layer ``name``'s coefficients from its replica
+        sums (and writes its ab rows) instead of a bn_finalize launch (empty: ab is final already)."""
+        if not train or self.bn_tail or not self.fin_in_consumer:
+            return {}
+        return dict(xfin_stats=self.bn[name]["stats"], xfin_gamma=self.P(name, "gamma"),
+                    xfin_beta=self.P(name, "beta"), xfin_count=float(self.bn_count(name)), xfin_eps=self.bn_eps)
+
+    def _jfin(self, name: str, train: bool) -> Dict[str, object]:
+        """_xfin for a residual conv's join epilogue (the join BN's first consumer)."""
+        return {"j" + k[1:]: v for k, v in self._xfin(name, train).items()}
+
+    def _bn_final(self, name: str, train: bool, consumer: bool = False) -> torch.Tensor:
+        """ab of BN layer ``name``; consumer=True: its next consumer finalizes it (_xfin), nothing is launched."""
         b = self.bn[name]
-        if not train or self.bn_tail:
+        if not train or self.bn_tail or (consumer and self.fin_in_consumer):
             return b["ab"]          # inference: written by forward()'s bn_eval_coefs; train: by the producer's tail
         self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
                            self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
@@ -430,11 +446,11 @@ class UNetEngine:
 
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
               Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor],
-              join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None) -> None:
+              join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None, **extra) -> None:
         pad = (ks - 1) // 2 if stride == 1 else 0
         B = self.B
         self._igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
-                    N, ks, stride, pad, pad, join=join, fin=fin)
+                    N, ks, stride, pad, pad, join=join, fin=fin, **extra)
 
     def forward(self, train: bool = True) -> None:
         C, B, r, A = self.C, self.B, self.r, self.act
@@ -447,23 +463,27 @@ class UNetEngine:
         st = self.bn[e_bn]["stats"] if train else None
         C.entry_fwd(self.images, self.idx, self.P(e_conv, "kernel"), self.P(e_conv, "bias"), A["y0"], st, B, self.S,
                     ENTRY_FILTERS, **self._fin(e_bn, train))
-        ab0 = self._bn_final(e_bn, train)
+        ab0 = self._bn_final(e_bn, train, consumer=True)
         x = Lazy(A["y0"], ab0, 1, r[0], ENTRY_FILTERS)     # a0 = relu(BN0(y0))
         for k, F in enumerate(ENC_FILTERS):
             s1, b1, s2, b2, rc = (next(n) for _ in range(5))
             H = r[k]
-            C.dw_fwd(x.t, self.P(s1, "depthwise_kernel"), A[f"e{k}_d1"], x.ab, 1, B, H, H, x.C)
+            # the depthwise conv is the first consumer of BN0 (k = 0): it finalizes it
+            C.dw_fwd(x.t, self.P(s1, "depthwise_kernel"), A[f"e{k}_d1"], x.ab, 1, B, H, H, x.C,
+                     **(self._xfin(e_bn, train) if k == 0 else {}))
             self._conv(Lazy(A[f"e{k}_d1"], None, 0, H, x.C), s1, PK_PW, A[f"e{k}_y1"], F, 1, 1, 0, H,
                        self.P(s1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
-            ab1 = self._bn_final(b1, train)
-            C.dw_fwd(A[f"e{k}_y1"], self.P(s2, "depthwise_kernel"), A[f"e{k}_d2"], ab1, 1, B, H, H, F)
+            ab1 = self._bn_final(b1, train, consumer=True)
+            C.dw_fwd(A[f"e{k}_y1"], self.P(s2, "depthwise_kernel"), A[f"e{k}_d2"], ab1, 1, B, H, H, F,
+                     **self._xfin(b1, train))
             self._conv(Lazy(A[f"e{k}_d2"], None, 0, H, F), s2, PK_PW, A[f"e{k}_y2"], F, 1, 1, 0, H,
                        self.P(s2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train))
-            ab2 = self._bn_final(b2, train)
+            ab2 = self._bn_final(b2, train, consumer=self.fuse_join)
             if self.fuse_join:   # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
                 self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
                            join=dict(join_mode=C.JOIN_POOL, join_y=A[f"e{k}_y2"], join_ab=ab2,
-                                     join_out=A[f"e{k}_x"], join_argmax=A[f"e{k}_am"], join_H=H, join_W=H))
+                                     join_out=A[f"e{k}_x"], join_argmax=A[f"e{k}_am"], join_H=H, join_W=H,
+                                     **self._jfin(b2, train)))
             else:
                 self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None)
                 C.pool_res_fwd(A[f"e{k}_y2"], ab2, A[f"e{k}_res"], A[f"e{k}_x"], A[f"e{k}_am"], B, H, H, F)
@@ -475,14 +495,16 @@ class UNetEngine:
             up = 0 if k == 0 else 1
             self._convt(Lazy(prev.t, None, 1, prev.H, prev.C), t1, A[f"d{k}_c1"], F, up, Rk,
                         self.P(t1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
-            abA = self._bn_final(b1, train)
+            abA = self._bn_final(b1, train, consumer=True)       # finalized by the convT2 forward below
             self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
-                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train))
-            abB = self._bn_final(b2, train)
+                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train),
+                        **self._xfin(b1, train))
+            abB = self._bn_final(b2, train, consumer=self.fuse_join)
             if self.fuse_join:   # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
                 self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None,
                            join=dict(join_mode=C.JOIN_ADD_UP if up else C.JOIN_ADD, join_y=A[f"d{k}_c2"],
-                                     join_ab=abB, join_out=A[f"d{k}_xlo"], join_H=Rk, join_W=Rk))
+                                     join_ab=abB, join_out=A[f"d{k}_xlo"], join_H=Rk, join_W=Rk,
+                                     **self._jfin(b2, train)))
             else:
                 self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
                 C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
@@ -690,12 +712,18 @@ class UNetEngine:
                             self.amax8 if step else None, self.n_views8)
 
     def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
-               bias: torch.Tensor, stats: Optional[torch.Tensor], fin: Optional[Dict[str, object]] = None) -> None:
+               bias: torch.Tensor, stats: Optional[torch.Tensor], fin: Optional[Dict[str, object]] = None,
+               **extra) -> None:
         """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled (maps of at least 8x8; smaller ones - only
-        at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel."""
+        at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel. ``extra``: consumer-side
+        finalize kwargs of the input's BN (bf16 path only)."""
         if not self.fp8 or Ho < 8:
-            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, fin=fin)
+            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, fin=fin, **extra)
             return
+        if extra:                              # the fp8 kernel reads a final ab
+            xs = extra
+            self.C.bn_finalize(xs["xfin_stats"], xs["xfin_gamma"], xs["xfin_beta"], xs["xfin_gamma"],
+                               xs["xfin_beta"], x.ab, x.C, xs["xfin_count"], xs["xfin_eps"], 1)
         B = self.B
         need = self.C.conv_splits_fp8(B, Ho, Ho, N, x.C)
         if need > 1 and need * B * Ho * Ho * N > self.ws.numel():

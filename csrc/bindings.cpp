@@ -73,6 +73,22 @@ BnNodeEpi node_epi_args(const OptT& node_y, const OptT& node_ab, const OptT& nod
   return e;
 }
 
+// BN finalize arguments of a consumer that computes its input's coefficients itself (launch.h BnStatsIn)
+BnStatsIn stats_in(const OptT& stats, const OptT& gamma, const OptT& beta, double count, double eps, int C,
+                   const OptT& ab) {
+  BnStatsIn f{};
+  if (!stats) return f;
+  TORCH_CHECK(gamma && beta && ab && count > 0 && stats->numel() >= (int64_t)STAT_REPLICAS * 2 * C &&
+              gamma->numel() >= C && beta->numel() >= C && ab->numel() >= 4 * C,
+              "consumer-side BN finalize: needs stats, gamma, beta and the ab destination");
+  f.stats = ptr<const float>(*stats, "fin_stats");
+  f.gamma = ptr<const float>(*gamma, "fin_gamma");
+  f.beta = ptr<const float>(*beta, "fin_beta");
+  f.count = (float)count;
+  f.eps = (float)eps;
+  return f;
+}
+
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
@@ -80,7 +96,9 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    int join_H, int join_W, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
                    double fin_eps, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
                    OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
-                   int pj_reps) {
+                   int pj_reps, OptT jfin_stats, OptT jfin_gamma, OptT jfin_beta, double jfin_count,
+                   double jfin_eps, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count,
+                   double xfin_eps) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -89,6 +107,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   p.y = ptr<bf16_t>(y, "y");
   p.stats = optr<float>(stats, "stats");
   p.xf = xf(ab, Cin, relu);
+  p.xfin = stats_in(xfin_stats, xfin_gamma, xfin_beta, xfin_count, xfin_eps, Cin, ab);
   p.B = B; p.Hin = Hin; p.Win = Win; p.Cin = Cin; p.up_in = up_in;
   p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
   p.M = B * Ho * Wo;
@@ -123,6 +142,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
     p.join.argmax = optr<uint8_t>(join_argmax, "join_argmax");
     p.join.H = join_H;
     p.join.W = join_W;
+    p.join.fin = stats_in(jfin_stats, jfin_gamma, jfin_beta, jfin_count, jfin_eps, N, join_ab);
   }
   if (bwd_y) {                      // BN-backward apply folded into the operand load (common.h BnBwdIn)
     TORCH_CHECK(bwd_ab && bwd_sums && bwd_dx, "conv_igemm: bwd_y needs bwd_ab, bwd_sums, bwd_dx");
@@ -245,13 +265,15 @@ DwParams dwp(int B, int H, int W, int C) {
   return p;
 }
 
-void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int B, int H, int W, int C, int algo) {
+void dw_fwd_op(at::Tensor x, at::Tensor w, at::Tensor y, OptT ab, int relu, int B, int H, int W, int C, int algo,
+               OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count, double xfin_eps) {
   DwParams p = dwp(B, H, W, C);
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
   p.w = ptr<const float>(w, "w");
   p.y = ptr<bf16_t>(y, "y");
   p.xf = xf(ab, C, relu);
+  p.xfin = stats_in(xfin_stats, xfin_gamma, xfin_beta, xfin_count, xfin_eps, C, ab);
   TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && y.numel() == x.numel() && w.numel() == 9 * C, "dw_fwd sizes");
   ok(dw_fwd(p, stream()), "dw_fwd");
 }
@@ -705,7 +727,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bwd_reps") = 1, py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(),
         py::arg("bwd_dbeta") = py::none(), py::arg("pj_v") = py::none(), py::arg("pj_add") = py::none(),
         py::arg("pj_out") = py::none(), py::arg("pj_sy") = py::none(), py::arg("pj_sab") = py::none(),
-        py::arg("pj_sums") = py::none(), py::arg("pj_reps") = 1);
+        py::arg("pj_sums") = py::none(), py::arg("pj_reps") = 1, py::arg("jfin_stats") = py::none(),
+        py::arg("jfin_gamma") = py::none(), py::arg("jfin_beta") = py::none(), py::arg("jfin_count") = 0.0,
+        py::arg("jfin_eps") = 1e-3, py::arg("xfin_stats") = py::none(), py::arg("xfin_gamma") = py::none(),
+        py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3);
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
@@ -723,7 +748,9 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD3_BLOCKS") = (int)TUNE_WGRAD3_BLOCKS;
   m.attr("TUNE_WGRAD3_MINTILES") = (int)TUNE_WGRAD3_MINTILES;
   m.def("dw_fwd", &dw_fwd_op, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("ab"), py::arg("relu"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("C"), py::arg("algo") = 0);
+        py::arg("H"), py::arg("W"), py::arg("C"), py::arg("algo") = 0, py::arg("xfin_stats") = py::none(),
+        py::arg("xfin_gamma") = py::none(), py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0,
+        py::arg("xfin_eps") = 1e-3);
   m.def("dw_dgrad", &dw_dgrad_op, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("B"), py::arg("H"),
         py::arg("W"), py::arg("C"), py::arg("algo") = 0, py::arg("node_y") = py::none(),
         py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,

@@ -51,28 +51,23 @@ __device__ __forceinline__ void replica_sums(const float* stats, int C, float (*
 __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, const float* gamma, const float* beta,
                                                          const float* mmean, const float* mvar, float* ab, int C,
                                                          float count, float eps, int train) {
-  __shared__ float part[2][FT];
+  // one thread per channel, all of its 2 * STAT_REPLICAS loads in one round (bn_coef_from_stats: the same
+  // arithmetic as the consumer-side finalize)
   const int c = threadIdx.x;
-  // every load this thread needs is issued before the replica reduction (one memory round trip, not two)
-  const float gm = c < C ? gamma[c] : 0.f, bt = c < C ? beta[c] : 0.f;
-  float mean = 0.f, var = 0.f;
+  if (c >= C) return;
+  float a, b, mean, rstd;
   if (train) {
-    float s, s2;
-    replica_sums(stats, C, part, s, s2);
-    mean = s / count;
-    var = fmaxf(s2 / count - mean * mean, 0.f);
-  } else if (c < C) {
+    bn_coef_from_stats(BnStatsIn{stats, gamma, beta, count, eps}, C, c, a, b, mean, rstd);
+  } else {
     mean = mmean[c];
-    var = mvar[c];
+    rstd = rsqrtf(mvar[c] + eps);
+    a = gamma[c] * rstd;
+    b = beta[c] - mean * a;
   }
-  if (c < C) {
-    const float rstd = rsqrtf(var + eps);
-    const float a = gm * rstd;
-    ab[c] = a;
-    ab[C + c] = bt - mean * a;
-    ab[2 * C + c] = mean;
-    ab[3 * C + c] = rstd;
-  }
+  ab[c] = a;
+  ab[C + c] = b;
+  ab[2 * C + c] = mean;
+  ab[3 * C + c] = rstd;
 }
 
 __global__ __launch_bounds__(256) void bn_eval_kernel(const BnEval* layers) {
@@ -367,8 +362,8 @@ bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
 int bn_finalize(const float* stats, const float* gamma, const float* beta, const float* mmean, const float* mvar,
                 float* ab, int C, float count, float eps, int train, hipStream_t st) {
-  if (C < 1 || C > FT / 4 || FT % C) return 1;          // >= 4 replica phases per channel (replica_sums)
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(FT), 0, st, stats, gamma, beta, mmean, mvar, ab, C, count,
+  if (C < 1 || C > FT) return 1;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(C <= 256 ? 256 : FT), 0, st, stats, gamma, beta, mmean, mvar, ab, C, count,
                      eps, train);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -37,7 +37,10 @@ __device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r
 // after the previous chunk's MFMAs; the N-block-0 blocks store the tile's interior dx (each input pixel once).
 // PJ: the decoder node join epilogue (launch.h PoolJoinEpi) - its own instantiation, so the registers of its
 // prefetched operands never cost the plain convs occupancy.
-template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false, bool PJ = false>
+// XFIN: consumer-side BN finalize of the input transform (p.xfin): every block turns the producer's replica sums
+// into the Cin channels' (a, b) in LDS (its loads in flight with the first chunk's); the first block writes the ab
+// rows for the layer's later consumers.
+template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false, bool PJ = false, bool XFIN = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
@@ -54,6 +57,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   __shared__ __attribute__((aligned(16))) bf16_t smem[SH + SB];
   __shared__ float sred[2][4][BN_];
   __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];
+  __shared__ float sxab[XFIN ? 2 * 256 : 1];            // consumer-side finalize: (a, b) of every input channel
   static_assert(!BWD || WB, "folded BN backward: whole-chunk path only");
   bf16_t* sH = smem;              // [2][HP][LDH]
   bf16_t* sB = smem + SH;         // [2][BN_][LDB]
@@ -85,11 +89,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   uint4 rh[H_PER_T], ryh[BWD ? H_PER_T : 1];
   uint32_t hvalid = 0;                                  // bit i = piece i inside the image
   float ha[8], hb[8];                                   // producer coefficients of the loaded chunk (quarter tid & 3)
+  auto load_coefs = [&](int chunk) {
+    // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
+    const int c8 = chunk * BK + (tid & 3) * 8;
+    if constexpr (XFIN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ha[j] = sxab[c8 + j];
+        hb[j] = sxab[256 + c8 + j];
+      }
+    } else {
+      load_f8_or(p.xf.ab + c8, has_ab, 1.f, ha);
+      load_f8_or(p.xf.ab + p.xf.C + c8, has_ab, 0.f, hb);
+    }
+  };
   auto load_halo = [&](int chunk) {
     const int cbase = chunk * BK;
-    // a thread's pieces all have channel quarter tid & 3 (NT % 4 == 0): one coefficient load per chunk
-    load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, ha);
-    load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, hb);
+    if (!XFIN) load_coefs(chunk);                       // (XFIN: after the prologue, below)
     uint32_t hv = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
@@ -239,6 +255,23 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       load_halo(ch0);
       load_bw(ch0);
     }
+    if constexpr (XFIN) {         // the first chunk's loads are in flight during the coefficient computation
+      if (tid < p.Cin) {
+        float a, bb, mean, rstd;
+        bn_coef_from_stats(p.xfin, p.Cin, tid, a, bb, mean, rstd);
+        sxab[tid] = a;
+        sxab[256 + tid] = bb;
+        if ((blockIdx.x | blockIdx.y | blockIdx.z) == 0) {
+          float* ab = const_cast<float*>(p.xf.ab);
+          ab[tid] = a;
+          ab[p.Cin + tid] = bb;
+          ab[2 * p.Cin + tid] = mean;
+          ab[3 * p.Cin + tid] = rstd;
+        }
+      }
+      __syncthreads();
+      load_coefs(ch0);
+    }
     if constexpr (BWD) {          // the first chunk's loads are in flight during the replica reduction
       bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
       if (ch0 < ch1) bwd_halo(ch0);
@@ -254,6 +287,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       if (next_chunk) {                                      // in flight during this chunk's 9 taps
         load_halo(ch + 1);
         load_bw(ch + 1);
+        if constexpr (XFIN) load_coefs(ch + 1);
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
@@ -440,7 +474,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 // only when it is written to LDS (after the MFMAs), so the loads are never waited for early. BN statistics /
 // BN-node sums accumulate in registers across the block's tiles: one set of channel atomics per block.
 // LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
-template <int TH, int TW, int CH, bool BWD = false, bool PJ = false>
+template <int TH, int TW, int CH, bool BWD = false, bool PJ = false, bool XFIN = false>
 __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
   constexpr int BN_ = 32, WM = 4;
   constexpr int BM = TH * TW;
@@ -475,12 +509,38 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
     *reinterpret_cast<uint4*>(sB + swz_off(row, q)) = *reinterpret_cast<const uint4*>(
         p.wt + (size_t)(nBlock + n) * p.K + (size_t)tap * p.Cin + ch * BK + q * 8);
   }
-  // producer BN coefficients of this thread's channel quarter, per chunk (constant over the block's tiles)
+  // producer BN coefficients of this thread's channel quarter, per chunk (constant over the block's tiles); XFIN:
+  // computed here from the producer's replica sums (consumer-side finalize, first block writes the ab rows)
   float a8[CH][8], b8[CH][8];
+  if constexpr (XFIN) {
+    __shared__ float sxab[2 * CH * BK];
+    if (tid < CH * BK) {
+      float a, bb, mean, rstd;
+      bn_coef_from_stats(p.xfin, p.Cin, tid, a, bb, mean, rstd);
+      sxab[tid] = a;
+      sxab[CH * BK + tid] = bb;
+      if (blockIdx.x == 0) {
+        float* ab = const_cast<float*>(p.xf.ab);
+        ab[tid] = a;
+        ab[p.Cin + tid] = bb;
+        ab[2 * p.Cin + tid] = mean;
+        ab[3 * p.Cin + tid] = rstd;
+      }
+    }
+    __syncthreads();
 #pragma unroll
-  for (int ch = 0; ch < CH; ++ch) {
-    load_f8_or(p.xf.ab + ch * BK + (tid & 3) * 8, has_ab, 1.f, a8[ch]);
-    load_f8_or(p.xf.ab + p.xf.C + ch * BK + (tid & 3) * 8, has_ab, 0.f, b8[ch]);
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a8[ch][j] = sxab[ch * BK + (tid & 3) * 8 + j];
+        b8[ch][j] = sxab[CH * BK + ch * BK + (tid & 3) * 8 + j];
+      }
+  } else {
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+      load_f8_or(p.xf.ab + ch * BK + (tid & 3) * 8, has_ab, 1.f, a8[ch]);
+      load_f8_or(p.xf.ab + p.xf.C + ch * BK + (tid & 3) * 8, has_ab, 0.f, b8[ch]);
+    }
   }
 
   auto tile_of = [&](int item, int& b, int& ty0, int& tx0) {
@@ -722,7 +782,8 @@ void launch_ws(const ConvParams& p, hipStream_t st) {
   grid = grid / nb * nb;
   if (grid < nb) grid = nb;
   if (grid > items) grid = items;
-  if (p.pj.v && p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  if (p.xfin.stats) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  else if (p.pj.v && p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true, true>), dim3(grid), dim3(NT), 0, st, p, items);
   else if (p.pj.v) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
   else if (p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
   else hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
@@ -736,6 +797,11 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
   const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   dim3 grid(tiles, p.N / BN_, splits);
   if constexpr (WB) {
+    if (p.xfin.stats) {
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, false, false, true>), grid, dim3(NT), 0, st, p,
+                         per, splits > 1 ? p.ws : nullptr);
+      return splits;
+    }
     if (p.pj.v && p.bwd.y) {
       hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
       return 1;
@@ -816,6 +882,15 @@ bool conv3x3_bwd_foldable(const ConvParams& p) {
 
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
+  if (p.xfin.stats && (p.bwd.y || p.pj.v || p.xf.C > 256 || !(ws_eligible(p) || use_wb(p)))) {
+    // a kernel without the consumer-side finalize: finalize first, then the plain call
+    const int rc = bn_finalize(p.xfin.stats, p.xfin.gamma, p.xfin.beta, nullptr, nullptr, const_cast<float*>(p.xf.ab),
+                               p.Cin, p.xfin.count, p.xfin.eps, 1, st);
+    if (rc) return rc;
+    ConvParams q = p;
+    q.xfin = BnStatsIn{};
+    return conv3x3(q, st);
+  }
   // LDS-DMA ring, no split-K (it has no in-launch BN-finalize tail: a BnFinal request keeps the other kernels)
   // (the folded BN backward, p.bwd, runs on the whole-chunk / weight-stationary kernels: conv3x3_bwd_foldable)
   if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y && !p.pj.v)

@@ -35,13 +35,17 @@ constexpr int NT = 256;
 // 2-4-way conflicts: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 29-43 % on these kernels, profiles/r2_pmc.)
 CFL_DEVICE int swz(int r, int q) { return r * BK + ((q ^ ((r >> 1) & 3)) << 3); }
 
-// Residual join (ConvJoin) of output pixel m, channels c..c+7, given the rounded conv output r (bias included).
-CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv) {
+// Residual join (ConvJoin) of output pixel m, channels c..c+7, given the rounded conv output r (bias included);
+// jab: the join BN's (a, b) rows (global ab, or the block's LDS copy under a consumer-side finalize)
+CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv, const float* ja, const float* jb) {
   const ConvJoin& J = p.join;
   float r[8], a[8], bb[8];
   unpack8(rv, r);
-  load_f8(J.ab + c, a);
-  load_f8(J.ab + p.N + c, bb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = ja[c + j];
+    bb[j] = jb[c + j];
+  }
   const int hw = p.Ho * p.Wo;
   const int b = m / hw, rem = m - b * hw, oh = rem / p.Wo, ow = rem - oh * p.Wo;
   if (J.mode == JOIN_POOL) {            // TF same 3x3/s2 window: rows 2*oh .. 2*oh+2 clipped at the bottom/right
@@ -237,6 +241,31 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
   if (kt0 < kt1) load_tiles(kt0);
+  // ---- join BN coefficients: global rows, or (consumer-side finalize) this block's N range computed into LDS,
+  //      its loads in flight with the first K tile's (visible to the epilogue after the K loop's barriers) ----
+  __shared__ float sJ[JN ? 2 * BN_ : 1];
+  const float* ja = p.join.ab;
+  const float* jb = p.join.ab + p.N;
+  if constexpr (JN) {
+    if (p.join.fin.stats) {
+      if (tid < BN_) {
+        float a, b, mean, rstd;
+        bn_coef_from_stats(p.join.fin, p.N, nBlock + tid, a, b, mean, rstd);
+        sJ[tid] = a;
+        sJ[BN_ + tid] = b;
+        if (blockIdx.x == 0 && blockIdx.z == 0) {      // this N range's rows for the layer's later consumers
+          float* ab = const_cast<float*>(p.join.ab);
+          ab[nBlock + tid] = a;
+          ab[p.N + nBlock + tid] = b;
+          ab[2 * p.N + nBlock + tid] = mean;
+          ab[3 * p.N + nBlock + tid] = rstd;
+        }
+      }
+      ja = sJ - nBlock;                                 // indexed by the global channel below
+      jb = sJ + BN_ - nBlock;
+    }
+  }
+
   if constexpr (BWD)                   // the first tile's loads are in flight during the replica reduction
     bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
   if (kt0 < kt1) store_tiles(0);
@@ -307,7 +336,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       const size_t off = (size_t)m * p.N + nBlock + cg * 8;
       uint4 v = *reinterpret_cast<const uint4*>(&sC[row][cg * 8]);
       if constexpr (JN) {                       // fused residual join: the conv output itself is not stored
-        join_store(p, m, nBlock + cg * 8, v);
+        join_store(p, m, nBlock + cg * 8, v, ja, jb);
         continue;
       }
       if (node) {
@@ -493,6 +522,14 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
   if (p.join.mode && (p.ks != 1 || p.stats || p.node.y || p.N % 8)) return 5;   // joins: 1x1 residual convs only
   if (p.pj.v && !use3x3(p)) return 7;     // the decoder node join lives in the 3x3 halo kernels' epilogues
+  if (p.xfin.stats && !use3x3(p)) {        // consumer-side finalize: 3x3 halo kernels only - finalize first here
+    const int rc = bn_finalize(p.xfin.stats, p.xfin.gamma, p.xfin.beta, nullptr, nullptr, const_cast<float*>(p.xf.ab),
+                               p.Cin, p.xfin.count, p.xfin.eps, 1, st);
+    if (rc) return rc;
+    ConvParams q = p;
+    q.xfin = BnStatsIn{};
+    return conv_igemm(q, st);
+  }
   if (p.bwd.y) {
     if (p.xf.ab || p.xf.relu || p.up_in || p.join.mode || p.Cin > BNB_MAX_C || p.bwd.dx == nullptr) return 6;
     if (!bwd_foldable(p)) return bwd_unfolded(p, st);

@@ -485,8 +485,31 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
   const int relu = tx ? p.xf.relu : 0;
   const bf16_t* src_b = (MODE == 1 ? p.dy : p.x) + (size_t)b * p.H * p.W * p.C + c0;
   float a4[4], b4[4];
-  load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
-  load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+  // forward with a consumer-side BN finalize (p.xfin): threads 0..CT-1 turn this channel slice's replica sums into
+  // (a, b) in LDS (the slice's first block also writes the ab rows for the layer's later consumers)
+  __shared__ float sAB[MODE == 0 ? 2 * CT : 1];
+  const bool xfin = MODE == 0 && p.xfin.stats != nullptr;
+  if (xfin) {
+    if (tid < CT) {
+      float a, bb, mean, rstd;
+      bn_coef_from_stats(p.xfin, p.C, cbase + tid, a, bb, mean, rstd);
+      sAB[MODE == 0 ? tid : 0] = a;
+      sAB[MODE == 0 ? CT + tid : 0] = bb;
+      if (tw == 0 && sg == 0 && b == 0) {
+        float* ab = const_cast<float*>(p.xf.ab);
+        ab[cbase + tid] = a;
+        ab[p.C + cbase + tid] = bb;
+        ab[2 * p.C + cbase + tid] = mean;
+        ab[3 * p.C + cbase + tid] = rstd;
+      }
+    }
+    __syncthreads();
+    load_f4(&sAB[cg * CPT], a4);
+    load_f4(&sAB[MODE == 0 ? CT + cg * CPT : 0], b4);
+  } else {
+    load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
+    load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+  }
   // fwd / dgrad taps live in LDS (re-read per input row: 36 fewer live registers than holding all 9 taps)
   __shared__ __attribute__((aligned(16))) float sW[MODE == 2 ? 4 : 9 * CT];
   if (MODE != 2) {
@@ -956,6 +979,14 @@ static bool streamed(const DwParams& p) { return tiled(p) && p.algo != 2; }
 
 int dw_fwd(const DwParams& p, hipStream_t st) {
   if (streamed(p)) return launch_stream<0>(p, 1, st);
+  if (p.xfin.stats) {                        // the other paths read a final ab: finalize it first
+    const int rc = bn_finalize(p.xfin.stats, p.xfin.gamma, p.xfin.beta, nullptr, nullptr, const_cast<float*>(p.xf.ab),
+                               p.C, p.xfin.count, p.xfin.eps, 1, st);
+    if (rc) return rc;
+    DwParams q = p;
+    q.xfin = BnStatsIn{};
+    return dw_fwd(q, st);
+  }
   if (tiled(p)) return launch_tile<0>(p, 1, st);
   return launch_dw(p.x, p.w, p.y, p.xf, p.B, p.H, p.W, p.C, 0, st);
 }

@@ -8,7 +8,7 @@
 
 // BN batch statistics are accumulated into STAT_REPLICAS replica rows [rep][2][C] (sum, sum of squares) so the
 // per-block atomics of thousands of workgroups do not all hit the same 2*C words; bn_finalize sums the replicas.
-#define STAT_REPLICAS 32
+#define STAT_REPLICAS 8
 
 // In-launch BatchNorm finalize ("last workgroup done"): the producer of a BN layer's batch statistics turns them into
 // the layer's (a, b, mean, rstd) rows itself instead of a separate 1-block bn_finalize launch (15 per step). Every
@@ -24,6 +24,40 @@ struct BnFinal {
   float count;             // pixels per channel
   float eps;
 };
+
+// Consumer-side BatchNorm finalize: the first kernel that applies a BN layer computes the layer's coefficients
+// itself from the producer's replica sums (no separate 1-block bn_finalize launch in between); the blocks that own a
+// channel range also write that range's ab rows (a, b, mean, rstd) for the later consumers of the layer.
+struct BnStatsIn {
+  const float* stats;      // [STAT_REPLICAS][2][C] batch sums (nullptr = off: ab is already final)
+  const float* gamma;
+  const float* beta;
+  float count;             // pixels per channel
+  float eps;
+};
+
+// Coefficients of channel c from the replica sums - THE arithmetic of bn_finalize (replicas summed in order, all
+// loads issued together), so a consumer-side finalize and a bn_finalize launch agree bit for bit.
+__device__ __forceinline__ void bn_coef_from_stats(const BnStatsIn& f, int C, int c, float& a, float& b, float& mean,
+                                                   float& rstd) {
+  float v0[STAT_REPLICAS], v1[STAT_REPLICAS];
+#pragma unroll
+  for (int r = 0; r < STAT_REPLICAS; ++r) {
+    v0[r] = f.stats[r * 2 * C + c];
+    v1[r] = f.stats[r * 2 * C + C + c];
+  }
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < STAT_REPLICAS; ++r) {
+    s += v0[r];
+    s2 += v1[r];
+  }
+  mean = s / f.count;
+  const float var = fmaxf(s2 / f.count - mean * mean, 0.f);
+  rstd = rsqrtf(var + f.eps);
+  a = f.gamma[c] * rstd;
+  b = f.beta[c] - mean * a;
+}
 
 // ---------------------------------------------------------------- implicit-GEMM conv (conv_igemm.hip)
 // BN-node gradient epilogue (backward). The kernel's output o is the incoming gradient of a BatchNorm node whose
@@ -51,6 +85,7 @@ struct ConvJoin {
   bf16_t* out;
   uint8_t* argmax;         // JOIN_POOL only
   int H, W;
+  BnStatsIn fin;           // consumer-side finalize of y's BN (ab computed here and its rows written), or off
 };
 
 // Decoder node join in a 3x3 data-gradient conv's epilogue (backward of x_lo_{k-1} -> UpSampling2D -> ReLU ->
@@ -84,6 +119,7 @@ struct ConvParams {
   int algo;            // 0 auto (3x3/s1 -> halo-tile conv3x3.hip, else generic), 1 generic only, 2 conv3x3 only
   BnNodeEpi node;      // optional BN-node gradient epilogue (dgrad producers); excludes stats / bias
   PoolJoinEpi pj;      // optional decoder node join (3x3 s1 dgrads, even tiles); excludes stats / bias / node / split
+  BnStatsIn xfin;      // optional consumer-side finalize of xf's BN (xf.ab computed here from the sums, rows written)
   ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
   BnFinal fin;         // optional in-launch finalize of `stats` (run by the launch that completes them)
   BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;
@@ -148,6 +184,7 @@ struct DwParams {
   // node, node_bwd(dz0 same [masked], dres stride-2 scatter) folded into the producer):
   const bf16_t* add_half;   // dres [B, ceil(H/2), ceil(W/2), C] added at even (h, w) (before the node epilogue)
   int mask_x;               // multiply the dgrad value (not add_half) by [x > 0] (x = the layer's transformed input)
+  BnStatsIn xfin;           // dw_fwd: xf.ab computed here from these sums (and written to xf.ab, 4 rows)
 };
 int dw_fwd(const DwParams& p, hipStream_t st);
 int dw_dgrad(const DwParams& p, hipStream_t st);

@@ -312,18 +312,19 @@ def test_engine_bn_moving_stats_and_adam_match_reference():
 
 def test_engine_graph_replay_matches_eager_and_learns():
     table, eng, flat, x, y = _engine_and_ref(seed=2)
-    eng.train_step(use_graph=False)
-    torch.cuda.synchronize()
-    after_eager = eng.get_flat()
-    eng.set_flat(flat)
-    eng.reset_optimizer()
-    eng.train_step(use_graph=True)
-    torch.cuda.synchronize()
-    after_graph = eng.get_flat()
-    # float-atomic reductions (BN stats, wgrad split-M) are order-nondeterministic: the first Adam step moves each
-    # weight by ~lr * sign(g), so near-zero gradients may flip sign -> per-element differences up to ~2 lr
-    d = np.abs(after_eager - after_graph)
-    assert d.max() < 2.5e-3 and (d > 1e-4).mean() < 0.01
+    runs = []
+    for graph in (False, False, True):
+        eng.set_flat(flat)
+        eng.reset_optimizer()
+        eng.train_step(use_graph=graph)
+        torch.cuda.synchronize()
+        runs.append(eng.get_flat())
+    # float-atomic reductions (BN stats, wgrad replica rows) are order-nondeterministic: the first Adam step moves
+    # each weight by ~lr * sign(g), so near-zero gradients may flip sign -> per-element differences up to ~2 lr. A
+    # second eager run measures that noise floor; the graph replay must stay within it.
+    noise = (np.abs(runs[0] - runs[1]) > 1e-4).mean()
+    d = np.abs(runs[0] - runs[2])
+    assert d.max() < 2.5e-3 and (d > 1e-4).mean() <= max(3 * noise, 0.01), ((d > 1e-4).mean(), noise)
     eng.read_metrics("train")
     losses = []
     for i in range(40):
@@ -728,11 +729,21 @@ def test_ops_autograd_layers_match_torch():
 
 @pytest.mark.parametrize("mode,H,Cin,N,B", [("pool", 16, 32, 64, 2), ("pool", 15, 64, 128, 1), ("add", 8, 256, 256, 2),
                                            ("add_up", 16, 64, 32, 2), ("add_up", 8, 128, 64, 3)])
-def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
+def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B, jfin=False):
     """conv_igemm residual-join epilogue (max-pool(BN(y)) + conv / BN(y) + conv / BN(y) + up2(conv)) is
-    bit-identical to the separate conv + pool_res_fwd / bn_add_fwd launches it replaces."""
+    bit-identical to the separate conv + pool_res_fwd / bn_add_fwd launches it replaces (jfin: the join BN's
+    coefficients computed in the conv from replica sums, equal to bn_finalize's, rows written)."""
     C_ = hip()
     torch.manual_seed(11)
+    jkw = {}
+    if jfin:
+        R_ = C_.STAT_REPLICAS
+        st = torch.zeros(R_, 2, N)
+        st[:, 0], st[:, 1] = torch.randn(R_, N) * 40, torch.rand(R_, N) * 300 + 100
+        st = st.reshape(-1).to(DEV)
+        gam, bet = (torch.rand(N) + 0.5).to(DEV), (torch.randn(N) * 0.2).to(DEV)
+        ab_f = torch.zeros(4 * N, device=DEV)
+        C_.bn_finalize(st, gam, bet, gam, bet, ab_f, N, float(B * H * H), 1e-3, 1)
     stride = 2 if mode == "pool" else 1
     Hx = H if mode == "pool" else (H // 2 if mode == "add_up" else H)     # conv input resolution
     Ho = (H + 1) // 2 if mode == "pool" else Hx
@@ -742,6 +753,11 @@ def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
     yb, _ = bf(torch.randn(B, H, H, N))
     ab, _, _ = ab_for(N, 12)
     ab = ab.to(DEV)
+    jab = ab
+    if jfin:
+        ab = ab_f                                  # the reference uses bn_finalize's rows
+        jab = torch.zeros(4 * N, device=DEV)       # the fused conv computes and writes them
+        jkw = dict(jfin_stats=st, jfin_gamma=gam, jfin_beta=bet, jfin_count=float(B * H * H), jfin_eps=1e-3)
     r = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
     C_.conv_igemm(xb, wb, bias, r, None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0, 0)
     if mode == "pool":
@@ -751,8 +767,8 @@ def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
         out = torch.zeros_like(ref)
         am = torch.zeros_like(am_ref)
         C_.conv_igemm(xb, wb, bias, torch.zeros_like(r), None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0,
-                      0, join_mode=C_.JOIN_POOL, join_y=yb, join_ab=ab, join_out=out, join_argmax=am, join_H=H,
-                      join_W=H)
+                      0, join_mode=C_.JOIN_POOL, join_y=yb, join_ab=jab, join_out=out, join_argmax=am, join_H=H,
+                      join_W=H, **jkw)
         assert torch.equal(am, am_ref)
     else:
         up = 1 if mode == "add_up" else 0
@@ -760,9 +776,16 @@ def test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B):
         C_.bn_add_fwd(yb, ab, r, up, ref, B, H, H, N)
         out = torch.zeros_like(ref)
         C_.conv_igemm(xb, wb, bias, torch.zeros_like(r), None, None, 0, B, Hx, Hx, Cin, 0, Ho, Ho, N, 1, stride, 0,
-                      0, join_mode=C_.JOIN_ADD_UP if up else C_.JOIN_ADD, join_y=yb, join_ab=ab, join_out=out,
-                      join_H=H, join_W=H)
+                      0, join_mode=C_.JOIN_ADD_UP if up else C_.JOIN_ADD, join_y=yb, join_ab=jab, join_out=out,
+                      join_H=H, join_W=H, **jkw)
     assert torch.equal(out, ref), int((out != ref).sum())
+    if jfin:
+        assert torch.equal(jab, ab_f)
+
+
+@pytest.mark.parametrize("mode,H,Cin,N,B", [("pool", 16, 32, 64, 2), ("add_up", 16, 64, 32, 2), ("add", 12, 32, 128, 3)])
+def test_conv_join_consumer_finalize(mode, H, Cin, N, B):
+    test_conv_join_epilogue_matches_separate_kernels(mode, H, Cin, N, B, jfin=True)
 
 
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [(2, 12, 64, 32, 0, True), (3, 6, 128, 64, 1, False),
@@ -1290,7 +1313,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
@@ -1447,6 +1470,74 @@ def test_conv3x3_pool_join_matches_node_bwd(B, H, Cin, N, tune):
         torch.cuda.synchronize()
         assert torch.equal(out, ref), int((out != ref).sum())
         assert torch.allclose(sums.view(4, -1).sum(0), s_ref, rtol=1e-4, atol=1e-3)
+    finally:
+        if tune:
+            C_.set_tune(keys[tune][0], 0)
+
+
+@pytest.mark.parametrize("B,H,C", [(2, 32, 64), (2, 24, 32), (3, 16, 256)])
+def test_dw_fwd_consumer_finalize_matches_bn_finalize(B, H, C):
+    """Consumer-side BN finalize (dw_fwd xfin_*: the depthwise forward turns the producer's replica sums into its
+    input's BN coefficients and writes the layer's ab rows) equals bn_finalize + dw_fwd bit for bit: same output,
+    same ab rows."""
+    torch.manual_seed(59)
+    C_ = hip()
+    R_ = C_.STAT_REPLICAS
+    yb, _ = bf(torch.randn(B, H, H, C))
+    w = (torch.randn(9 * C) * 0.2).to(DEV)
+    stats = torch.zeros(R_, 2, C)
+    stats[:, 0] = torch.randn(R_, C) * 50
+    stats[:, 1] = torch.rand(R_, C) * 400 + 200
+    stats = stats.reshape(-1).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.2).to(DEV)
+    count = float(B * H * H * R_)
+    ab_ref = torch.zeros(4 * C, device=DEV)
+    C_.bn_finalize(stats, gamma, beta, gamma, beta, ab_ref, C, count, 1e-3, 1)   # (moving stats unused in training)
+    y_ref = torch.zeros_like(yb)
+    C_.dw_fwd(yb, w, y_ref, ab_ref, 1, B, H, H, C)
+    ab = torch.zeros(4 * C, device=DEV)
+    y = torch.zeros_like(yb)
+    C_.dw_fwd(yb, w, y, ab, 1, B, H, H, C, xfin_stats=stats, xfin_gamma=gamma, xfin_beta=beta, xfin_count=count,
+              xfin_eps=1e-3)
+    torch.cuda.synchronize()
+    assert torch.equal(ab, ab_ref)
+    assert torch.equal(y, y_ref), int((y != y_ref).sum())
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,tune", [(2, 16, 64, 64, ""), (2, 16, 32, 64, "ws"), (2, 16, 64, 32, "ws"),
+                                              (3, 8, 256, 128, "small"), (2, 12, 128, 64, "")])
+def test_conv3x3_consumer_finalize_matches_bn_finalize(B, Hs, Cin, N, tune):
+    """Consumer-side BN finalize of a 3x3 conv's input (conv_igemm xfin_*: per-tile, weight-stationary and 8x8-tile
+    kernels compute the input BN's (a, b) from the replica sums in LDS and write the ab rows) equals bn_finalize +
+    the conv bit for bit: same output, statistics and ab rows."""
+    torch.manual_seed(61)
+    C_ = hip()
+    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2)}
+    if tune:
+        C_.set_tune(*keys[tune])
+    try:
+        R_ = C_.STAT_REPLICAS
+        xb, _ = bf(torch.randn(B, Hs, Hs, Cin))
+        wt, _ = bf(torch.randn(N, 9 * Cin) * 0.05)
+        st = torch.zeros(R_, 2, Cin)
+        st[:, 0], st[:, 1] = torch.randn(R_, Cin) * 40, torch.rand(R_, Cin) * 300 + 100
+        st = st.reshape(-1).to(DEV)
+        gam, bet = (torch.rand(Cin) + 0.5).to(DEV), (torch.randn(Cin) * 0.2).to(DEV)
+        cnt = float(B * Hs * Hs)
+        ab_ref = torch.zeros(4 * Cin, device=DEV)
+        C_.bn_finalize(st, gam, bet, gam, bet, ab_ref, Cin, cnt, 1e-3, 1)
+        outs = []
+        for fin in (False, True):
+            y = torch.zeros(B, Hs, Hs, N, dtype=torch.int16, device=DEV)
+            stats = torch.zeros(R_ * 2 * N, device=DEV)
+            ab = ab_ref if not fin else torch.zeros(4 * Cin, device=DEV)
+            kw = dict(xfin_stats=st, xfin_gamma=gam, xfin_beta=bet, xfin_count=cnt, xfin_eps=1e-3) if fin else {}
+            C_.conv_igemm(xb, wt, None, y, stats, ab, 1, B, Hs, Hs, Cin, 0, Hs, Hs, N, 3, 1, 1, 1, **kw)
+            torch.cuda.synchronize()
+            outs.append((y, stats, ab))
+        assert torch.equal(outs[1][2], ab_ref)
+        assert torch.equal(outs[1][0], outs[0][0]), int((outs[1][0] != outs[0][0]).sum())
+        assert torch.allclose(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-2)
     finally:
         if tune:
             C_.set_tune(keys[tune][0], 0)
