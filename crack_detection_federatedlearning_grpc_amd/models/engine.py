@@ -207,7 +207,7 @@ class UNetEngine:
         bn_layers = [ly for ly in self.table.weighted_layers() if ly.kind == "bn"]
         self.bn_names = [ly.name for ly in bn_layers]
         tot_c = sum(ly.cout for ly in bn_layers)
-        RS = self.RS = self.C.SUM_REPLICAS
+        RS = self.RS = int(os.environ.get("CFL_SUM_REPLICAS", self.C.SUM_REPLICAS))
         self.stats_all = torch.zeros(R * 2 * tot_c, dtype=torch.float32, device=self.dev)
         self.sums_all = torch.zeros(RS * 2 * tot_c, dtype=torch.float32, device=self.dev)
         self.ab_all = torch.zeros(4 * tot_c, dtype=torch.float32, device=self.dev)

@@ -807,7 +807,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("sum_reps") = 1, py::arg("sy") = py::none(), py::arg("sab") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply_op, py::arg("g"), py::arg("y"), py::arg("ab"), py::arg("sums"), py::arg("dy"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("M"), py::arg("C"), py::arg("sum_reps") = 1);
-  m.attr("SUM_REPLICAS") = 16;
+  m.attr("SUM_REPLICAS") = 4;    // BN-backward sum replica rows (whole-step A/B: 16 / 8 / 4 / 2 / 1 -> 1.550 / 1.529 / 1.522 / 1.537 / 1.584 ms)
   m.def("pool_res_fwd", &pool_res_fwd_op);
   m.def("bn_add_fwd", &bn_add_fwd_op);
   m.def("head_fwd", &head_fwd_op);
