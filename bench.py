@@ -126,10 +126,11 @@ def main() -> int:
     batches = torch.as_tensor(epoch_batches(data.train_idx, args.batch, args.local_steps, seed=rank),
                               dtype=torch.int32, device=dev)
     use_graph = not args.no_graph
+    eng.bind_batches(batches)          # each step selects its batch on the device (no per-step host index copy)
 
     if args.profile_steps:
+        eng.set_batch_cursor(0)
         for s in range(args.profile_steps):
-            eng.idx.copy_(batches[s % batches.shape[0]])
             eng.train_step(use_graph)
         torch.cuda.synchronize()
         print(json.dumps({"profile_steps": args.profile_steps, "metrics": eng.read_metrics("train")}))
@@ -160,8 +161,8 @@ def main() -> int:
         eng.reset_optimizer()                              # fresh Adam per round (client_fit_model.py:155-157)
         for _ep in range(args.epochs):                     # model.fit(epochs=10, validation_data=val_gen)
             with phase("bench/train_epoch"):               # roctx ranges with CFL_ROCTX=1 (utils/trace.py)
+                eng.set_batch_cursor(0)                    # this epoch's batches: rows 0.. of the bound table
                 for s in range(args.local_steps):
-                    eng.idx.copy_(batches[s])
                     eng.train_step(use_graph)
             with phase("bench/validate"):
                 if overlap_val and val_steps:

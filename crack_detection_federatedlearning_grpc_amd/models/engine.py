@@ -79,6 +79,10 @@ class UNetEngine:
         self.metrics = torch.zeros(10, dtype=torch.float64, device=dev)        # head.hip metrics layout
         self.eval_metrics = torch.zeros(10, dtype=torch.float64, device=dev)
         self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
+        # optional device batch table (bind_batches): the step's first kernel selects idx = table[cursor % nb] and
+        # its last advances the cursor, so replayed steps need no host-issued index copy
+        self.batch_table: Optional[torch.Tensor] = None
+        self.batch_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
         self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
@@ -704,9 +708,27 @@ class UNetEngine:
         C.bn_moving_update(self.moving_table, len(self.bn_names), self.momentum)
         self.pack(step=True)                               # also advances the Adam step counter
 
+    def bind_batches(self, batches: torch.Tensor) -> None:
+        """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
+        ``cursor % nb`` (selected in the step's zero_spans launch, the cursor advanced by its pack launch) instead of
+        a host copy into ``idx``. Rebinding a table of the same shape copies into the bound buffer (graph-safe)."""
+        batches = batches.to(device=self.dev, dtype=torch.int32).contiguous()
+        if batches.dim() != 2 or batches.shape[1] != self.B:
+            raise ValueError(f"bind_batches: expected [nb, {self.B}], got {tuple(batches.shape)}")
+        if self.batch_table is not None and self.batch_table.shape == batches.shape:
+            self.batch_table.copy_(batches)
+            return
+        if self.graph is not None:
+            raise RuntimeError("bind_batches: a differently shaped table after graph capture")
+        self.batch_table = batches.clone()
+
+    def set_batch_cursor(self, i: int = 0) -> None:
+        self.batch_cursor.fill_(i)
+
     def pack(self, step: bool = False) -> None:
+        cursor = self.batch_cursor if step and self.batch_table is not None else None
         self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack,
-                            self.step_t if step else None)
+                            self.step_t if step else None, cursor)
         if self.fp8:   # after an optimizer step also fold the recorded activation amax (delayed scaling)
             self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
                             self.amax8 if step else None, self.n_views8)
@@ -754,7 +776,11 @@ class UNetEngine:
         self.metrics.copy_(saved)
 
     def _zero_step(self) -> None:
-        self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
+        if self.batch_table is not None:
+            self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero, self.batch_table, self.batch_cursor,
+                              self.idx)
+        else:
+            self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
 
     def train_step_eager(self) -> None:
         self._fp8_calibrate()
@@ -770,9 +796,10 @@ class UNetEngine:
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
             # warm-up launch outside capture (module load, lazy init) on a scratch copy of the state
-            saved = [t.clone() for t in (self.flat, self.m, self.v, self.step_t, self.metrics)]
+            state = (self.flat, self.m, self.v, self.step_t, self.metrics, self.batch_cursor)
+            saved = [t.clone() for t in state]
             self.train_step_eager()
-            for t, c in zip((self.flat, self.m, self.v, self.step_t, self.metrics), saved):
+            for t, c in zip(state, saved):
                 t.copy_(c)
             self.pack()
         torch.cuda.current_stream(self.dev).wait_stream(s)

@@ -572,10 +572,11 @@ at::Tensor make_pack_table(std::vector<std::tuple<int, int64_t, int64_t, int, in
   return cpu.to(like.device());
 }
 
-void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n_views, int max_elems, OptT step) {
+void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n_views, int max_elems, OptT step,
+                     OptT cursor) {
   TORCH_CHECK(table.numel() == (int64_t)n_views * (int64_t)sizeof(PackView), "pack: table size");
   ok(pack_weights(ptr<const float>(flat, "flat"), ptr<bf16_t>(packed, "packed"), ptr<const PackView>(table, "table"),
-                  n_views, max_elems, stream(), optr<int>(step, "step")),
+                  n_views, max_elems, stream(), optr<int>(step, "step"), optr<int>(cursor, "cursor")),
      "pack_weights");
 }
 
@@ -621,9 +622,20 @@ at::Tensor make_zero_table(std::vector<at::Tensor> spans) {
   return cpu.to(spans.at(0).device());
 }
 
-void zero_spans_op(at::Tensor table, int n, int64_t max_bytes) {
+void zero_spans_op(at::Tensor table, int n, int64_t max_bytes, OptT batches, OptT cursor, OptT idx) {
   TORCH_CHECK(table.numel() == (int64_t)n * (int64_t)sizeof(ZeroSpan), "zero_spans: table size");
-  ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream()), "zero_spans");
+  BatchSelect bs{};
+  if (batches) {
+    TORCH_CHECK(cursor && idx && batches->dim() == 2 && batches->size(1) == idx->numel() &&
+                batches->scalar_type() == at::kInt && idx->scalar_type() == at::kInt && cursor->numel() >= 1,
+                "zero_spans: batches [nb][B] int32 with cursor and idx [B]");
+    bs.table = ptr<const int32_t>(*batches, "batches");
+    bs.cursor = ptr<const int>(*cursor, "cursor");
+    bs.idx = ptr<int32_t>(*idx, "idx");
+    bs.B = (int)idx->numel();
+    bs.nb = (int)batches->size(0);
+  }
+  ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream(), bs), "zero_spans");
 }
 
 // views: list of (kind, src, dst_bytes, ks, cin, cout, dst_scale) -> device table (fp8 pack)
@@ -771,7 +783,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("make_grad_finish_table", &make_grad_finish_table);
   m.def("grad_finish", &grad_finish_op);
   m.def("make_zero_table", &make_zero_table);
-  m.def("zero_spans", &zero_spans_op);
+  m.def("zero_spans", &zero_spans_op, py::arg("table"), py::arg("n"), py::arg("max_bytes"),
+        py::arg("batches") = py::none(), py::arg("cursor") = py::none(), py::arg("idx") = py::none());
   m.def("set_tune", &cfl_set_tune);
   m.attr("GF_REDUCE") = (int)GF_REDUCE;
   m.attr("GF_COPY") = (int)GF_COPY;
@@ -827,7 +840,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ws") = py::none(), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
         py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
-        py::arg("max_elems"), py::arg("step") = py::none());
+        py::arg("max_elems"), py::arg("step") = py::none(), py::arg("cursor") = py::none());
   m.def("render_cracks", &render_cracks_op);
   m.def("resize_batch", &resize_batch_op, py::arg("src"), py::arg("offs"), py::arg("dims"), py::arg("dst"),
         py::arg("binarize") = 0);

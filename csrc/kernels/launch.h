@@ -344,7 +344,7 @@ int pack_fp8(const float* flat, uint8_t* packed8, float* scales, const PackView*
              hipStream_t st, float* amax = nullptr, int n_amax = 0);
 // step != nullptr: also increments the Adam step counter (adam_step_done folded into this launch)
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
-                 hipStream_t st, int* step = nullptr);
+                 hipStream_t st, int* step = nullptr, int* cursor = nullptr);   // cursor: BatchSelect's, += 1
 
 // ---------------------------------------------------------------- step bookkeeping (optim.hip)
 // grad_finish: ONE launch at the end of backward for every gradient that was accumulated into replica rows
@@ -365,7 +365,17 @@ struct ZeroSpan {
   void* p;
   int64_t bytes;           // multiple of 16
 };
-int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st);
+// batch: optionally also selects the step's dataset indices on the device, idx[0..B) = table[(*cursor) % nb]
+// (a batch table bound once per epoch; the cursor is advanced by pack_weights at the end of the step), so the
+// replayed step needs no host-issued index copy
+struct BatchSelect {
+  const int32_t* table;    // [nb][B] or nullptr
+  const int* cursor;
+  int32_t* idx;
+  int B, nb;
+};
+int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st,
+               BatchSelect batch = BatchSelect{});
 
 // launch-shape tuning knobs (0 = built-in heuristic), set from Python for micro-benchmark sweeps
 enum TuneKey {

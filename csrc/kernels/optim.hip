@@ -44,8 +44,11 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
 __global__ void step_done_kernel(int* step) { *step += 1; }
 
 __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* packed, const PackView* views,
-                                                  int* step) {
-  if (step != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *step += 1;   // adam_step_done
+                                                  int* step, int* cursor) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (step != nullptr) *step += 1;                  // adam_step_done
+    if (cursor != nullptr) *cursor += 1;              // next step's batch (BatchSelect)
+  }
   const PackView v = views[blockIdx.y];
   const int taps = v.ks * v.ks;
   int N, K;
@@ -172,7 +175,9 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
   }
 }
 
-__global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans) {
+__global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs) {
+  if (bs.table != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < bs.B)
+    bs.idx[threadIdx.x] = bs.table[(size_t)(*bs.cursor % bs.nb) * bs.B + threadIdx.x];
   const ZeroSpan z = spans[blockIdx.y];
   uint4* p = reinterpret_cast<uint4*>(z.p);
   const int64_t n = z.bytes >> 4;
@@ -207,12 +212,13 @@ int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipS
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st) {
+int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st, BatchSelect batch) {
   if (n_spans <= 0) return 0;
+  if (batch.table != nullptr && (batch.B < 1 || batch.B > NT || batch.nb < 1)) return 1;
   int64_t bx = (max_bytes / 16 + NT - 1) / NT;
   if (bx > 1024) bx = 1024;
   if (bx < 1) bx = 1;
-  hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans);
+  hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans, batch);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -230,10 +236,10 @@ int adam_step_done(int* step, hipStream_t st) {
 }
 
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
-                 hipStream_t st, int* step) {
+                 hipStream_t st, int* step, int* cursor) {
   int bx = (max_elems + NT - 1) / NT;
   if (bx > 256) bx = 256;
-  hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views, step);
+  hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views, step, cursor);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
