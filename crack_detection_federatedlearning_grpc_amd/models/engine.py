@@ -711,15 +711,16 @@ class UNetEngine:
     def bind_batches(self, batches: torch.Tensor) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
         ``cursor % nb`` (selected in the step's zero_spans launch, the cursor advanced by its pack launch) instead of
-        a host copy into ``idx``. Rebinding a table of the same shape copies into the bound buffer (graph-safe)."""
+        a host copy into ``idx``. Rebinding a table of at most the bound row count copies into the bound buffer
+        (graph-safe; steps from cursor 0 then use its first rows)."""
         batches = batches.to(device=self.dev, dtype=torch.int32).contiguous()
         if batches.dim() != 2 or batches.shape[1] != self.B:
             raise ValueError(f"bind_batches: expected [nb, {self.B}], got {tuple(batches.shape)}")
-        if self.batch_table is not None and self.batch_table.shape == batches.shape:
-            self.batch_table.copy_(batches)
+        if self.batch_table is not None and batches.shape[0] <= self.batch_table.shape[0]:
+            self.batch_table[:batches.shape[0]].copy_(batches)
             return
         if self.graph is not None:
-            raise RuntimeError("bind_batches: a differently shaped table after graph capture")
+            raise RuntimeError("bind_batches: a larger table after graph capture")
         self.batch_table = batches.clone()
 
     def set_batch_cursor(self, i: int = 0) -> None:
@@ -987,8 +988,9 @@ class HipBackend:
         e = self.eng
         dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)
         e.metrics.zero_()
-        for s in range(dev_b.shape[0]):
-            e.idx.copy_(dev_b[s])
+        e.bind_batches(dev_b)                  # the steps select their batches on the device (no per-step copy)
+        e.set_batch_cursor(0)
+        for _ in range(dev_b.shape[0]):
             e.train_step(self.use_graph)
         m = e.read_metrics("train")
         if e.dice:
