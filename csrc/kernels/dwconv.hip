@@ -783,11 +783,11 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     fetch<SR>(x_b, p, x0, a + SR + 1, more, rx, okx);
     const int oy = a + sr;
     const float live = oy < yend ? 1.f : 0.f;              // rows past the segment belong to the next block
-    float acc[SL][4], g[SL][4], xc[SL][4];
+    float acc[SL][4], g[SL][4];
 #pragma unroll
     for (int i = 0; i < SL; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = xc[i][j] = 0.f;
+      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = 0.f;
     // dgrad: flipped taps over the dy halo; the centre row's columns 1..SL are this strip's own dy (wgrad operand)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
@@ -823,10 +823,6 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       for (int cx = 0; cx < SL + 2; ++cx) {
         float f[4];
         unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
-        if (ky == 1 && cx >= 1 && cx <= SL) {             // centre pixels' transformed x (mask_x)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xc[cx - 1][j] = f[j];
-        }
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int o = cx - kx;
@@ -846,9 +842,11 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
           if (p.add_half || p.mask_x) {                      // residual join (node_bwd semantics, one rounding)
             float o[4];
             unpack4(v, o);
-            if (p.mask_x) {
+            if (p.mask_x) {                                  // transformed x at this pixel: the x ring's centre row
+              float xt[4];
+              unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), xt);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) o[j] = xc[i][j] > 0.f ? o[j] : 0.f;
+              for (int j = 0; j < 4; ++j) o[j] = xt[j] > 0.f ? o[j] : 0.f;
             }
             const int xx = x0 + sc + i;
             if (p.add_half && ((oy | xx) & 1) == 0) {
