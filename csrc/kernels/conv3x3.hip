@@ -824,7 +824,12 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
 }  // namespace
 
 // output-channel tile of the whole-chunk path: 64 (fewer halo re-loads) unless tuned to 32 (more blocks, 122 vs 208
-// VGPRs -> 4 vs 2 waves per SIMD)
+// VGPRs -> 4 vs 2 waves per SIMD). Counters behind the tile choices (profiles/r2_pmc/pmc_summary.txt and
+// pmc_latency.txt, 256^2 / B16 bench step): the 8x16 x 64 tile runs at 14 % of the MFMA peak and 0.8 TB/s with
+// 1.3 % LDS bank conflicts (the swizzle), an 89 % L2 hit rate and ~320-cycle L1->L2 latency - neither MFMA, HBM nor
+// LDS bound but latency-bound per block, which is why the halo is prefetched a chunk ahead, the producer transform
+// deferred to the LDS store and the 128^2 level moved to the weight-stationary persistent kernel (weights loaded
+// once per block instead of per tile: 8.7 % MFMA, 2.5 TB/s). tools/conv3_probe.py times the variants per shape.
 static int wb_bn(const ConvParams& p) {
   const int v = cfl_tune(TUNE_CONV3_BN);
   if (v == 32 || p.N % 64 != 0) return 32;
