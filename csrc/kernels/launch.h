@@ -401,7 +401,8 @@ enum TuneKey {
   TUNE_DW_BWD_BLOCKS = 21,     // fused depthwise backward: target grid size (default 512)
   TUNE_BBA_BLOCKS = 22,        // bn_bwd_apply grid cap (default 1024)
   TUNE_NODE_POOL_BLOCKS = 23,  // max-pool node gradient grid cap (default: TUNE_NODE_BWD_BLOCKS / 512)
-  TUNE_N = 24
+  TUNE_WGRAD1_RM = 24,         // generic wgrad 64x64 tiles: pixels per pipeline stage (0 = 64, 128)
+  TUNE_N = 28
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
