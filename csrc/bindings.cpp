@@ -810,6 +810,9 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_BBA_BLOCKS") = (int)TUNE_BBA_BLOCKS;
   m.attr("TUNE_NODE_POOL_BLOCKS") = (int)TUNE_NODE_POOL_BLOCKS;
   m.attr("TUNE_WGRAD1_RM") = (int)TUNE_WGRAD1_RM;
+  m.attr("TUNE_PW") = (int)TUNE_PW;
+  m.attr("TUNE_PW_BLOCKS") = (int)TUNE_PW_BLOCKS;
+  m.attr("TUNE_PW_DEPTH") = (int)TUNE_PW_DEPTH;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

@@ -549,7 +549,8 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
-  if (p.algo == 2) return 4;
+  if (pw_conv_supported(p)) return pw_conv(p, st);
+  if (p.algo == 2) return 4;   // plain 1x1 / stride 1: streaming kernel (pw.hip)
   int splits = p.join.mode ? 1 : conv_igemm_splits(p);
   if (splits > 1 && (p.ws == nullptr || p.ws_elems < (int64_t)splits * p.M * p.N)) splits = 1;
   const int cfg = cfl_tune(TUNE_IGEMM_CFG);

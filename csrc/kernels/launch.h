@@ -130,6 +130,10 @@ struct ConvParams {
                        // does not fold fall back to bn_bwd_apply into bwd.dx + the plain conv (same results)
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
+// plain 1x1 / stride-1 convs (no input transform, epilogue = bias + optional BN statistics): streaming MFMA kernel
+// with swapped operands and resident weights (pw.hip); conv_igemm routes them there unless TUNE_PW = 1
+bool pw_conv_supported(const ConvParams& p);
+int pw_conv(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
 int conv3x3_splits(const ConvParams& p);
 int conv3x3_split_k(const ConvParams& p);     // K splits of the standard tiles (fp8 path)
@@ -402,6 +406,9 @@ enum TuneKey {
   TUNE_BBA_BLOCKS = 22,        // bn_bwd_apply grid cap (default 1024)
   TUNE_NODE_POOL_BLOCKS = 23,  // max-pool node gradient grid cap (default: TUNE_NODE_BWD_BLOCKS / 512)
   TUNE_WGRAD1_RM = 24,         // generic wgrad 64x64 tiles: pixels per pipeline stage (0 = 64, 128)
+  TUNE_PW = 25,                // plain 1x1 convs: 0 = streaming kernel (pw.hip), 1 = conv_igemm tiles
+  TUNE_PW_BLOCKS = 26,         // streaming 1x1 kernel: resident-grid cap (default 512 = 2 blocks per CU)
+  TUNE_PW_DEPTH = 27,          // streaming 1x1 kernel: tiles in flight per wave (1 default, 2, 4 at K = 32)
   TUNE_N = 28
 };
 int cfl_tune(int key);

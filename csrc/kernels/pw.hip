@@ -1,0 +1,233 @@
+// Streaming 1x1 convolution on gfx950 MFMA: the SeparableConv2D pointwise convs (forward, with the next BatchNorm's
+// batch statistics) and the 1x1 data gradients of the pointwise and residual convs
+// (/root/reference/client_fit_model.py:107-116, 118-121, 133-136).
+//
+// These GEMMs have K = Cin = 32-256 and M = B*H*W = 16k-262k pixels: 1-8 K-steps per output tile, i.e. a streaming
+// pass over the input. conv_igemm's tile-per-block form (one 64x64 tile, LDS-staged operands, block barriers,
+// per-block statistics atomics) measured 2.2-3.7 TB/s against 6.8 TB/s for a copy of the same bytes, and its
+// statistics epilogue alone cost 9 us of 22.5 at 128^2 (tools/pw_probe.py: 4,096 blocks x 128 atomics).
+//
+// Here the MFMA operands are swapped - D = W * X^T - so that
+//   * the B operand (16 pixels x 32 channels per fragment: lane = (pixel, 8 channels)) is a plain 16-byte global
+//     load of the NHWC input straight into the MFMA registers (no LDS staging of the activations, no barrier);
+//   * the accumulator holds 4 consecutive output channels of one pixel per lane: 8-byte bf16 stores straight from
+//     the registers, no LDS transpose;
+//   * the weights (A operand) of the block's output-channel slice stay resident in LDS for the whole launch
+//     (swizzled 16-byte quarters: conflict-free fragment reads).
+// Each wave is its own pipeline: a persistent loop over WR-pixel tiles whose next tile's loads are issued right after
+// the current tile's MFMAs, so they are in flight during its epilogue. Statistics (from the rounded bf16 outputs, as
+// in conv_igemm) stay in registers across the tiles: one atomic per (channel, statistic) per block at the end.
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// bf16 offset of 16-byte quarter q of weight row n in a [rows][32] k-block: quarter q stored at q ^ ((n >> 1) & 3)
+// (conv_igemm.hip's swizzle: a fragment read of 16 consecutive rows at one quarter covers all 64 banks)
+CFL_DEVICE int wswz(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3); }
+
+template <int K>
+constexpr int pw_rows() { return K >= 128 ? 4096 / K : 64; }   // pixels per wave tile (A: WR*K/128 VGPRs)
+
+template <int NB, int K, int D>
+__global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices) {
+  constexpr int WR = pw_rows<K>();
+  constexpr int MF = WR / 16, NF = NB / 16, KS = K / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
+  __shared__ __attribute__((aligned(16))) float sBias[NB];
+  __shared__ float sred[2][NT / 64][NB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, q = lane >> 4;
+  // block -> (output-channel slice, block within the slice); the slices of one pixel range sit on one XCD
+  // (dispatch order b, b + 8, ... share an XCD and its L2, which then serves the second slice's input reads)
+  const int j = blockIdx.x >> 3;
+  const int slice = j % nslices, bs = (j / nslices) * 8 + (blockIdx.x & 7);
+  const int bps = gridDim.x / nslices;
+  const int n0 = slice * NB;
+  const int tiles = (p.M + WR - 1) / WR;
+  const int wstride = bps * (NT / 64);
+  int t = bs * (NT / 64) + wid;
+
+  // B operand: lane (r16, q) holds pixel m0 + i*16 + r16, channels s*32 + q*8 .. +7. Rows past M are clamped to the
+  // last pixel (their results are neither stored nor counted).
+  s8v a[D][MF][KS];
+  auto load = [&](s8v (&buf)[MF][KS], int tt) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      int m = tt * WR + i * 16 + r16;
+      m = m < p.M ? m : p.M - 1;
+      const bf16_t* src = p.x + (size_t)m * K + q * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        buf[i][s] = *reinterpret_cast<const s8v*>(src + s * 32);
+    }
+  };
+  // D tiles in flight per wave: the first D tiles' loads are issued while the weights are staged
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (t + d * wstride < tiles) load(a[d], t + d * wstride);
+
+  for (int c = tid; c < NB * K / 8; c += NT) {
+    const int n = c / (K / 8), kc = c - n * (K / 8);
+    *reinterpret_cast<uint4*>(sW + (kc >> 2) * NB * 32 + wswz(n, kc & 3)) =
+        *reinterpret_cast<const uint4*>(p.wt + (size_t)(n0 + n) * K + kc * 8);
+  }
+  if (tid < NB) sBias[tid] = p.bias ? p.bias[n0 + tid] : 0.f;
+  __syncthreads();
+
+  const bool stats = p.stats != nullptr;
+  float s1[NF][4], s2[NF][4];
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[nf][r] = s2[nf][r] = 0.f;
+
+  for (; t < tiles; t += D * wstride) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int tt = t + d * wstride;
+      if (tt >= tiles) break;
+      // opaque zero: keeps the (loop-invariant) weight fragment reads inside the loop - hoisted, NF*KS fragments would
+      // stay live in registers across the whole loop and spill
+      int wo = 0;
+      asm volatile("" : "+v"(wo));
+      const bf16_t* sWt = sW + wo;
+      f4v acc[NF][MF];
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+        for (int i = 0; i < MF; ++i) acc[nf][i] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const s8v w = *reinterpret_cast<const s8v*>(sWt + s * NB * 32 + wswz(nf * 16 + r16, q));
+#pragma unroll
+          for (int i = 0; i < MF; ++i)
+            acc[nf][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[d][i][s], acc[nf][i], 0, 0, 0);
+        }
+      const int m0 = tt * WR;
+      if (tt + D * wstride < tiles) load(a[d], tt + D * wstride);   // refill this buffer: D tiles stay in flight
+
+      // D = W * X^T: lane (r16, q) holds output channels n0 + nf*16 + q*4 + r (r = 0..3) of pixel m0 + i*16 + r16.
+      // Fragments nf = 2h, 2h+1 are paired: lanes q, q^1 (lane +- 16) swap one 8-byte half each so every lane owns
+      // 8 consecutive channels and each store instruction writes 64 contiguous bytes per pixel (8-byte stores of
+      // 32-byte pieces measured at half the write rate: tools/pw_probe.py)
+      const bool odd = q & 1;
+#pragma unroll
+      for (int h = 0; h < NF / 2; ++h) {
+        const float4 b0 = *reinterpret_cast<const float4*>(&sBias[(2 * h) * 16 + q * 4]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&sBias[(2 * h + 1) * 16 + q * 4]);
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int m = m0 + i * 16 + r16;
+          const f4v c0 = acc[2 * h][i], c1 = acc[2 * h + 1][i];
+          const uint2 u0 = make_uint2(pack2bf(c0[0] + b0.x, c0[1] + b0.y), pack2bf(c0[2] + b0.z, c0[3] + b0.w));
+          const uint2 u1 = make_uint2(pack2bf(c1[0] + b1.x, c1[1] + b1.y), pack2bf(c1[2] + b1.z, c1[3] + b1.w));
+          const uint2 give = odd ? u0 : u1;
+          const uint2 got = make_uint2(__shfl_xor(give.x, 16, 64), __shfl_xor(give.y, 16, 64));
+          const uint4 v = odd ? make_uint4(got.x, got.y, u1.x, u1.y) : make_uint4(u0.x, u0.y, got.x, got.y);
+          if (m < p.M) {
+            *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + n0 + (2 * h + odd) * 16 + (q >> 1) * 8) = v;
+            if (stats) {
+              const uint32_t w[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float lo = __uint_as_float(w[e] << 16), hi = __uint_as_float(w[e] & 0xffff0000u);
+                const int nf = 2 * h + (e >> 1), r = (e & 1) * 2;
+                s1[nf][r] += lo;
+                s2[nf][r] = fmaf(lo, lo, s2[nf][r]);
+                s1[nf][r + 1] += hi;
+                s2[nf][r + 1] = fmaf(hi, hi, s2[nf][r + 1]);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+
+  if (!stats) return;
+  // lanes of one q group hold the same 4 channels per fragment column: reduce over r16, then over the 4 waves
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[nf][r] += __shfl_xor(s1[nf][r], o, 64);
+        s2[nf][r] += __shfl_xor(s2[nf][r], o, 64);
+      }
+  if (r16 == 0) {
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sred[0][wid][nf * 16 + q * 4 + r] = s1[nf][r];
+        sred[1][wid][nf * 16 + q * 4 + r] = s2[nf][r];
+      }
+  }
+  __syncthreads();
+  float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+  for (int e = tid; e < 2 * NB; e += NT) {
+    const int st = e / NB, cc = e - st * NB;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
+    atomicAdd(&rep[st * p.N + n0 + cc], v);
+  }
+}
+
+template <int NB, int K, int D>
+void launch_d(const ConvParams& p, hipStream_t st) {
+  constexpr int WR = pw_rows<K>();
+  const int nslices = p.N / NB;
+  const int tiles = (p.M + WR - 1) / WR;
+  // persistent grid: each wave takes a multiple of D tiles (ideally exactly D: its whole share in flight at once),
+  // at most one round of resident blocks (2 per CU) per launch
+  int cap = cfl_tune(TUNE_PW_BLOCKS);
+  if (cap <= 0) cap = 512;
+  int per_slice = cap / nslices / 8 * 8;
+  if (per_slice < 8) per_slice = 8;
+  int tpw = (tiles + per_slice * 4 - 1) / (per_slice * 4);           // tiles per wave
+  tpw = (tpw + D - 1) / D * D;
+  const int waves = (tiles + tpw - 1) / tpw;
+  const int bps = ((waves + 3) / 4 + 7) / 8 * 8;
+  hipLaunchKernelGGL((pw_kernel<NB, K, D>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+}
+
+template <int NB, int K>
+void launch(const ConvParams& p, hipStream_t st) {
+  int d = cfl_tune(TUNE_PW_DEPTH);
+  if (d <= 0) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration
+  if constexpr (K == 32) {                                // deeper rings spill at K >= 64
+    if (d >= 4) return launch_d<NB, K, 4>(p, st);
+  }
+  if (d >= 2) launch_d<NB, K, 2>(p, st);
+  else launch_d<NB, K, 1>(p, st);
+}
+
+}  // namespace
+
+bool pw_conv_supported(const ConvParams& p) {
+  return cfl_tune(TUNE_PW) != 1 && cfl_tune(TUNE_IGEMM_CFG) == 0 && p.algo == 0 && p.ks == 1 && p.stride == 1 &&
+         p.pad_t == 0 && p.pad_l == 0 && !p.up_in && p.Ho == p.Hin && p.Wo == p.Win && p.K == p.Cin &&
+         (p.Cin == 32 || p.Cin == 64 || p.Cin == 128 || p.Cin == 256) && (p.N == 32 || p.N % 64 == 0) &&
+         p.xf.ab == nullptr && !p.xf.relu && p.node.y == nullptr && p.join.mode == JOIN_NONE &&
+         p.bwd.y == nullptr && p.pj.v == nullptr && p.xfin.stats == nullptr && p.fin.gamma == nullptr && p.M > 0;
+}
+
+int pw_conv(const ConvParams& p, hipStream_t st) {
+  if (!pw_conv_supported(p)) return 1;
+  const bool n32 = p.N == 32;
+  switch (p.Cin) {
+    case 32: n32 ? launch<32, 32>(p, st) : launch<64, 32>(p, st); break;
+    case 64: n32 ? launch<32, 64>(p, st) : launch<64, 64>(p, st); break;
+    case 128: n32 ? launch<32, 128>(p, st) : launch<64, 128>(p, st); break;
+    default: n32 ? launch<32, 256>(p, st) : launch<64, 256>(p, st); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}

@@ -1574,3 +1574,41 @@ def test_engine_device_batch_table_selects_and_advances():
     u1, u2 = after_table - flat, eng2.get_flat() - flat
     cos = float(np.dot(u1, u2) / (np.linalg.norm(u1) * np.linalg.norm(u2) + 1e-30))
     assert np.abs(u1 - u2).max() < 1e-2 and cos > 0.9, cos
+
+
+@pytest.mark.parametrize("B,H,Cin,N,use_stats,use_bias,cap", [
+    (2, 24, 32, 64, True, True, 0), (3, 17, 64, 32, True, False, 0), (2, 16, 128, 128, True, True, 0),
+    (1, 16, 256, 256, False, True, 0), (2, 20, 64, 64, True, True, 8), (2, 12, 128, 64, False, False, 16)])
+def test_pw_streaming_1x1_matches_igemm_and_reference(B, H, Cin, N, use_stats, use_bias, cap):
+    """Plain 1x1 / stride-1 convs run on the streaming swapped-operand kernel (pw.hip): same output as the
+    conv_igemm tile kernel (TUNE_PW = 1) and the fp32 reference, statistics = sums of the stored bf16 outputs;
+    partial last tiles (M = 867) and several tiles per wave (grid cap 8 / 16 blocks)."""
+    C = hip()
+    torch.manual_seed(20)
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    w = torch.randn(1, 1, Cin, N) * 0.1
+    wb = pack(PK_PW, w, 1, Cin, N)
+    bias = (torch.randn(N) * 0.1) if use_bias else None
+    outs, sts = [], []
+    for tune in (0, 1):
+        C.set_tune(C.TUNE_PW, tune)
+        C.set_tune(C.TUNE_PW_BLOCKS, cap)
+        try:
+            y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            stats = torch.zeros(C.STAT_REPLICAS * 2 * N, device=DEV) if use_stats else None
+            C.conv_igemm(xb, wb, bias.to(DEV) if use_bias else None, y, stats, None, 0, B, H, H, Cin, 0, H, H, N, 1,
+                         1, 0, 0)
+            torch.cuda.synchronize()
+        finally:
+            C.set_tune(C.TUNE_PW, 0)
+            C.set_tune(C.TUNE_PW_BLOCKS, 0)
+        outs.append(from_bits(y))
+        sts.append(stats.view(-1, 2, N).sum(0).cpu() if use_stats else None)
+    ref = xf @ w.view(Cin, N).to(torch.bfloat16).float() + (bias if use_bias else 0.)
+    assert rel(outs[0], ref) < 1e-2
+    assert rel(outs[0], outs[1]) < 1e-3
+    if use_stats:
+        o = outs[0].double()
+        assert torch.allclose(sts[0].double()[0], o.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(sts[0].double()[1], (o * o).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(sts[0], sts[1], rtol=1e-3, atol=1e-2)
