@@ -274,6 +274,9 @@ class UNetEngine:
         # bwd=...; 14 of the 15 bn_bwd_apply passes - the entry BN's feeds only the entry weight gradient), which
         # also stores dx for the weight gradient (CFL_BNB_FOLD=0: separate bn_bwd_apply launches)
         self.fold_bnb = os.environ.get("CFL_BNB_FOLD", "0") == "1"
+        # ... or only at the levels whose side is <= CFL_BNB_FOLD_RES (the low-resolution bn_bwd_apply passes are
+        # launch-bound: 4.3 us for 1-6 MB, profiles/r2_final/roofline.txt)
+        self.fold_res = int(os.environ.get("CFL_BNB_FOLD_RES", "0"))
         # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
         # dgrad launch plus a deferred, grouped wgrad)
         self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
@@ -526,6 +529,10 @@ class UNetEngine:
         else:
             self._side(lambda: self.C.dw_wgrad(*args))
 
+    def _fold_at(self, res: int) -> bool:
+        """Fold the BN-backward apply of a level with side ``res`` into its data-gradient conv's operand load."""
+        return self.fold_bnb or res <= self.fold_res
+
     def backward(self) -> None:
         self._wq = [] if self.defer_wgrad else None
         self._dwq = [] if self.defer_wgrad else None
@@ -547,7 +554,6 @@ class UNetEngine:
 
     def _backward(self) -> None:
         C, B, r, A, D = self.C, self.B, self.r, self.act, self.dg
-        fold = self.fold_bnb
         names = self.names
         hl = names[-1]
         # the head's input gradient is also the gradient of the last BN_B node (x_lo = BN_B(c2) + q, no ReLU): its
@@ -567,6 +573,7 @@ class UNetEngine:
             prevres = Rk if k == 0 else Rk // 2
             up = 0 if k == 0 else 1
             bnB, bnA = self.bn[b2], self.bn[b1]
+            fold = self._fold_at(Rk)
             # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. Its BN-backward sums were
             # accumulated by the pass that produced dxlo: head_bwd (k = 3) or the plain node pass of level k+1
             gB = dxlo
@@ -631,6 +638,7 @@ class UNetEngine:
             else:
                 xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
             bnb, bna = self.bn[b2], self.bn[b1]
+            fold = self._fold_at(H)
             # BN_b node: routed through the max-pool (no ReLU)
             C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
                        bnb["sums"], B, H, H, F, self.RS)

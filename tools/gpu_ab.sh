@@ -4,8 +4,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -q -m gpu -p no:cacheprovider --timeout 120 \
-      --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_kernels.py} -x -q -m gpu -p no:cacheprovider --timeout 120 \
+      --timeout-method thread ${TEST_K:+-k "$TEST_K"} > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
   tail -1 gpurun_out/gpu_tests.log
 fi
 V=${AB_VAR:-CFL_TUNE}

@@ -20,10 +20,16 @@ tr.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(tr) if "zero_spans_kernel" in r["Kernel_Name"]]
 if len(starts) < 3:
     sys.exit(f"{path}: fewer than 3 training steps in the trace")
-steady = tr[starts[1]:]                     # from the first graph replay on (step 0 = eager warm-up)
-nsteps = len(starts) - 1
-bounds = [int(tr[i]["Start_Timestamp"]) for i in starts[1:]] + [int(tr[-1]["End_Timestamp"])]
-walls = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
+# steps = zero_spans-to-zero_spans segments from the first graph replay on (step 0 = eager warm-up); segments whose
+# kernel count differs from the typical step's (extra eager / calibration launches, e.g. the fp8 path's amax warm-up
+# before its capture) are left out, so the figures describe graph-replayed steps only
+segs = [(starts[i], starts[i + 1] if i + 1 < len(starts) else len(tr)) for i in range(1, len(starts))]
+mode = collections.Counter(b - a for a, b in segs[:-1] or segs).most_common(1)[0][0]
+segs = [(a, b) for a, b in segs if b - a == mode or (b == len(tr) and b - a >= mode)]
+nsteps = len(segs)
+steady = [r for a, b in segs for r in tr[a:a + mode]]
+walls = [(int(tr[b]["Start_Timestamp"]) if b < len(tr) else int(tr[a + mode - 1]["End_Timestamp"]))
+         - int(tr[a]["Start_Timestamp"]) for a, b in segs]
 per = collections.defaultdict(lambda: [0, 0])
 busy = 0
 for r in steady:
@@ -32,7 +38,7 @@ for r in steady:
     per[name][0] += t
     per[name][1] += 1
     busy += t
-wall = bounds[-1] - bounds[0]
+wall = sum(walls)
 print(f"steady state: {nsteps} graph-replayed steps (eager warm-up + dataset render excluded)")
 print(f"step wall-clock {wall / nsteps / 1e3:.1f} us (min {min(walls) / 1e3:.1f}, max {max(walls) / 1e3:.1f}); "
       f"kernel busy {busy / nsteps / 1e3:.1f} us/step; idle between kernels {100 * (1 - busy / wall):.1f}%; "
