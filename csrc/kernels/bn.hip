@@ -235,6 +235,9 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
 // argmax up to 4x from L2). Window (i,j) holds pixel (dy,dx) at tap dy*3+dx, window (i-1,j) the top row at tap
 // 6+dx, window (i,j-1) the left column at tap dy*3+2, window (i-1,j-1) pixel (0,0) at tap 8. Same BN-backward sums
 // as node_bwd (sum g, sum g * xhat).
+// IPT items per thread per trip: all their window / argmax / BN-input loads are issued before any of them is routed
+// (one memory round trip per IPT items; the grid is capped, so the 128^2 level runs several trips per thread).
+template <int IPT>
 __global__ __launch_bounds__(NT) void node_pool_bwd_kernel(NodeBwdParams p) {
   __shared__ float red[2][4][256];
   const int G = p.C >> 3, lg = ilog2(G);
@@ -249,50 +252,69 @@ __global__ __launch_bounds__(NT) void node_pool_bwd_kernel(NodeBwdParams p) {
   const int Hh = p.H >> 1, Wh = p.W >> 1;
   const int total = (p.B * Hh * Wh) << lg;
   const int HWh = Hh * Wh;
-  for (int it = blockIdx.x * NT + threadIdx.x; it < total; it += gridDim.x * NT) {
-    const int blk = it >> lg, b = blk / HWh, r = blk - b * HWh, i = r / Wh, j = r - i * Wh;
-    // windows q = (wi, wj): 0 = (i, j), 1 = (i, j-1), 2 = (i-1, j), 3 = (i-1, j-1); missing ones read window 0
-    // with a tap no argmax holds
-    float u[4][8];
-    uint2 am[4];
+  const int stride = gridDim.x * NT;                     // a multiple of G: a thread's channel group never changes
+  for (int it0 = blockIdx.x * NT + threadIdx.x; it0 < total; it0 += IPT * stride) {
+    uint4 uw[IPT][4], yv[IPT][4];
+    uint2 am[IPT][4];
+    size_t pix0[IPT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool up = q >= 2, left = q & 1;
-      const bool ok = (!up || i > 0) && (!left || j > 0);
-      const int wi = ok ? i - up : i, wj = ok ? j - left : j;
-      const size_t o = ((size_t)(b * Hh + wi) * Wh + wj) * p.C + c0;
-      am[q] = *reinterpret_cast<const uint2*>(p.argmax + o);
-      load8(p.src[0].p + o, u[q]);
-      if (!ok) am[q] = make_uint2(0xffffffffu, 0xffffffffu);
+    for (int v = 0; v < IPT; ++v) {
+      const int itv = it0 + v * stride;
+      const int blk = (itv < total ? itv : it0) >> lg;   // clamped: every load issues, only valid items store
+      const int b = blk / HWh, r = blk - b * HWh, i = r / Wh, j = r - i * Wh;
+      // windows q = (wi, wj): 0 = (i, j), 1 = (i, j-1), 2 = (i-1, j), 3 = (i-1, j-1); missing ones read window 0
+      // with a tap no argmax holds
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool up = q >= 2, left = q & 1;
+        const bool ok = (!up || i > 0) && (!left || j > 0);
+        const int wi = ok ? i - up : i, wj = ok ? j - left : j;
+        const size_t o = ((size_t)(b * Hh + wi) * Wh + wj) * p.C + c0;
+        am[v][q] = *reinterpret_cast<const uint2*>(p.argmax + o);
+        uw[v][q] = *reinterpret_cast<const uint4*>(p.src[0].p + o);
+        if (!ok) am[v][q] = make_uint2(0xffffffffu, 0xffffffffu);
+      }
+      pix0[v] = (size_t)(b * p.H + 2 * i) * p.W + 2 * j;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        yv[v][d] = stats ? *reinterpret_cast<const uint4*>(p.v + (pix0[v] + (d >> 1) * p.W + (d & 1)) * p.C + c0)
+                         : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int dy = d >> 1, dx = d & 1;
-      const size_t pix = ((size_t)(b * p.H + 2 * i + dy) * p.W + 2 * j + dx);
-      float y[8], g[8];
-      if (stats) load8(p.v + pix * p.C + c0, y);
-      // taps of this pixel in windows 0..3 (64 = not contained)
-      const uint32_t tw[4] = {(uint32_t)(dy * 3 + dx), dx == 0 ? (uint32_t)(dy * 3 + 2) : 64u,
-                              dy == 0 ? (uint32_t)(6 + dx) : 64u, (dy == 0 && dx == 0) ? 8u : 64u};
+    for (int v = 0; v < IPT; ++v) {
+      if (it0 + v * stride >= total) break;
+      float u[4][8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        float t = 0.f;
+      for (int q = 0; q < 4; ++q) unpack8(uw[v][q], u[q]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t word = jj < 4 ? am[q].x : am[q].y;
-          if (((word >> (8 * (jj & 3))) & 0xffu) == tw[q]) t += u[q][jj];
-        }
-        g[jj] = t;
-      }
-      const uint4 gv = pack8(g);
-      *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
-      if (stats) {
-        float gr[8];
-        unpack8(gv, gr);
+      for (int d = 0; d < 4; ++d) {
+        const int dy = d >> 1, dx = d & 1;
+        const size_t pix = pix0[v] + dy * p.W + dx;
+        // taps of this pixel in windows 0..3 (64 = not contained)
+        const uint32_t tw[4] = {(uint32_t)(dy * 3 + dx), dx == 0 ? (uint32_t)(dy * 3 + 2) : 64u,
+                                dy == 0 ? (uint32_t)(6 + dx) : 64u, (dy == 0 && dx == 0) ? 8u : 64u};
+        float g[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          s[0][jj] += gr[jj];
-          s[1][jj] += gr[jj] * (y[jj] - mean[jj]) * rstd[jj];
+          float t = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = jj < 4 ? am[v][q].x : am[v][q].y;
+            if (((word >> (8 * (jj & 3))) & 0xffu) == tw[q]) t += u[q][jj];
+          }
+          g[jj] = t;
+        }
+        const uint4 gv = pack8(g);
+        *reinterpret_cast<uint4*>(p.out + pix * p.C + c0) = gv;
+        if (stats) {
+          float gr[8], y[8];
+          unpack8(gv, gr);
+          unpack8(yv[v][d], y);
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            s[0][jj] += gr[jj];
+            s[1][jj] += gr[jj] * (y[jj] - mean[jj]) * rstd[jj];
+          }
         }
       }
     }
@@ -407,7 +429,10 @@ int node_bwd(const NodeBwdParams& p, hipStream_t st) {
     const int pcap = cfl_tune(TUNE_NODE_POOL_BLOCKS) > 0 ? cfl_tune(TUNE_NODE_POOL_BLOCKS) : cap;
     if (b2 > pcap) b2 = pcap;
     if (b2 < 1) b2 = 1;
-    hipLaunchKernelGGL(node_pool_bwd_kernel, dim3(b2), dim3(NT), 0, st, p);
+    // one item per thread per trip: 2 (TUNE_NODE_POOL_IPT=2) needs 188 VGPRs (occupancy 3 -> 2) and measured slower
+    // (whole step 1.4652-1.4664 vs 1.4580-1.4616 ms/iteration)
+    if (cfl_tune(TUNE_NODE_POOL_IPT) == 2) hipLaunchKernelGGL(node_pool_bwd_kernel<2>, dim3(b2), dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL(node_pool_bwd_kernel<1>, dim3(b2), dim3(NT), 0, st, p);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   // specialised instances for the engine's source combinations (fewer live registers, no mode branches)

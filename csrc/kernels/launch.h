@@ -409,7 +409,8 @@ enum TuneKey {
   TUNE_PW = 25,                // plain 1x1 convs: 0 = streaming kernel (pw.hip), 1 = conv_igemm tiles
   TUNE_PW_BLOCKS = 26,         // streaming 1x1 kernel: resident-grid cap (default 512 = 2 blocks per CU)
   TUNE_PW_DEPTH = 27,          // streaming 1x1 kernel: tiles in flight per wave (1 default, 2, 4 at K = 32)
-  TUNE_N = 28
+  TUNE_NODE_POOL_IPT = 28,     // max-pool node gradient: 2x2 items per thread per trip (1 default, 2)
+  TUNE_N = 29
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -902,8 +902,8 @@ def test_evaluator_engine_matches_per_batch_eval():
         assert abs(big["accuracy"] - small["accuracy"]) < 1e-6
 
 
-@pytest.mark.parametrize("B,H,C", [(2, 16, 64), (3, 8, 128), (1, 32, 32)])
-def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C):
+@pytest.mark.parametrize("B,H,C,cap", [(2, 16, 64, 0), (3, 8, 128, 0), (1, 32, 32, 0), (2, 34, 64, 3)])
+def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C, cap):
     """node_pool_bwd_kernel (one 2x2 input block per item, each pooled window read once) == the per-pixel gather
     of node_bwd<GM_MAXPOOL> (bit-identical gradient, same BN-backward sums), on argmaxes from the real forward."""
     C_ = hip()
@@ -920,8 +920,12 @@ def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C):
     C_.pool_res_fwd(yb, ab, res, x, am, B, H, H, C)          # argmaxes as the engine's forward records them
     dxb, _ = bf(torch.randn(B, Ho, Ho, C))
     outs = []
-    for tune in (1, 0):                                          # 1 = per-pixel gather, 0 = 2x2 blocks
+    # 1 = per-pixel gather; 0 = 2x2 blocks with 1 (default) or 2 items per thread per trip; cap > 0: a grid of `cap`
+    # blocks, so every thread runs several trips (and the last one a half-valid item pair)
+    for tune, ipt in ((1, 0), (0, 0), (0, 2)):
         C_.set_tune(C_.TUNE_NODE_POOL2X2, tune)
+        C_.set_tune(C_.TUNE_NODE_POOL_IPT, ipt)
+        C_.set_tune(C_.TUNE_NODE_POOL_BLOCKS, cap)
         try:
             g = torch.zeros(B, H, H, C, dtype=torch.int16, device=DEV)
             sums = torch.zeros(16 * 2 * C, device=DEV)
@@ -929,8 +933,11 @@ def test_maxpool_node_2x2_blocks_match_per_pixel_gather(B, H, C):
             outs.append((g.clone(), sums.view(16, 2, C).sum(0).cpu()))
         finally:
             C_.set_tune(C_.TUNE_NODE_POOL2X2, 0)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-3)
+            C_.set_tune(C_.TUNE_NODE_POOL_IPT, 0)
+            C_.set_tune(C_.TUNE_NODE_POOL_BLOCKS, 0)
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.allclose(outs[0][1], o[1], rtol=1e-4, atol=1e-3)
     # every pooled gradient lands exactly once: total mass is preserved
     assert abs(float(from_bits(outs[1][0]).sum()) - float(from_bits(dxb).sum())) < 1e-2 * B * H * H
 
