@@ -277,6 +277,10 @@ class UNetEngine:
         # ... or only at the levels whose side is <= CFL_BNB_FOLD_RES (the low-resolution bn_bwd_apply passes are
         # launch-bound: 4.3 us for 1-6 MB, profiles/r2_final/roofline.txt)
         self.fold_res = int(os.environ.get("CFL_BNB_FOLD_RES", "0"))
+        # ... and (default) into the encoder's pointwise data gradients: the streaming 1x1 kernel (pw.hip) applies it
+        # to its B-fragment registers and stores dx from the first output slice's blocks - 6 bn_bwd_apply launches
+        # fewer, whole step 1.4421-1.4524 -> 1.4358-1.4361 ms/iteration (CFL_BNB_FOLD_PW=0: separate passes)
+        self.fold_pw = os.environ.get("CFL_BNB_FOLD_PW", "1") != "0"
         # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
         # dgrad launch plus a deferred, grouped wgrad)
         self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
@@ -638,7 +642,7 @@ class UNetEngine:
             else:
                 xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
             bnb, bna = self.bn[b2], self.bn[b1]
-            fold = self._fold_at(H)
+            fold = self._fold_at(H) or self.fold_pw
             # BN_b node: routed through the max-pool (no ReLU)
             C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
                        bnb["sums"], B, H, H, F, self.RS)

@@ -31,13 +31,18 @@ CFL_DEVICE int wswz(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3);
 template <int K>
 constexpr int pw_rows() { return K >= 128 ? 4096 / K : 64; }   // pixels per wave tile (A: WR*K/128 VGPRs)
 
-template <int NB, int K, int D>
+// BWD: the input is the gradient g w.r.t. a BatchNorm output and the operand is its BN-backward apply (common.h
+// BnBwdIn, the bn_bwd_apply arithmetic): g and the BN input y are loaded into the B-fragment registers and combined
+// right before the MFMAs; the blocks of output slice 0 also store dx (each pixel once) for the weight gradient, and
+// block 0 writes dgamma / dbeta. Replaces a bn_bwd_apply pass (one write + read of dx and a launch fewer).
+template <int NB, int K, int D, bool BWD>
 __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices) {
   constexpr int WR = pw_rows<K>();
   constexpr int MF = WR / 16, NF = NB / 16, KS = K / 32;
   __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
   __shared__ __attribute__((aligned(16))) float sBias[NB];
   __shared__ float sred[2][NT / 64][NB];
+  __shared__ float sco[BWD ? 5 * K + NT : 1];            // BN-backward coefficients (bnb_prologue)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, q = lane >> 4;
@@ -54,21 +59,24 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
   // B operand: lane (r16, q) holds pixel m0 + i*16 + r16, channels s*32 + q*8 .. +7. Rows past M are clamped to the
   // last pixel (their results are neither stored nor counted).
   s8v a[D][MF][KS];
-  auto load = [&](s8v (&buf)[MF][KS], int tt) {
+  uint4 ya[BWD ? D : 1][MF][KS];                         // BWD: the BN input y of the same elements
+  auto load = [&](int d, int tt) {
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       int m = tt * WR + i * 16 + r16;
       m = m < p.M ? m : p.M - 1;
-      const bf16_t* src = p.x + (size_t)m * K + q * 8;
+      const size_t off = (size_t)m * K + q * 8;
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        buf[i][s] = *reinterpret_cast<const s8v*>(src + s * 32);
+      for (int s = 0; s < KS; ++s) {
+        a[d][i][s] = *reinterpret_cast<const s8v*>(p.x + off + s * 32);
+        if constexpr (BWD) ya[d][i][s] = *reinterpret_cast<const uint4*>(p.bwd.y + off + s * 32);
+      }
     }
   };
   // D tiles in flight per wave: the first D tiles' loads are issued while the weights are staged
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (t + d * wstride < tiles) load(a[d], t + d * wstride);
+    if (t + d * wstride < tiles) load(d, t + d * wstride);
 
   for (int c = tid; c < NB * K / 8; c += NT) {
     const int n = c / (K / 8), kc = c - n * (K / 8);
@@ -76,7 +84,8 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
         *reinterpret_cast<const uint4*>(p.wt + (size_t)(n0 + n) * K + kc * 8);
   }
   if (tid < NB) sBias[tid] = p.bias ? p.bias[n0 + tid] : 0.f;
-  __syncthreads();
+  if constexpr (BWD) bnb_prologue<NT>(p.bwd, K, sco, sco + 5 * K, blockIdx.x == 0);   // ends with a barrier
+  else __syncthreads();
 
   const bool stats = p.stats != nullptr;
   float s1[NF][4], s2[NF][4];
@@ -90,11 +99,27 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
     for (int d = 0; d < D; ++d) {
       const int tt = t + d * wstride;
       if (tt >= tiles) break;
-      // opaque zero: keeps the (loop-invariant) weight fragment reads inside the loop - hoisted, NF*KS fragments would
-      // stay live in registers across the whole loop and spill
+      // opaque zero: keeps the (loop-invariant) weight fragment / BN-coefficient reads inside the loop - hoisted,
+      // they would stay live in registers across the whole loop and spill
       int wo = 0;
       asm volatile("" : "+v"(wo));
       const bf16_t* sWt = sW + wo;
+      if constexpr (BWD) {
+        // dx = BN-backward apply of (g, y); slice-0 blocks store it (rows past M are clamped copies: not stored)
+        const bool side = slice == 0 && p.bwd.dx != nullptr;
+        const float* co = sco + wo;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int m = tt * WR + i * 16 + r16;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const uint4 dx = bnb_apply8(*reinterpret_cast<const uint4*>(&a[d][i][s]), ya[d][i][s], co, K,
+                                        s * 32 + q * 8);
+            a[d][i][s] = *reinterpret_cast<const s8v*>(&dx);
+            if (side && m < p.M) *reinterpret_cast<uint4*>(p.bwd.dx + (size_t)m * K + s * 32 + q * 8) = dx;
+          }
+        }
+      }
       f4v acc[NF][MF];
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf)
@@ -110,7 +135,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
             acc[nf][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[d][i][s], acc[nf][i], 0, 0, 0);
         }
       const int m0 = tt * WR;
-      if (tt + D * wstride < tiles) load(a[d], tt + D * wstride);   // refill this buffer: D tiles stay in flight
+      if (tt + D * wstride < tiles) load(d, tt + D * wstride);   // refill this buffer: D tiles stay in flight
 
       // D = W * X^T: lane (r16, q) holds output channels n0 + nf*16 + q*4 + r (r = 0..3) of pixel m0 + i*16 + r16.
       // Fragments nf = 2h, 2h+1 are paired: lanes q, q^1 (lane +- 16) swap one 8-byte half each so every lane owns
@@ -183,6 +208,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
 
 template <int NB, int K, int D>
 void launch_d(const ConvParams& p, hipStream_t st) {
+  const bool bwd = p.bwd.y != nullptr;
   constexpr int WR = pw_rows<K>();
   const int nslices = p.N / NB;
   const int tiles = (p.M + WR - 1) / WR;
@@ -196,13 +222,20 @@ void launch_d(const ConvParams& p, hipStream_t st) {
   tpw = (tpw + D - 1) / D * D;
   const int waves = (tiles + tpw - 1) / tpw;
   const int bps = ((waves + 3) / 4 + 7) / 8 * 8;
-  hipLaunchKernelGGL((pw_kernel<NB, K, D>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+  if constexpr (D == 1) {
+    if (bwd) {
+      hipLaunchKernelGGL((pw_kernel<NB, K, 1, true>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((pw_kernel<NB, K, D, false>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
 }
 
 template <int NB, int K>
 void launch(const ConvParams& p, hipStream_t st) {
   int d = cfl_tune(TUNE_PW_DEPTH);
-  if (d <= 0) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration
+  if (d <= 0 || p.bwd.y) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration; the
+                                  // BN-backward form holds y as well and runs at depth 1 only (deeper rings spill)
   if constexpr (K == 32) {                                // deeper rings spill at K >= 64
     if (d >= 4) return launch_d<NB, K, 4>(p, st);
   }
@@ -217,7 +250,8 @@ bool pw_conv_supported(const ConvParams& p) {
          p.pad_t == 0 && p.pad_l == 0 && !p.up_in && p.Ho == p.Hin && p.Wo == p.Win && p.K == p.Cin &&
          (p.Cin == 32 || p.Cin == 64 || p.Cin == 128 || p.Cin == 256) && (p.N == 32 || p.N % 64 == 0) &&
          p.xf.ab == nullptr && !p.xf.relu && p.node.y == nullptr && p.join.mode == JOIN_NONE &&
-         p.bwd.y == nullptr && p.pj.v == nullptr && p.xfin.stats == nullptr && p.fin.gamma == nullptr && p.M > 0;
+         (p.bwd.y == nullptr || (p.bwd.dx != nullptr && p.bwd.reps <= BNB_MAX_REPS)) && p.pj.v == nullptr &&
+         p.xfin.stats == nullptr && p.fin.gamma == nullptr && p.M > 0;
 }
 
 int pw_conv(const ConvParams& p, hipStream_t st) {

@@ -1246,8 +1246,12 @@ def test_folder_dataset_device_resize_matches_host(tmp_path):
 
 
 @pytest.mark.parametrize("ks,Cin,N,H,B,tune,split,node", [
-    (1, 64, 32, 16, 2, None, False, False),          # 1x1 generic, 128x32 tiles
-    (1, 128, 128, 128, 4, None, False, False),       # 1x1 generic, 128x128 tiles (M >= 65536)
+    (1, 64, 32, 16, 2, None, False, False),          # 1x1: streaming kernel (pw.hip), N = 32 slices
+    (1, 128, 128, 128, 4, None, False, False),       # 1x1: streaming kernel, 2 output slices, long persistent loop
+    (1, 256, 128, 10, 3, None, False, False),        # 1x1: streaming kernel, K = 256, ragged last tile (M = 300)
+    (1, 32, 64, 33, 2, None, False, False),          # 1x1: streaming kernel, K = 32, ragged rows
+    (1, 64, 32, 16, 2, "pw_off", False, False),      # 1x1 generic, 128x32 tiles
+    (1, 128, 128, 128, 4, "pw_off", False, False),   # 1x1 generic, 128x128 tiles (M >= 65536)
     (1, 64, 64, 24, 2, "igemm_cfg", False, False),   # forced tile config: not folded -> bn_bwd_apply + conv
     (3, 64, 64, 16, 2, None, False, True),           # halo tile kernel (whole-chunk B) + BN-node epilogue
     (3, 64, 64, 16, 2, None, True, False),           # ... split over the 2 input chunks
@@ -1263,7 +1267,8 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
     vs the fp32 formula."""
     torch.manual_seed(41)
     C_ = hip()
-    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "igemm_cfg": (C_.TUNE_IGEMM_CFG, 3)}
+    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "igemm_cfg": (C_.TUNE_IGEMM_CFG, 3),
+            "pw_off": (C_.TUNE_PW, 1)}
     if tune:
         C_.set_tune(*keys[tune])
     try:
@@ -1320,7 +1325,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
