@@ -281,6 +281,9 @@ class UNetEngine:
         # to its B-fragment registers and stores dx from the first output slice's blocks - 6 bn_bwd_apply launches
         # fewer, whole step 1.4421-1.4524 -> 1.4358-1.4361 ms/iteration (CFL_BNB_FOLD_PW=0: separate passes)
         self.fold_pw = os.environ.get("CFL_BNB_FOLD_PW", "1") != "0"
+        # ... and into the entry conv's weight gradient, its only consumer (whole step 1.4412-1.4416 -> 1.4328-1.4346
+        # ms/iteration; CFL_BNB_FOLD_ENTRY=0: a separate pass)
+        self.fold_entry = os.environ.get("CFL_BNB_FOLD_ENTRY", "1") != "0"
         # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
         # dgrad launch plus a deferred, grouped wgrad)
         self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
@@ -707,10 +710,16 @@ class UNetEngine:
             if k > 0:
                 dx_out = out
             else:
-                C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
-                               self.G(names[1], "beta"), B * H * H, cin, self.RS)
-                C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
-                              ENTRY_FILTERS, self.C.STAT_REPLICAS)
+                if self.fold_entry:        # the entry BN's backward apply folded into the entry wgrad's dy load
+                    C.entry_wgrad(self.images, self.idx, D["g0"], self.gslab[(names[0], "kernel")], B, self.S,
+                                  ENTRY_FILTERS, self.C.STAT_REPLICAS, bwd_y=A["y0"], bwd_ab=bn0["ab"],
+                                  bwd_sums=bn0["sums"], bwd_reps=self.RS, bwd_dx=D["dy0"],
+                                  bwd_dgamma=self.G(names[1], "gamma"), bwd_dbeta=self.G(names[1], "beta"))
+                else:
+                    C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
+                                   self.G(names[1], "beta"), B * H * H, cin, self.RS)
+                    C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
+                                  ENTRY_FILTERS, self.C.STAT_REPLICAS)
 
     def optimizer_step(self) -> None:
         self._await_all()

@@ -355,8 +355,11 @@ void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bi
   ok(entry_fwd(p, stream()), "entry_fwd");
 }
 
+// bwd_y given: dy is the gradient w.r.t. the entry BN's output and the operand its BN-backward apply (folded into
+// the dy load; bwd_dx is only written by the unfolded fallback)
 void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor dw, int B, int S, int Cout,
-                    int replicas) {
+                    int replicas, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
+                    OptT bwd_dbeta) {
   EntryParams p{};
   p.replicas = replicas < 1 ? 1 : replicas;
   p.images = ptr<const uint8_t>(images, "images");
@@ -366,6 +369,21 @@ void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor
   p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
   TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout && dw.numel() == (int64_t)p.replicas * 27 * Cout,
               "entry_wgrad sizes");
+  if (bwd_y) {
+    TORCH_CHECK(bwd_ab && bwd_sums, "entry_wgrad: bwd_y needs bwd_ab and bwd_sums");
+    TORCH_CHECK(Cout <= BNB_MAX_C && bwd_reps >= 1 && bwd_reps <= BNB_MAX_REPS && bwd_y->numel() == dy.numel() &&
+                bwd_ab->numel() >= 4 * Cout && bwd_sums->numel() >= (int64_t)bwd_reps * 2 * Cout &&
+                (!bwd_dx || bwd_dx->numel() == dy.numel()) && (!bwd_dgamma || bwd_dgamma->numel() >= Cout) &&
+                (!bwd_dbeta || bwd_dbeta->numel() >= Cout), "entry_wgrad: bwd tensor sizes");
+    p.bwd.y = ptr<const bf16_t>(*bwd_y, "bwd_y");
+    p.bwd.ab = ptr<const float>(*bwd_ab, "bwd_ab");
+    p.bwd.sums = ptr<const float>(*bwd_sums, "bwd_sums");
+    p.bwd.reps = bwd_reps;
+    p.bwd.invM = 1.f / (float)((int64_t)B * p.Ho * p.Wo);
+    p.bwd.dx = optr<bf16_t>(bwd_dx, "bwd_dx");
+    p.bwd.dgamma = optr<float>(bwd_dgamma, "bwd_dgamma");
+    p.bwd.dbeta = optr<float>(bwd_dbeta, "bwd_dbeta");
+  }
   ok(entry_wgrad(p, stream()), "entry_wgrad");
 }
 
@@ -779,7 +797,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
         py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
   m.def("entry_wgrad", &entry_wgrad_op, py::arg("images"), py::arg("idx"), py::arg("dy"), py::arg("dw"), py::arg("B"),
-        py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1);
+        py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1, py::arg("bwd_y") = py::none(),
+        py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(), py::arg("bwd_reps") = 1,
+        py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(), py::arg("bwd_dbeta") = py::none());
   m.def("make_grad_finish_table", &make_grad_finish_table);
   m.def("grad_finish", &grad_finish_op);
   m.def("make_zero_table", &make_zero_table);

@@ -282,11 +282,30 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
   }
 }
 
+// BWD: the entry BN's backward apply folded into the dy load (p.bwd; the bn_bwd_apply arithmetic, bit-identical):
+// g and y are loaded together and dx = a * (g - s0/M - xhat * s1/M) is formed right before the LDS store, with this
+// thread's 8 channels' coefficients held in registers; block 0 writes dgamma / dbeta. dx itself is never stored.
+template <bool BWD>
 __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int nch, int steps, int replicas) {
   __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sG[2][ECH][ELD];
   __shared__ float red[4][32 * 32];
+  __shared__ float sco[BWD ? 5 * 32 + NT : 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // this thread's dy channels (tid & 3) * 8 .. +7 (e & 3 below with e = tid + NT * k)
+  float ca[8], cm[8], cr[8], k1[8], k2[8];
+  if constexpr (BWD) {
+    bnb_prologue<NT>(p.bwd, 32, sco, sco + 5 * 32, blockIdx.x == 0);
+    const int c0 = (tid & 3) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = sco[c0 + j];
+      cm[j] = sco[32 + c0 + j];
+      cr[j] = sco[64 + c0 + j];
+      k1[j] = sco[96 + c0 + j];
+      k2[j] = sco[128 + c0 + j];
+    }
+  }
   const int g = lane >> 4, r16 = lane & 15;
   // A operand (X^T): lane holds tap row 16i + r16 at pixels 32*wid + 8g + 0..7 (column stride 2 pixels = 6 bytes)
   int aoff[2][8], astr[8];
@@ -297,15 +316,18 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
     astr[j] = 6 * j;
   }
   uint32_t rv[3];
-  uint4 gv[2];
+  uint4 gv[2], yv[BWD ? 2 : 1];
+  bool okv[2];
   auto load = [&](int s) {
     const int row = s / nch, ow0 = (s % nch) * ECH;
     rows_load(p, row, ow0, rv);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + NT * k, ow = ow0 + (e >> 2);
-      gv[k] = ow < p.Wo ? *reinterpret_cast<const uint4*>(p.dy + ((size_t)row * p.Wo + ow) * 32 + (e & 3) * 8)
-                        : make_uint4(0, 0, 0, 0);
+      const size_t off = ((size_t)row * p.Wo + ow) * 32 + (e & 3) * 8;
+      okv[k] = ow < p.Wo;
+      gv[k] = okv[k] ? *reinterpret_cast<const uint4*>(p.dy + off) : make_uint4(0, 0, 0, 0);
+      if constexpr (BWD) yv[k] = okv[k] ? *reinterpret_cast<const uint4*>(p.bwd.y + off) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&](int b) {
@@ -313,7 +335,18 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + NT * k;
-      *reinterpret_cast<uint4*>(&sG[b][e >> 2][(e & 3) * 8]) = gv[k];
+      uint4 v = gv[k];
+      if constexpr (BWD) {
+        if (okv[k]) {                                  // pixels past the row stay zero
+          float g[8], y[8], o[8];
+          unpack8(v, g);
+          unpack8(yv[k], y);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = bnb_apply(g[j], y[j], ca[j], cm[j], cr[j], k1[j], k2[j]);
+          v = pack8(o);
+        }
+      }
+      *reinterpret_cast<uint4*>(&sG[b][e >> 2][(e & 3) * 8]) = v;
     }
   };
   f4v acc[2][2];
@@ -390,11 +423,32 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
   const int reps = p.replicas > 1 ? p.replicas : 1;
+  if (p.bwd.y && (!use_mfma(p) || p.bwd.reps > BNB_MAX_REPS)) {   // unfolded: bn_bwd_apply into bwd.dx, then dy = dx
+    if (p.bwd.dx == nullptr) return 5;
+    BnBwdApplyParams a{};
+    a.g = p.dy;
+    a.y = p.bwd.y;
+    a.ab = p.bwd.ab;
+    a.sums = p.bwd.sums;
+    a.dy = p.bwd.dx;
+    a.dgamma = p.bwd.dgamma;
+    a.dbeta = p.bwd.dbeta;
+    a.M = p.B * p.Ho * p.Wo;
+    a.C = p.Cout;
+    a.sum_reps = p.bwd.reps;
+    const int rc = bn_bwd_apply(a, st);
+    if (rc) return rc;
+    EntryParams q = p;
+    q.dy = p.bwd.dx;
+    q.bwd = BnBwdIn{};
+    return entry_wgrad(q, st);
+  }
   if (use_mfma(p)) {
     const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
     const int mcap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 512;
-    hipLaunchKernelGGL(entry_wgrad_mfma_kernel, dim3(steps < mcap ? steps : mcap), dim3(NT), 0, st, p, nch, steps,
-                       reps);
+    const dim3 grid(steps < mcap ? steps : mcap);
+    if (p.bwd.y) hipLaunchKernelGGL(entry_wgrad_mfma_kernel<true>, grid, dim3(NT), 0, st, p, nch, steps, reps);
+    else hipLaunchKernelGGL(entry_wgrad_mfma_kernel<false>, grid, dim3(NT), 0, st, p, nch, steps, reps);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   const int cap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 256;   // measured

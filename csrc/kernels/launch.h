@@ -215,6 +215,8 @@ struct EntryParams {
   int B, S, Cout, Ho, Wo;
   int replicas;            // wgrad: >1 = spread block atomics over that many row copies (summed by grad_finish)
   BnFinal fin;             // forward: in-launch finalize of `stats`
+  BnBwdIn bwd;             // wgrad: dy is the gradient g w.r.t. the entry BN's output and the operand its BN-backward
+                           // apply (common.h; y = the conv output, computed on load; dx stored only on the fallback)
 };
 int entry_fwd(const EntryParams& p, hipStream_t st);
 int entry_wgrad(const EntryParams& p, hipStream_t st);

@@ -984,6 +984,49 @@ def test_entry_conv_mfma_and_valu_match_reference(S, B):
     assert rel(ys[0], ys[1]) < 1e-2
 
 
+@pytest.mark.parametrize("S,B,algo", [(64, 3, 0), (256, 2, 0), (100, 2, 0), (64, 2, 1)])
+def test_entry_wgrad_bwd_fold_matches_unfolded(S, B, algo):
+    """The entry BN's backward apply folded into the entry weight gradient's dy load (entry_wgrad bwd_y=...) equals
+    bn_bwd_apply + the plain entry wgrad bit for bit (weight-gradient rows, dgamma, dbeta); algo 1 (VALU kernels)
+    takes the unfolded fallback, which also stores dx."""
+    C = hip()
+    torch.manual_seed(37)
+    g = torch.Generator().manual_seed(37)
+    imgs = torch.randint(0, 256, (5, S, S, 3), dtype=torch.uint8, generator=g).to(DEV)
+    idx = torch.tensor([4, 0, 2][:B], dtype=torch.int32, device=DEV)
+    Ho = (S + 1) // 2
+    M, reps = B * Ho * Ho, 4
+    gb, _ = bf(torch.randn(B, Ho, Ho, 32))
+    yb, _ = bf(torch.randn(B, Ho, Ho, 32) * 0.7 + 0.2)
+    ab, _, _ = ab_for(32, 13)
+    ab[64:96], ab[96:] = torch.randn(32) * 0.1 + 0.2, torch.rand(32) + 0.6
+    ab = ab.to(DEV)
+    sums = (torch.randn(reps, 2, 32) * (M / reps) ** 0.5).reshape(-1).to(DEV)
+    C.set_tune(C.TUNE_ENTRY_ALGO, algo)
+    try:
+        outs = []
+        for fold in (True, False):
+            dw = torch.zeros(4 * 27 * 32, device=DEV)
+            dx = torch.zeros_like(gb)
+            dgam, dbet = torch.zeros(32, device=DEV), torch.zeros(32, device=DEV)
+            if fold:
+                C.entry_wgrad(imgs, idx, gb, dw, B, S, 32, 4, bwd_y=yb, bwd_ab=ab, bwd_sums=sums, bwd_reps=reps,
+                              bwd_dx=dx, bwd_dgamma=dgam, bwd_dbeta=dbet)
+            else:
+                C.bn_bwd_apply(gb, yb, ab, sums, dx, dgam, dbet, M, 32, reps)
+                C.entry_wgrad(imgs, idx, dx, dw, B, S, 32, 4)
+            torch.cuda.synchronize()
+            outs.append((dw.view(4, -1).sum(0).cpu(), dgam.cpu(), dbet.cpu(), dx.cpu()))
+    finally:
+        C.set_tune(C.TUNE_ENTRY_ALGO, 0)
+    f, u = outs
+    # the wgrad's replica-row atomics add in a run-dependent order: equal up to fp32 summation-order noise
+    assert torch.allclose(f[0], u[0], rtol=1e-5, atol=1e-3), float((f[0] - u[0]).abs().max())
+    assert torch.equal(f[1], u[1]) and torch.equal(f[2], u[2])
+    if algo == 1:
+        assert torch.equal(f[3], u[3])
+
+
 @pytest.mark.parametrize("dice", [0, 1])
 def test_head_loss_metrics_and_gradients_match_autograd(dice):
     """head.hip (4 lanes per low-resolution pixel: 8 channels and one sub-pixel of the 2x2 target block each):
@@ -1325,7 +1368,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
