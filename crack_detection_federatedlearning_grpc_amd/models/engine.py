@@ -281,6 +281,10 @@ class UNetEngine:
         # to its B-fragment registers and stores dx from the first output slice's blocks - 6 bn_bwd_apply launches
         # fewer, whole step 1.4421-1.4524 -> 1.4358-1.4361 ms/iteration (CFL_BNB_FOLD_PW=0: separate passes)
         self.fold_pw = os.environ.get("CFL_BNB_FOLD_PW", "1") != "0"
+        # decoder residual-conv gradient dq = 2x2 sums of dxlo formed in its 1x1 dgrad's operand load (pw.hip) instead
+        # of a node_bwd pass: 3 launches fewer, whole step 1.4574-1.4693 -> 1.4463-1.4493 ms/iteration on the same box
+        # (CFL_SUM2X2_FOLD=0: the separate pass)
+        self.fold_sum2x2 = os.environ.get("CFL_SUM2X2_FOLD", "1") != "0"
         # ... and into the entry conv's weight gradient, its only consumer (whole step 1.4412-1.4416 -> 1.4328-1.4346
         # ms/iteration; CFL_BNB_FOLD_ENTRY=0: a separate pass)
         self.fold_entry = os.environ.get("CFL_BNB_FOLD_ENTRY", "1") != "0"
@@ -588,16 +592,20 @@ class UNetEngine:
                 C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
                                self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
+            # (k > 0, default) the 2x2 sum is formed by the dgrad's operand load, which also stores dq for the
+            # weight gradient (issued after it)
+            s2 = k > 0 and self.fold_sum2x2
             if k == 0:
                 dq = dxlo
             else:
                 dq = D[f"d{k}_dq"]
-                C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
-            self._side(lambda: self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
-                                           F, 1, 1, 0, 0, 0))
+                if not s2:
+                    C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
-                         prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0)
+                         prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if s2 else {}))
+            self._side(lambda: self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
+                                           F, 1, 1, 0, 0, 0))
             # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue; folded: its operand is
             # BN_B's backward apply of g_B (it stores dc = that dx for the weight gradient)
             self._igemm(gB if fold else D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None,

@@ -98,7 +98,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
                    int pj_reps, OptT jfin_stats, OptT jfin_gamma, OptT jfin_beta, double jfin_count,
                    double jfin_eps, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count,
-                   double xfin_eps) {
+                   double xfin_eps, OptT sum2x2) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -176,6 +176,11 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
     p.pj.sab = optr<const float>(pj_sab, "pj_sab");
     p.pj.sums = p.pj.sy ? ptr<float>(*pj_sums, "pj_sums") : nullptr;
     p.pj.reps = pj_reps < 1 ? 1 : pj_reps;
+  }
+  if (sum2x2) {                     // x = 2x2-block sums of sum2x2, formed on load and stored into x
+    TORCH_CHECK(sum2x2->numel() == 4 * x.numel() && ks == 1 && stride == 1 && !up_in && !ab && !relu && !bwd_y &&
+                !p.bias && !p.stats && !node_y && !join_mode && !pj_v, "conv_igemm: sum2x2 is a plain 1x1 dgrad input");
+    p.sum2x2 = ptr<const bf16_t>(*sum2x2, "sum2x2");
   }
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
@@ -760,7 +765,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pj_sums") = py::none(), py::arg("pj_reps") = 1, py::arg("jfin_stats") = py::none(),
         py::arg("jfin_gamma") = py::none(), py::arg("jfin_beta") = py::none(), py::arg("jfin_count") = 0.0,
         py::arg("jfin_eps") = 1e-3, py::arg("xfin_stats") = py::none(), py::arg("xfin_gamma") = py::none(),
-        py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3);
+        py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3,
+        py::arg("sum2x2") = py::none());
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;

@@ -524,6 +524,19 @@ int conv_igemm_splits(const ConvParams& p) {
 
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
+  if (p.sum2x2 && !pw_conv_supported(p)) {   // 2x2-sum input on another kernel: node_bwd(GM_SUM2X2) into x first
+    NodeBwdParams q{};
+    q.src[0] = GradSrc{p.sum2x2, GM_SUM2X2, 0};
+    q.src[1] = GradSrc{nullptr, GM_NONE, 0};
+    q.v = p.x;                                // read as the (unused) node value: no ab, no mask, no sums
+    q.out = const_cast<bf16_t*>(p.x);
+    q.B = p.B; q.H = p.Hin; q.W = p.Win; q.C = p.Cin;
+    const int rc = node_bwd(q, st);
+    if (rc) return rc;
+    ConvParams r = p;
+    r.sum2x2 = nullptr;
+    return conv_igemm(r, st);
+  }
   if (p.join.mode && (p.ks != 1 || p.stats || p.node.y || p.N % 8)) return 5;   // joins: 1x1 residual convs only
   if (p.pj.v && !use3x3(p)) return 7;     // the decoder node join lives in the 3x3 halo kernels' epilogues
   if (p.xfin.stats && !use3x3(p)) {        // consumer-side finalize: 3x3 halo kernels only - finalize first here

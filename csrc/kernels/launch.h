@@ -128,6 +128,9 @@ struct ConvParams {
   BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;
                        // common.h). Data-gradient convs only: 1x1/s1 or 3x3/s1, no upsample, no xf; shapes a kernel
                        // does not fold fall back to bn_bwd_apply into bwd.dx + the plain conv (same results)
+  const bf16_t* sum2x2;  // optional: x = the 2x2-block sums of this [B, 2*Hin, 2*Win, Cin] gradient (node_bwd
+                         // GM_SUM2X2 order), formed on load by the streaming 1x1 kernel and stored into x (const cast)
+                         // for the weight gradient; other kernels run node_bwd into x first (same results)
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
 // plain 1x1 / stride-1 convs (no input transform, epilogue = bias + optional BN statistics): streaming MFMA kernel

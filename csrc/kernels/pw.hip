@@ -28,16 +28,21 @@ constexpr int NT = 256;
 // (conv_igemm.hip's swizzle: a fragment read of 16 consecutive rows at one quarter covers all 64 banks)
 CFL_DEVICE int wswz(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3); }
 
-template <int K>
-constexpr int pw_rows() { return K >= 128 ? 4096 / K : 64; }   // pixels per wave tile (A: WR*K/128 VGPRs)
+// pixels per wave tile (B operand: WR*K/128 VGPRs; the 2x2-sum input holds four times that while loading, so its
+// tiles are halved below K = 128)
+template <int K, bool S2 = false>
+constexpr int pw_rows() { return K >= 128 ? 4096 / K : (S2 ? 32 : 64); }
 
 // BWD: the input is the gradient g w.r.t. a BatchNorm output and the operand is its BN-backward apply (common.h
 // BnBwdIn, the bn_bwd_apply arithmetic): g and the BN input y are loaded into the B-fragment registers and combined
 // right before the MFMAs; the blocks of output slice 0 also store dx (each pixel once) for the weight gradient, and
 // block 0 writes dgamma / dbeta. Replaces a bn_bwd_apply pass (one write + read of dx and a launch fewer).
-template <int NB, int K, int D, bool BWD>
+// S2: the input is the 2x2-block sum of p.sum2x2 (the decoder residual conv's upsample gradient): the four full-
+// resolution pixels of each B-fragment pixel are loaded and summed ((o00 + o01) + (o10 + o11), rounded once: node_bwd's
+// GM_SUM2X2), and the slice-0 blocks store the sums into x for the weight gradient.
+template <int NB, int K, int D, bool BWD, bool S2 = false>
 __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices) {
-  constexpr int WR = pw_rows<K>();
+  constexpr int WR = pw_rows<K, S2>();
   constexpr int MF = WR / 16, NF = NB / 16, KS = K / 32;
   __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
   __shared__ __attribute__((aligned(16))) float sBias[NB];
@@ -60,16 +65,30 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
   // last pixel (their results are neither stored nor counted).
   s8v a[D][MF][KS];
   uint4 ya[BWD ? D : 1][MF][KS];                         // BWD: the BN input y of the same elements
+  uint4 qa[S2 ? D : 1][MF][KS][3];                       // S2: the other three pixels of each 2x2 block
   auto load = [&](int d, int tt) {
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       int m = tt * WR + i * 16 + r16;
       m = m < p.M ? m : p.M - 1;
       const size_t off = (size_t)m * K + q * 8;
+      if constexpr (S2) {
+        const int hw = p.Hin * p.Win, b = m / hw, r = m - b * hw, h = r / p.Win, w = r - h * p.Win;
+        const size_t W2 = (size_t)p.Win * 2;
+        const size_t o00 = (((size_t)b * 2 * p.Hin + 2 * h) * W2 + 2 * w) * K + q * 8;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        a[d][i][s] = *reinterpret_cast<const s8v*>(p.x + off + s * 32);
-        if constexpr (BWD) ya[d][i][s] = *reinterpret_cast<const uint4*>(p.bwd.y + off + s * 32);
+        for (int s = 0; s < KS; ++s) {
+          a[d][i][s] = *reinterpret_cast<const s8v*>(p.sum2x2 + o00 + s * 32);
+          qa[d][i][s][0] = *reinterpret_cast<const uint4*>(p.sum2x2 + o00 + K + s * 32);
+          qa[d][i][s][1] = *reinterpret_cast<const uint4*>(p.sum2x2 + o00 + W2 * K + s * 32);
+          qa[d][i][s][2] = *reinterpret_cast<const uint4*>(p.sum2x2 + o00 + (W2 + 1) * K + s * 32);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          a[d][i][s] = *reinterpret_cast<const s8v*>(p.x + off + s * 32);
+          if constexpr (BWD) ya[d][i][s] = *reinterpret_cast<const uint4*>(p.bwd.y + off + s * 32);
+        }
       }
     }
   };
@@ -104,6 +123,26 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
       int wo = 0;
       asm volatile("" : "+v"(wo));
       const bf16_t* sWt = sW + wo;
+      if constexpr (S2) {
+        const bool side = slice == 0;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int m = tt * WR + i * 16 + r16;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            float u0[8], u1[8], u2[8], u3[8], o[8];
+            unpack8(*reinterpret_cast<const uint4*>(&a[d][i][s]), u0);
+            unpack8(qa[d][i][s][0], u1);
+            unpack8(qa[d][i][s][1], u2);
+            unpack8(qa[d][i][s][2], u3);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = 0.f + ((u0[j] + u1[j]) + (u2[j] + u3[j]));
+            const uint4 v = pack8(o);
+            a[d][i][s] = *reinterpret_cast<const s8v*>(&v);
+            if (side && m < p.M) *reinterpret_cast<uint4*>(const_cast<bf16_t*>(p.x) + (size_t)m * K + s * 32 + q * 8) = v;
+          }
+        }
+      }
       if constexpr (BWD) {
         // dx = BN-backward apply of (g, y); slice-0 blocks store it (rows past M are clamped copies: not stored)
         const bool side = slice == 0 && p.bwd.dx != nullptr;
@@ -209,7 +248,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
 template <int NB, int K, int D>
 void launch_d(const ConvParams& p, hipStream_t st) {
   const bool bwd = p.bwd.y != nullptr;
-  constexpr int WR = pw_rows<K>();
+  const int WR = p.sum2x2 ? pw_rows<K, true>() : pw_rows<K>();
   const int nslices = p.N / NB;
   const int tiles = (p.M + WR - 1) / WR;
   // persistent grid: each wave takes a multiple of D tiles (ideally exactly D: its whole share in flight at once),
@@ -223,6 +262,10 @@ void launch_d(const ConvParams& p, hipStream_t st) {
   const int waves = (tiles + tpw - 1) / tpw;
   const int bps = ((waves + 3) / 4 + 7) / 8 * 8;
   if constexpr (D == 1) {
+    if (p.sum2x2) {
+      hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+      return;
+    }
     if (bwd) {
       hipLaunchKernelGGL((pw_kernel<NB, K, 1, true>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
       return;
@@ -234,7 +277,7 @@ void launch_d(const ConvParams& p, hipStream_t st) {
 template <int NB, int K>
 void launch(const ConvParams& p, hipStream_t st) {
   int d = cfl_tune(TUNE_PW_DEPTH);
-  if (d <= 0 || p.bwd.y) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration; the
+  if (d <= 0 || p.bwd.y || p.sum2x2) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration; the
                                   // BN-backward form holds y as well and runs at depth 1 only (deeper rings spill)
   if constexpr (K == 32) {                                // deeper rings spill at K >= 64
     if (d >= 4) return launch_d<NB, K, 4>(p, st);
@@ -250,7 +293,8 @@ bool pw_conv_supported(const ConvParams& p) {
          p.pad_t == 0 && p.pad_l == 0 && !p.up_in && p.Ho == p.Hin && p.Wo == p.Win && p.K == p.Cin &&
          (p.Cin == 32 || p.Cin == 64 || p.Cin == 128 || p.Cin == 256) && (p.N == 32 || p.N % 64 == 0) &&
          p.xf.ab == nullptr && !p.xf.relu && p.node.y == nullptr && p.join.mode == JOIN_NONE &&
-         (p.bwd.y == nullptr || (p.bwd.dx != nullptr && p.bwd.reps <= BNB_MAX_REPS)) && p.pj.v == nullptr &&
+         (p.bwd.y == nullptr || (p.bwd.dx != nullptr && p.bwd.reps <= BNB_MAX_REPS)) &&
+         (p.sum2x2 == nullptr || (p.bwd.y == nullptr && p.bias == nullptr && p.stats == nullptr)) && p.pj.v == nullptr &&
          p.xfin.stats == nullptr && p.fin.gamma == nullptr && p.M > 0;
 }
 

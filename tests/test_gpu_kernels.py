@@ -1027,6 +1027,38 @@ def test_entry_wgrad_bwd_fold_matches_unfolded(S, B, algo):
         assert torch.equal(f[3], u[3])
 
 
+@pytest.mark.parametrize("B,H,K,N,pw_off", [(2, 16, 32, 64, False), (2, 8, 64, 128, False), (2, 8, 128, 256, False),
+                                            (3, 5, 64, 64, False), (2, 8, 64, 128, True)])
+def test_conv_sum2x2_input_matches_node_bwd(B, H, K, N, pw_off):
+    """Decoder residual-conv data gradient with the 2x2-block sum formed on load (conv_igemm sum2x2=...; the
+    streaming 1x1 kernel, or node_bwd + conv on the generic path): output and the stored sums equal node_bwd(SUM2X2)
+    + the plain conv bit for bit."""
+    C_ = hip()
+    torch.manual_seed(43)
+    gb, g32 = bf(torch.randn(B, 2 * H, 2 * H, K))
+    wt, _ = bf(torch.randn(N, K) * 0.1)
+    if pw_off:
+        C_.set_tune(C_.TUNE_PW, 1)
+    try:
+        outs = []
+        for fold in (True, False):
+            dq = torch.full((B, H, H, K), 0x7fc0, dtype=torch.int16, device=DEV)   # NaN fill: every pixel written
+            y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            if fold:
+                C_.conv_igemm(dq, wt, None, y, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0, None, sum2x2=gb)
+            else:
+                C_.node_bwd(gb, 3, 0, None, 0, 0, None, dq, None, 0, dq, None, B, H, H, K)
+                C_.conv_igemm(dq, wt, None, y, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0, None)
+            torch.cuda.synchronize()
+            outs.append((dq.cpu(), y.cpu()))
+    finally:
+        C_.set_tune(C_.TUNE_PW, 0)
+    assert torch.equal(outs[0][0], outs[1][0]), int((outs[0][0] != outs[1][0]).sum())
+    assert torch.equal(outs[0][1], outs[1][1]), int((outs[0][1] != outs[1][1]).sum())
+    ref = g32.view(B, H, 2, H, 2, K).sum((2, 4))
+    assert rel(from_bits(outs[0][0]), ref) < 5e-3
+
+
 @pytest.mark.parametrize("dice", [0, 1])
 def test_head_loss_metrics_and_gradients_match_autograd(dice):
     """head.hip (4 lanes per low-resolution pixel: 8 channels and one sub-pixel of the 2x2 target block each):
@@ -1368,7 +1400,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_SUM2X2_FOLD", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
