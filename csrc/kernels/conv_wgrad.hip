@@ -208,10 +208,11 @@ void wgrad_shape(const WgradParams& p, int bko, int bno, int rm, int& chunk, int
   const int tiles = (p.K / bko) * (p.N / bno);
   chunk = p.m_chunk;
   if (chunk <= 0) {
-    // 256 blocks per layer: the deferred wgrads of a step are launched grouped (launch_group), so a layer's grid
-    // need not fill the chip alone - fewer, longer blocks halve the replica-row atomics (whole-step A/B: 1.691 ->
-    // 1.676 ms/iteration vs 512, profiles/README.md)
-    const int target = cfl_tune(TUNE_WGRAD1_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD1_BLOCKS) : 256;
+    // 320 blocks per layer: the deferred wgrads of a step are launched grouped (launch_group), so a layer's grid
+    // need not fill the chip alone - fewer, longer blocks than 512 halve the replica-row atomics (whole-step A/B:
+    // 1.691 -> 1.676 ms/iteration vs 512, profiles/README.md); re-swept after the round-2 folds: 256 / 320 / 384 /
+    // 448 -> 1.4255-1.4340 / 1.4176-1.4187 / 1.4197-1.4201 / 1.4324-1.4345 ms
+    const int target = cfl_tune(TUNE_WGRAD1_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD1_BLOCKS) : 320;
     const int minpix = cfl_tune(TUNE_WGRAD1_MINPIX) > 0 ? cfl_tune(TUNE_WGRAD1_MINPIX) : 512;
     int splits = (target + tiles - 1) / tiles;
     const int max_splits = (p.M + minpix - 1) / minpix;   // keep >= minpix pixels per block (512: 4 RM=128 stages)

@@ -404,7 +404,7 @@ enum TuneKey {
   TUNE_CONV3_WS_GRID = 15,     // weight-stationary conv3x3: persistent grid size (default 512)
   TUNE_WGRAD_GROUP = 16,       // conv_wgrad_batch: 1 = launch every wgrad on its own, 2 = group the 3x3 ones only
   TUNE_CONV3_DEEP = 17,        // conv3x3 Cin >= 128: 0 = LDS-DMA 3-stage deep-K kernel, 1 = off, 2 = force (any Cin)
-  TUNE_WGRAD1_BLOCKS = 18,     // generic (1x1) wgrad: target blocks per layer (default 256)
+  TUNE_WGRAD1_BLOCKS = 18,     // generic (1x1) wgrad: target blocks per layer (default 320)
   TUNE_WGRAD1_MINPIX = 19,     // generic (1x1) wgrad: min pixels per block (default 512)
   TUNE_NODE_BWD_IPT = 20,      // node_bwd: items in flight per thread (2 or 4; default 2)
   TUNE_DW_BWD_BLOCKS = 21,     // fused depthwise backward: target grid size (default 512)
