@@ -133,8 +133,9 @@ struct ConvParams {
                          // for the weight gradient; other kernels run node_bwd into x first (same results)
 };
 int conv_igemm(const ConvParams& p, hipStream_t st);
-// plain 1x1 / stride-1 convs (no input transform, epilogue = bias + optional BN statistics): streaming MFMA kernel
-// with swapped operands and resident weights (pw.hip); conv_igemm routes them there unless TUNE_PW = 1
+// plain 1x1 / stride-1 convs (no input transform, epilogue = bias + optional BN statistics; input optionally formed
+// on load: bwd = BN-backward apply, sum2x2 = 2x2-block sums): streaming MFMA kernel with swapped operands and resident
+// weights (pw.hip); conv_igemm routes them there unless TUNE_PW = 1
 bool pw_conv_supported(const ConvParams& p);
 int pw_conv(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)

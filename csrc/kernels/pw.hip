@@ -17,6 +17,11 @@
 // Each wave is its own pipeline: a persistent loop over WR-pixel tiles whose next tile's loads are issued right after
 // the current tile's MFMAs, so they are in flight during its epilogue. Statistics (from the rounded bf16 outputs, as
 // in conv_igemm) stay in registers across the tiles: one atomic per (channel, statistic) per block at the end.
+//
+// Because the input goes straight from global memory into the MFMA registers, producer passes of a data gradient
+// fold into this load (the kernel also stores the formed input for the weight gradient that reads it later):
+//   BWD - the BN-backward apply of (g, y) (common.h BnBwdIn; the encoder pointwise dgrads), and
+//   S2  - the 2x2-block sum of a full-resolution gradient (the decoder residual conv's upsample gradient).
 #include "common.h"
 #include "launch.h"
 
