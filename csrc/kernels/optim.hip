@@ -176,8 +176,10 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
 }
 
 __global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs) {
-  if (bs.table != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < bs.B)
-    bs.idx[threadIdx.x] = bs.table[(size_t)(*bs.cursor % bs.nb) * bs.B + threadIdx.x];
+  if (bs.table != nullptr && blockIdx.x == 0 && blockIdx.y == 0) {   // any batch size (the 512^2 plan: ~1,100)
+    const size_t row = (size_t)(*bs.cursor % bs.nb) * bs.B;
+    for (int i = threadIdx.x; i < bs.B; i += NT) bs.idx[i] = bs.table[row + i];
+  }
   const ZeroSpan z = spans[blockIdx.y];
   uint4* p = reinterpret_cast<uint4*>(z.p);
   const int64_t n = z.bytes >> 4;
@@ -214,7 +216,7 @@ int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipS
 
 int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st, BatchSelect batch) {
   if (n_spans <= 0) return 0;
-  if (batch.table != nullptr && (batch.B < 1 || batch.B > NT || batch.nb < 1)) return 1;
+  if (batch.table != nullptr && (batch.B < 1 || batch.nb < 1)) return 1;
   int64_t bx = (max_bytes / 16 + NT - 1) / NT;
   if (bx > 1024) bx = 1024;
   if (bx < 1) bx = 1;

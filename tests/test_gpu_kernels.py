@@ -1630,6 +1630,23 @@ def test_conv3x3_consumer_finalize_matches_bn_finalize(B, Hs, Cin, N, tune):
             C_.set_tune(keys[tune][0], 0)
 
 
+@pytest.mark.parametrize("B", [16, 256, 1096])
+def test_zero_spans_batch_select_any_batch_size(B):
+    """The step's zero_spans launch selects row cursor % nb of the device batch table for any batch size (the
+    512^2 HBM plan runs ~1,100 images per step: more indices than one block's threads) and zeroes its spans."""
+    C_ = hip()
+    nb = 3
+    tab = torch.randint(0, 10000, (nb, B), dtype=torch.int32, device=DEV)
+    cursor = torch.tensor([4], dtype=torch.int32, device=DEV)
+    idx = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+    buf = torch.ones(4096, device=DEV)
+    zt = C_.make_zero_table([buf])
+    C_.zero_spans(zt, 1, buf.numel() * 4, tab, cursor, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(idx.cpu(), tab[4 % nb].cpu())
+    assert float(buf.abs().sum()) == 0.0
+
+
 def test_engine_device_batch_table_selects_and_advances():
     """UNetEngine.bind_batches: each training step (eager or graph-replayed) takes its dataset indices from row
     cursor % nb of the bound table - selected by the step's zero_spans launch, the cursor advanced by its pack launch
