@@ -20,6 +20,11 @@ import os
 import sys
 import time
 
+# multi-rank GPU work (RCCL, CUDA-tensor sharing between processes): the host driver only supports dmabuf IPC, so
+# the legacy IPC mode must be off - HSA reads this once, at its initialisation, so it is set before this process
+# makes any GPU call (with legacy IPC RCCL fails with "hipIpcGetMemHandle: invalid argument")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -251,8 +256,9 @@ def main() -> int:
                           "img_size": args.img, "global_batch": args.batch * world, "per_client_batch": args.batch,
                           "seq_len": None, "epochs_per_round": args.epochs,
                           "local_steps_per_round": args.epochs * args.local_steps,
-                          "parallelism": f"fedavg-dp{world} (1 FL client per GPU, weighted all-reduce over "
-                                         f"{'RCCL' if world == 1 or dist.get_backend() == 'nccl' else dist.get_backend()})",
+                          "parallelism": (f"fedavg-dp{world} (1 FL client per GPU, weighted all-reduce over "
+                                          f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})")
+                          if agg is not None else "fedavg-dp1 (no aggregation at N=1: weight repack only)",
                           "graph": use_graph, "memplan": plan.as_dict() if plan else None}}
         print(json.dumps(out), flush=True)
     if args.fl:

@@ -50,6 +50,8 @@ class FLConfig:
     data_plane: str = "grpc"             # grpc | rccl
     rccl_timeout_s: float = 300.0        # collective timeout; on expiry / peer loss the client aborts the
                                          # communicator and falls back to the gRPC data plane
+    dist_backend: str = "nccl"           # rccl data plane backend: nccl (= RCCL over xGMI) | gloo (CPU clients, or
+                                         # a rehearsal of N clients sharing one GPU, which RCCL refuses)
     codec: str = "flat"                  # client upload / advertised reply format: flat (safe) | pickle (reference
                                          # wire format). The server answers each client in the format it
                                          # advertised, pickle for a reference client that advertises none
@@ -88,6 +90,8 @@ class FLConfig:
     # --- persistence / observability -------------------------------------------------------------
     work_dir: str = "."
     client_weight_file: str = "./saved_weight/weights.pickle"
+    final_weight_file: str = ""          # where a client writes the model it holds at FIN (rccl data plane: the
+                                         # final global average; "" = not written)
     server_weight_file: str = "./server_weights/weights.pickle"
     log_dir: str = "send_logs/logs"
     metrics_file: str = ""               # JSONL metrics sink ("" = stdout only)

@@ -16,7 +16,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import os
 import random
-from typing import List, Optional, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -57,23 +57,32 @@ def decode(path: str, mode: str) -> np.ndarray:
         return np.ascontiguousarray(np.asarray(im.convert(mode), dtype=np.uint8))
 
 
-def resize_on_device(arrays: List[np.ndarray], size: int, binarize: bool, chunk: int = 1024):
-    """Decoded uint8 images of any sizes -> torch uint8 [n, size, size(, c)] on the current GPU, resized by the HIP
-    batch kernel (cv2.resize INTER_LINEAR grid, as the host ``_native.resize_bilinear``)."""
+def resize_on_device(items: Sequence, size: int, binarize: bool, chunk: int = 1024,
+                     load: Optional[Callable[[str], np.ndarray]] = None, pool=None, channels: Optional[int] = None):
+    """uint8 images of any sizes -> torch uint8 [n, size, size(, c)] on the current GPU, resized by the HIP batch
+    kernel (cv2.resize INTER_LINEAR grid, as the host ``_native.resize_bilinear``). ``items`` are decoded arrays,
+    or paths that ``load`` decodes one ``chunk`` at a time (on ``pool`` if given), so host memory holds at most one
+    chunk of source-resolution images. ``channels`` (3, or None for single-channel) shapes an empty result."""
     import torch
     from .._native_loader import hip
     C = hip()
-    c = arrays[0].shape[2] if arrays[0].ndim == 3 else 1
-    shape = (len(arrays), size, size) + ((c,) if arrays[0].ndim == 3 else ())
-    out = torch.empty(shape, dtype=torch.uint8, device="cuda")
-    for s0 in range(0, len(arrays), chunk):
-        part = arrays[s0:s0 + chunk]
+    n = len(items)
+    out = None
+    for s0 in range(0, n, chunk):
+        part = items[s0:s0 + chunk]
+        if load is not None:
+            part = list(pool.map(load, part)) if pool is not None else [load(p) for p in part]
+        if out is None:
+            c = part[0].shape[2] if part[0].ndim == 3 else None
+            out = torch.empty((n, size, size) + ((c,) if c else ()), dtype=torch.uint8, device="cuda")
         sizes = np.array([a.size for a in part], np.int64)
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
         dims = np.array([a.shape[:2] for a in part], np.int32).reshape(-1)
         src = torch.from_numpy(np.concatenate([a.reshape(-1) for a in part])).to("cuda", non_blocking=False)
         C.resize_batch(src, torch.from_numpy(offs).cuda(), torch.from_numpy(dims).cuda(), out[s0:s0 + len(part)],
                        1 if binarize else 0)
+    if out is None:                                       # empty folder / limit 0
+        out = torch.empty((0, size, size) + ((channels,) if channels else ()), dtype=torch.uint8, device="cuda")
     return out
 
 
@@ -88,9 +97,9 @@ def load_folder_dataset(image_dir: str, mask_dir: str, img: int, split: int = 62
         imgs, masks = imgs[:limit], masks[:limit]
     n = len(imgs)
     if device == "cuda":                      # decode on the host, resize + binarise on the GPU
-        with cf.ThreadPoolExecutor(max_workers=workers) as ex:
-            X = resize_on_device(list(ex.map(lambda p: decode(p, "RGB"), imgs)), img, False)
-            Y = resize_on_device(list(ex.map(lambda p: decode(p, "L"), masks)), img, True)
+        with cf.ThreadPoolExecutor(max_workers=workers) as ex:   # decode chunk by chunk (bounded host memory)
+            X = resize_on_device(imgs, img, False, load=lambda p: decode(p, "RGB"), pool=ex, channels=3)
+            Y = resize_on_device(masks, img, True, load=lambda p: decode(p, "L"), pool=ex)
         split = min(split, n)
         idx = np.arange(n)
         return CrackDataset(X, Y, idx[:split], idx[split:])

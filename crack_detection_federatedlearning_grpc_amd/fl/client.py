@@ -105,9 +105,12 @@ class FLClient:
     def _training(self, stub) -> None:
         self._call(stub, P.transportRequest(update_req=P.UpdateReq(type="T", cname=self.name, state=P.TRAINING)))
 
-    def _train_done(self, stub, cr: int, payload: bytes, n: int):
+    def _train_done(self, stub, cr: int, payload: bytes, n: int, plane: str = ""):
+        """``plane`` = "rccl" (in ``title``): this client's local model already IS the round's average (the
+        collective succeeded), so the server sends it no parameters back (a reference client sends no title)."""
         req = P.transportRequest(update_req=P.UpdateReq(type="D", buffer_chunk=payload, state=P.TRAIN_DONE,
-                                                        cname=self.name, current_round=cr, file_len=int(n)))
+                                                        cname=self.name, current_round=cr, file_len=int(n),
+                                                        title=plane))
         return self._call(stub, req).update_rep
 
     def _version(self, stub, mv: int, cr: int, wait_s: float):
@@ -152,9 +155,14 @@ class FLClient:
         if self.cfg.client_weight_file:   # trainer -> driver hand-off file (client_fit_model.py:238-240)
             codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
 
-    def _payload(self) -> bytes:
+    def _payload(self) -> tuple:
+        """(TRAIN_DONE payload, data plane). RCCL mode: the weighted all-reduce runs here (in place on the GPU, or
+        over host arrays); rank 0 alone uploads the average for the server's copy, the other ranks send nothing.
+        A failed collective leaves the local model unchanged (fedavg_device rolls back) and the client continues
+        on the gRPC data plane."""
         n = getattr(self.trainer, "n_samples", 0)
         arrays = None
+        plane = ""
         if self.aggregator is not None:
             try:
                 dev = getattr(self.trainer, "fedavg_device", None)
@@ -171,13 +179,14 @@ class FLClient:
                 self.fallbacks += 1
                 arrays = None
             else:
+                plane = "rccl"
                 if self.aggregator.rank != 0:
-                    return b""                                   # rank 0 alone uploads the server's copy
+                    return b"", plane                            # rank 0 alone uploads the server's copy
         if self.cfg.fault_corrupt:
-            return b"\x80corrupt" + os.urandom(64)
+            return b"\x80corrupt" + os.urandom(64), plane
         if arrays is None:
-            arrays = self.trainer.get_weights()                  # (rank 0: the D2H waits for the last bucket)
-        return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype)
+            arrays = self.trainer.get_weights()
+        return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype), plane
 
     def _apply(self, blob: bytes) -> None:
         if self.aggregator is not None or not blob:
@@ -211,13 +220,13 @@ class FLClient:
                     time.sleep(self.cfg.fault_delay_s)
                 t0 = time.perf_counter()
                 with trace_phase("fl/aggregate"):
-                    payload = self._payload()             # RCCL mode: the all-reduce runs here
+                    payload, plane = self._payload()      # RCCL mode: the all-reduce runs here
                 t1 = time.perf_counter()
                 with trace_phase("fl/upload"):
-                    rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0))
+                    rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0), plane)
                 t2 = time.perf_counter()
                 phase = {"round": cr, "aggregate_s": t1 - t0, "upload_s": t2 - t1, "wait_s": 0.0,
-                         "payload_bytes": len(payload)}
+                         "payload_bytes": len(payload), "data_plane": plane or "grpc"}
                 st = rep.config["state"].scstring
                 print(f"### Received from state {st} ###")
                 if st == "RESP_ACY":
@@ -225,6 +234,7 @@ class FLClient:
                         vr = self._version(stub, mv, cr, self.cfg.long_poll_s)
                         if vr.state == P.NOT_WAIT:
                             phase["wait_s"] = time.perf_counter() - t2
+                            phase["reply_bytes"] = len(vr.buffer_chunk)
                             self._log_phase(phase)
                             cr = vr.config["current_round"].scint32
                             mv = vr.config["model_version"].scint32
@@ -244,6 +254,7 @@ class FLClient:
                     if self.final_state == "FIN":
                         break
                 elif st == "RESP_ARY":
+                    phase["reply_bytes"] = len(rep.buffer_chunk)
                     self._log_phase(phase)
                     self._training(stub)
                     cr = rep.config["current_round"].scint32
@@ -260,6 +271,8 @@ class FLClient:
                     print(f"[{self.name}] unexpected state {st!r}; exiting")
                     self.final_state = st
                     break
+            if self.cfg.final_weight_file:
+                codec.save_weight_file(self.cfg.final_weight_file, self.trainer.get_weights())
             if self.cfg.upload_logs:
                 self.send_logs(stub)
             print("all training finish")

@@ -31,6 +31,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     port = srv.start()
     print(f"[launch] server on :{port}, starting {n} client process(es) (data plane {cfg.data_plane})", flush=True)
     env = dict(os.environ)
+    # the client processes share GPU memory over RCCL: the host driver only supports dmabuf IPC, and HSA reads
+    # this at its initialisation, so each child gets it in its environment from the start (fl_client.py also
+    # sets it before its first GPU call)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     procs = []

@@ -9,7 +9,10 @@ Reference: fl_server.py. Same single bidi-stream RPC and verbs (dispatcher fl_se
   version_req.type 'P'         -> WAIT / NOT_WAIT(+params) / FIN                     :197-207
 Extra READY reply keys (ignored by reference clients): ``rank``, ``world_size``, ``dist_addr``, ``dist_port``,
 ``data_plane`` - the server doubles as the RCCL rendezvous for on-node GPU clients.
-``UpdateReq.file_len`` on a 'D' request carries the client's sample count n_k for weighted FedAvg.
+``UpdateReq.file_len`` on a 'D' request carries the client's sample count n_k for weighted FedAvg, and
+``UpdateReq.title`` = "rccl" says the client's local model already holds the round's average (the RCCL data plane
+reduced it on the GPUs): its RESP_ARY / NOT_WAIT replies then carry no parameters (8.2 MB per client per round the
+client would discard).
 
 Reply codec per client (drop-in compatibility): a reference client ``pickle.loads`` whatever arrives in
 ``buffer_chunk`` (client_fit_model.py:51,231) and never says what it can read, so parameters go out as the
@@ -76,6 +79,8 @@ class FLServer(TransportServiceServicer):
         self._blob_lock = threading.Lock()
         self._blob_cache: Dict[tuple, bytes] = {}
         self._codec: Dict[str, tuple] = {}          # client name -> (codec, wire_dtype) it can decode
+        self._rccl_round: Dict[str, int] = {}       # client -> round whose average it holds already (RCCL plane)
+        self._eval_pool: Optional[futures.ThreadPoolExecutor] = None
         self.server: Optional[grpc.Server] = None
         self.port: Optional[int] = None
         self.dist_port = 0
@@ -129,10 +134,28 @@ class FLServer(TransportServiceServicer):
             save_snapshot(self.cfg.snapshot_dir, self.table, st.global_flat, st.current_round, st.model_version,
                           st.finished)
         if self.evaluator is not None:   # fl_server.py:27-37 (dead code in the reference)
-            res = self.evaluator(st.global_flat)
-            print(f"[fl_server] Evaluate Loss : {res.get('loss')} Evaluate Accuracy : {res.get('accuracy')}")
+            # off the RoundState lock (this hook runs under it): READY / VERSION / heartbeat RPCs keep flowing
+            # while the global model is evaluated on a worker thread
+            if self._eval_pool is None:
+                self._eval_pool = futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fl-eval")
+            self._eval_pool.submit(self._evaluate, rec.round, st.global_flat.copy())
         if st.finished:
             self.done.set()
+
+    def _evaluate(self, rnd: int, flat: np.ndarray) -> None:
+        try:
+            res = self.evaluator(flat)
+            print(f"[fl_server] round {rnd} Evaluate Loss : {res.get('loss')} "
+                  f"Evaluate Accuracy : {res.get('accuracy')}")
+        except Exception as e:
+            print(f"[fl_server] evaluation of round {rnd} failed: {e!r}")
+
+    def _params_for(self, name: str, new_round: int, fmt: tuple) -> bytes:
+        """The new global for a client, or nothing for an RCCL client that holds it already (it reported the
+        round just aggregated with title "rccl")."""
+        if self._rccl_round.get(name) == new_round - 1:
+            return b""
+        return self.send_parameter(fmt)
 
     # -- RPC ---------------------------------------------------------------------------------------
     def transport(self, request_iterator, context):
@@ -187,13 +210,18 @@ class FLServer(TransportServiceServicer):
             except Exception as e:
                 print(f"[fl_server] rejected payload from {u.cname}: {e}")
                 context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"bad weight payload: {e}")
+        if u.title == "rccl":
+            self._rccl_round[u.cname] = u.current_round
+        else:
+            self._rccl_round.pop(u.cname, None)
         try:
             state, conf = self.state.submit(u.cname, u.current_round, flat, max(n, 0.0))
         except ValueError as e:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         conf = dict(conf, state=state)
         print(f"### Current state: {state} ###")
-        chunk = self.send_parameter(self.client_format(u.cname)) if state == RESP_ARY else b""
+        chunk = self._params_for(u.cname, conf["current_round"], self.client_format(u.cname)) \
+            if state == RESP_ARY else b""
         return P.transportResponse(update_rep=P.UpdateRep(type="D", buffer_chunk=chunk, config=_cfg(conf)))
 
     def _version(self, v):
@@ -202,8 +230,9 @@ class FLServer(TransportServiceServicer):
         wait = v.config["wait_s"].scfloat if "wait_s" in v.config else 0.0
         state, conf = self.state.version(mv, cr, min(wait, self.cfg.long_poll_s))
         if state == NOT_WAIT:
-            fmt = self.client_format(v.config["cname"].scstring if "cname" in v.config else "", v.config)
-            return P.transportResponse(version_rep=P.VersionRep(state=P.NOT_WAIT, buffer_chunk=self.send_parameter(fmt),
+            name = v.config["cname"].scstring if "cname" in v.config else ""
+            chunk = self._params_for(name, conf["current_round"], self.client_format(name, v.config))
+            return P.transportResponse(version_rep=P.VersionRep(state=P.NOT_WAIT, buffer_chunk=chunk,
                                                                 config=_cfg(conf)))
         if state == FIN:
             return P.transportResponse(version_rep=P.VersionRep(state=P.FIN, config=_cfg(conf)))
@@ -236,6 +265,8 @@ class FLServer(TransportServiceServicer):
         self.state.stop()
         if self.server is not None:
             self.server.stop(grace)
+        if self._eval_pool is not None:
+            self._eval_pool.shutdown(wait=True)
 
     def serve_forever(self, exit_on_fin: bool = True) -> None:
         try:

@@ -740,17 +740,28 @@ class UNetEngine:
     def bind_batches(self, batches: torch.Tensor) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
         ``cursor % nb`` (selected in the step's zero_spans launch, the cursor advanced by its pack launch) instead of
-        a host copy into ``idx``. Rebinding a table of at most the bound row count copies into the bound buffer
-        (graph-safe; steps from cursor 0 then use its first rows)."""
+        a host copy into ``idx``. After graph capture the table buffer is fixed (the graph holds its address and
+        row count): a table of the same row count is copied in; a smaller one whose row count divides the bound
+        one is tiled into it, so ``cursor % nb`` still wraps onto the NEW rows; anything else is refused.
+        Every index is checked against the bound dataset (the kernels read images / masks through them)."""
         batches = batches.to(device=self.dev, dtype=torch.int32).contiguous()
         if batches.dim() != 2 or batches.shape[1] != self.B:
             raise ValueError(f"bind_batches: expected [nb, {self.B}], got {tuple(batches.shape)}")
-        if self.batch_table is not None and batches.shape[0] <= self.batch_table.shape[0]:
-            self.batch_table[:batches.shape[0]].copy_(batches)
+        if self.images is not None and batches.numel():
+            lo, hi = int(batches.min()), int(batches.max())
+            if lo < 0 or hi >= self.n_data:
+                raise ValueError(f"bind_batches: indices [{lo}, {hi}] outside the bound dataset of {self.n_data}")
+        nb = batches.shape[0]
+        if self.batch_table is not None and nb == self.batch_table.shape[0]:
+            self.batch_table.copy_(batches)
             return
-        if self.graph is not None:
-            raise RuntimeError("bind_batches: a larger table after graph capture")
-        self.batch_table = batches.clone()
+        if self.graph is None:
+            self.batch_table = batches.clone()
+            return
+        bound = self.batch_table.shape[0]
+        if nb > bound or bound % nb:
+            raise RuntimeError(f"bind_batches: {nb} rows after graph capture of a {bound}-row table (must divide it)")
+        self.batch_table.copy_(batches.repeat(bound // nb, 1))
 
     def set_batch_cursor(self, i: int = 0) -> None:
         self.batch_cursor.fill_(i)

@@ -18,7 +18,7 @@ On CPU-only hosts the same code runs over gloo (tests).
 """
 from __future__ import annotations
 
-import os
+import time
 from datetime import timedelta
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -101,23 +101,34 @@ class FedAvgAllReduce:
 
 
 class RcclAggregator:
-    """FL-client data plane: weighted all-reduce between the registered clients."""
+    """FL-client data plane: weighted all-reduce between the registered clients.
+
+    ``backend``: "nccl" (RCCL over xGMI, the product path) or "gloo" (CPU clients, and the one-GPU rehearsal of
+    N clients sharing a card, which RCCL refuses). Collectives stay asynchronous to the host - no
+    ``TORCH_NCCL_BLOCKING_WAIT``, which would serialise the bucketed all-reduce bucket by bucket on the host: the
+    side stream waits on each bucket's collective, and a dead peer is detected by ``wait_complete``'s host-side
+    deadline (``timeout_s``), which fires before the process group's own timeout so this process aborts the
+    communicator first and the client can fall back to gRPC."""
 
     def __init__(self, rank: int, world: int, addr: str, port: int, device: Optional[torch.device] = None,
-                 timeout_s: float = 300.0):
+                 timeout_s: float = 300.0, backend: Optional[str] = None):
         self.rank, self.world = rank, world
         cuda = device is not None and device.type == "cuda"
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        # blocking waits: a collective that cannot complete (dead peer) raises on the host after ``timeout_s``
-        # instead of the watchdog tearing the process down, so the client can fall back to gRPC (fl/client.py)
-        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        backend = backend or ("nccl" if cuda else "gloo")
+        if backend == "nccl" and not cuda:
+            backend = "gloo"                                   # CPU clients: RCCL needs a GPU
+        self.timeout_s = float(timeout_s)
         if not dist.is_initialized():
-            dist.init_process_group("nccl" if cuda else "gloo", init_method=f"tcp://{addr}:{port}", rank=rank,
-                                    world_size=world, timeout=timedelta(seconds=timeout_s),
-                                    **({"device_id": device} if cuda else {}))
+            # gloo raises on its own timeout (the host waits in work.wait()); under RCCL the group timeout only
+            # arms the watchdog, so it is set past the host-side deadline of wait_complete
+            pg_timeout = self.timeout_s if backend == "gloo" else self.timeout_s + 60.0
+            dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world,
+                                    timeout=timedelta(seconds=pg_timeout),
+                                    **({"device_id": device} if backend == "nccl" else {}))
         self.device = device if cuda else torch.device("cpu")
         self._cached = None
-        print(f"[rccl] rank {rank}/{world} backend {dist.get_backend()} device "
+        self._backup: Optional[torch.Tensor] = None
+        print(f"[rccl] rank {rank}/{world} world_size {world} backend {dist.get_backend()} device "
               f"{self.device if not cuda else torch.cuda.get_device_name(device)} ({self.device})", flush=True)
 
     @classmethod
@@ -126,7 +137,8 @@ class RcclAggregator:
         if torch.cuda.is_available() and (cfg is None or cfg.device != "cpu"):
             dev = torch.device("cuda", torch.cuda.current_device())
         return cls(int(info.get("rank", 0)), int(info["world_size"]), str(info.get("dist_addr") or "127.0.0.1"),
-                   int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)))
+                   int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)),
+                   backend=getattr(cfg, "dist_backend", None) or None)
 
     def _reducer(self, flat: torch.Tensor) -> FedAvgAllReduce:
         key = (flat.data_ptr(), flat.numel())
@@ -152,6 +164,38 @@ class RcclAggregator:
         """Device-resident FedAvg of a trainer's flat fp32 parameter buffer, in place: bucketed weighted
         all-reduce on a side stream (no host staging); returns the per-bucket events for ``defer_until``."""
         return self._reducer(flat).average_async(float(max(n_local, 1)), on_bucket=on_bucket)
+
+    def wait_complete(self, events: Sequence[Tuple[slice, object]]) -> None:
+        """Host-side completion check with a deadline: poll the last bucket's event (recorded after every earlier
+        bucket on the same side stream) without blocking inside the runtime, so a collective that can never
+        finish (dead peer) raises ``TimeoutError`` here instead of hanging the client."""
+        if not events:
+            return
+        ev = events[-1][1]
+        end = time.monotonic() + self.timeout_s
+        while not ev.query():
+            if time.monotonic() > end:
+                raise TimeoutError(f"FedAvg all-reduce not complete after {self.timeout_s:.0f} s (peer lost?)")
+            time.sleep(5e-5)
+
+    def fedavg_device(self, flat: torch.Tensor, n_local: float,
+                      on_bucket: Optional[Callable[[slice], None]] = None) -> List[Tuple[slice, object]]:
+        """``average_device`` + ``wait_complete`` with rollback: the buckets are pre-scaled (w_k * n_k / sum n) and
+        reduced in place, so a failure part-way would leave ``flat`` a mix of scaled, reduced and untouched
+        buckets. The buffer is copied first (8 MB device copy); on any failure the communicator is aborted (no
+        collective still writes ``flat``), the local model restored and the error re-raised - the caller then
+        uploads its unchanged local weights over gRPC."""
+        if self._backup is None or self._backup.numel() != flat.numel() or self._backup.device != flat.device:
+            self._backup = torch.empty_like(flat)
+        self._backup.copy_(flat)
+        try:
+            evs = self.average_device(flat, n_local, on_bucket=on_bucket)
+            self.wait_complete(evs)
+            return evs
+        except BaseException:
+            self.abort()
+            flat.copy_(self._backup)
+            raise
 
     def abort(self) -> None:
         """A peer died or a collective timed out: tear the communicator down without a collective shutdown

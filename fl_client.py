@@ -12,6 +12,11 @@ import random
 import sys
 from typing import List, Optional
 
+# multi-rank GPU work (RCCL, CUDA-tensor sharing between processes): the host driver only supports dmabuf IPC, so
+# the legacy IPC mode must be off - HSA reads this once, at its initialisation, so it is set before this process
+# makes any GPU call (with legacy IPC RCCL fails with "hipIpcGetMemHandle: invalid argument")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 from crack_detection_federatedlearning_grpc_amd import config as _config
 from crack_detection_federatedlearning_grpc_amd.fl import codec
 from crack_detection_federatedlearning_grpc_amd.fl import proto as P

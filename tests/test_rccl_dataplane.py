@@ -105,3 +105,78 @@ def test_rccl_peer_loss_falls_back_to_grpc(tmp_path):
     assert np.isclose(srv.state.global_flat[e.offset], r3, atol=1e-5)
     # c2 left the live set at the round-2 deadline: round 3 closes without waiting for it again
     assert [h.dropped for h in srv.state.history] == [[], ["c2"], []]
+
+
+def _client_proc_flat(port, name, delta, n, fail_bucket, metrics, q):
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.client import FLClient
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+    from fakes import FakeFlatTrainer
+    cfg = FLConfig(device="cpu", data_plane="rccl", dist_backend="gloo", num_clients=2, register_window_s=20,
+                   ready_stall_s=0, poll_period_s=0.05, long_poll_s=1.0, max_rounds=2, client_weight_file="",
+                   rpc_timeout_s=60, rccl_timeout_s=20.0, metrics_file=metrics)
+    table = ParamTable()
+    tr = FakeFlatTrainer(table, delta, n_samples=n, fail_bucket=fail_bucket)
+    c = FLClient(cfg, lambda: tr, name=name, target=f"127.0.0.1:{port}",
+                 aggregator_factory=lambda info: RcclAggregator.from_ready_info(info, cfg))
+    st = c.run()
+    e = table.entries[0]
+    q.put((name, st, float(tr.flat[e.offset]), c.fallbacks, [float(u[e.offset]) for u in tr.uploads]))
+
+
+def _run_flat_pair(tmp_path, fail_bucket):
+    import json
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=2, register_window_s=20, ready_stall_s=0,
+                   max_rounds=2, work_dir=str(tmp_path), server_weight_file="", long_poll_s=1.0)
+    srv = FLServer(cfg, global_flat=np.zeros(table.total, np.float32), table=table)
+    port = srv.start(0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_client_proc_flat,
+                      args=(port, f"c{i}", d, n, fail_bucket, str(tmp_path / f"c{i}.jsonl"), q))
+          for i, (d, n) in enumerate([(1.0, 10), (5.0, 30)])]
+    for p in ps:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=120) for _ in ps)}
+    for p in ps:
+        p.join(30)
+    srv.stop()
+    phases = {i: [json.loads(x) for x in open(tmp_path / f"c{i}.jsonl") if '"phases"' in x] for i in range(2)}
+    return table, srv, res, phases
+
+
+def test_rccl_device_path_sends_no_parameters(tmp_path):
+    """The in-place (device-buffer) RCCL path end to end over gloo: the weighted average lands in every client's
+    buffer, rank 0 alone uploads it, rank 1's payload is empty, and the server's RESP_ARY / NOT_WAIT replies carry
+    no parameters to clients that hold the average already."""
+    table, srv, res, phases = _run_flat_pair(tmp_path, fail_bucket=-1)
+    assert all(r[0] == "FIN" and r[2] == 0 for r in res.values()), res
+    assert np.isclose(res["c0"][1], 8.0) and np.isclose(res["c1"][1], 8.0)       # (see the two-process test)
+    assert np.isclose(srv.state.global_flat[table.entries[0].offset], 8.0)
+    assert all(p["data_plane"] == "rccl" for ph in phases.values() for p in ph)
+    assert [p["payload_bytes"] for p in phases[1]] == [0, 0]                       # rank 1 uploads nothing
+    assert all(p["payload_bytes"] > 0 for p in phases[0])
+    # round 1's reply (RESP_ARY or NOT_WAIT) carried no parameters to either client
+    assert all(p.get("reply_bytes", 0) == 0 for ph in phases.values() for p in ph), phases
+
+
+def test_rccl_failure_mid_bucket_uploads_local_model(tmp_path):
+    """A collective lost after some buckets were scaled / reduced: the aggregator aborts the communicator and
+    restores the local model, so the gRPC fallback uploads exactly the locally trained weights (not a mix of
+    pre-scaled and reduced buckets) and the round is averaged over gRPC."""
+    table, srv, res, phases = _run_flat_pair(tmp_path, fail_bucket=2)
+    assert all(r[0] == "FIN" and r[2] == 1 for r in res.values()), res
+    # each client's uploads: round 1 = its local model (delta), round 2 = 4 + delta (the gRPC average + delta)
+    assert res["c0"][3] == [1.0, 5.0] and res["c1"][3] == [5.0, 9.0], res
+    assert np.isclose(srv.state.global_flat[table.entries[0].offset], 8.0)
+    assert all(p["data_plane"] == "grpc" for ph in phases.values() for p in ph)
+    assert all(p["payload_bytes"] > 0 for ph in phases.values() for p in ph)

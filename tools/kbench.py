@@ -75,7 +75,8 @@ def main():
                          "achieved GB/s / TF/s and the roofline floor max(bytes / 6.3 TB/s, flops / 2.5 PF/s)")
     args = ap.parse_args()
     table = ParamTable()
-    data = make_synthetic_device(64, args.img, seed=0)
+    # at least one image per batch slot: the step's batch indices (0..batch-1) address the resident dataset
+    data = make_synthetic_device(max(64, args.batch), args.img, seed=0)
     eng = UNetEngine(table, args.batch, args.img)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))
