@@ -229,7 +229,8 @@ class UNetEngine:
         dt = {2: torch.int16, 1: torch.uint8, 4: torch.float32}
         self.act = {n: t(*shp, dtype=dt[isz]) for n, (shp, isz) in shapes_a.items() if n != "h"}
         self.h = t(*shapes_a["h"][0], dtype=torch.float32)
-        self.dg = {n: (t(*v[0], dtype=dt[v[1]]) if v else None) for n, v in shapes_d.items()}
+        # inference-only engines (evaluator) never run backward: no gradient buffers (33.5 of 55 MB per 256^2 image)
+        self.dg = {n: (t(*v[0], dtype=dt[v[1]]) if v and self._share is None else None) for n, v in shapes_d.items()}
         # replica rows for the small weight gradients every block adds into (depthwise kernels, entry conv):
         # [R][n] slabs summed into the flat gradient by ONE grad_finish launch at the end of backward, which
         # also applies the gradient copies (residual-conv bias grad == its BN's beta grad)
@@ -297,6 +298,10 @@ class UNetEngine:
         # BN finalize done by the layer's first consumer from the replica sums (CFL_FIN_CONSUMER=0: a 1-block
         # bn_finalize launch per BN layer)
         self.fin_in_consumer = os.environ.get("CFL_FIN_CONSUMER", "1") != "0"
+        # training head: forward (logits, loss / accuracy sums) and backward in ONE pass over x_lo (head.hip FWD),
+        # possible whenever the loss has no whole-batch term (the Dice gradient needs the forward's sums first)
+        # (CFL_HEAD_FUSE=0: head_fwd at the end of forward + head_bwd)
+        self.fuse_head = self.dice == 0 and os.environ.get("CFL_HEAD_FUSE", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
@@ -528,6 +533,8 @@ class UNetEngine:
                 C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
             prev = Lazy(A[f"d{k}_xlo"], None, 0, Rk, F)
         hl = next(n)
+        if train and self.fuse_head:             # the training step's head forward runs inside head_bwd (backward)
+            return
         C.head_fwd(prev.t, self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics if train else self.eval_metrics, B, r[0], DEC_FILTERS[-1], self.dice)
 
@@ -572,7 +579,8 @@ class UNetEngine:
         bn_last = self.bn[names[17 + 5 * 3 + 3]]
         C.head_bwd(A["d3_xlo"], self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics, D["dxlo3"], self.G(hl, "kernel"), self.G(hl, "bias"), B, r[0], DEC_FILTERS[-1],
-                   self.dice, node_y=A["d3_c2"], node_ab=bn_last["ab"], node_sums=bn_last["sums"], node_reps=self.RS)
+                   self.dice, node_y=A["d3_c2"], node_ab=bn_last["ab"], node_sums=bn_last["sums"], node_reps=self.RS,
+                   fused=1 if self.fuse_head else 0)
         dxlo = D["dxlo3"]
         for k in range(3, -1, -1):
             F = DEC_FILTERS[k]
@@ -961,9 +969,13 @@ class UNetEngine:
         main.wait_event(copied)                 # training may overwrite the parameters once they are copied
         return done
 
-    def eval_batch_for(self, n_images: int, cap: int = 128) -> int:
+    def eval_batch_for(self, n_images: int, cap: int = 0) -> int:
         """Largest eval batch <= cap that is a multiple of B and divides ``n_images`` (a whole number of the
-        reference's batches), so every held-out image is evaluated exactly once."""
+        reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 1024
+        images - the inference engine holds forward activations only (21.7 MB per 256^2 image), and batches of
+        several hundred images fill the chip where the 16-48-image forward is launch / latency-bound."""
+        if cap <= 0:
+            cap = int(os.environ.get("CFL_EVAL_CAP", "1024"))
         nb = n_images // self.B
         best = 1
         for k in range(1, nb + 1):
@@ -1039,7 +1051,8 @@ class HipBackend:
 
     def eval_batches(self, batches: np.ndarray) -> Dict[str, float]:
         """Validation over the images of ``batches`` (the reference's 16-image batches), evaluated in the largest
-        multiple of them <= 128 per launch (engine.evaluator: same per-pixel means, fewer / fuller launches)."""
+        multiple of them up to the eval cap per launch (eval_batch_for / evaluator: same per-pixel means, fewer and
+        fuller launches)."""
         e = self.eng
         idx = np.asarray(batches, np.int32).reshape(-1)
         ev = e.evaluator(e.eval_batch_for(len(idx)))

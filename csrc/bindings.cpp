@@ -554,8 +554,9 @@ void head_fwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, 
 
 void head_bwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, at::Tensor idx, at::Tensor h,
                  at::Tensor metrics, at::Tensor dx, at::Tensor dw, at::Tensor db, int B, int R, int Cin, int dice,
-                 OptT node_y, OptT node_ab, OptT node_sums, int node_reps) {
+                 OptT node_y, OptT node_ab, OptT node_sums, int node_reps, int fused) {
   HeadParams p = headp(x, w, bias, masks, idx, h, metrics, B, R, Cin, dice);
+  p.fused = fused;
   p.dx = ptr<bf16_t>(dx, "dx");
   p.dw = ptr<float>(dw, "dw");
   p.db = ptr<float>(db, "db");
@@ -859,7 +860,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_bwd", &head_bwd_op, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("masks"), py::arg("idx"),
         py::arg("h"), py::arg("metrics"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("B"), py::arg("R"),
         py::arg("Cin"), py::arg("dice"), py::arg("node_y") = py::none(), py::arg("node_ab") = py::none(),
-        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1);
+        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("fused") = 0);
   m.def("adam_update", &adam_update_op);
   m.def("adam_step_done", &adam_step_done_op);
   m.def("make_pack_table", &make_pack_table);

@@ -320,6 +320,7 @@ struct HeadParams {
   float* db;
   int B, R, Cin;
   int dice;                // add the Dice loss
+  int fused;               // head_bwd: also do the forward (logits, loss / accuracy sums) in the same pass (dice 0)
   BnNodeEpi node;          // head_bwd: dx is also the (unmasked) gradient of a BN node whose input is node.y (same
                            // layout as x): accumulate its BN-backward sums (the decoder's last BN_B; node.relu unused)
 };

@@ -1114,6 +1114,48 @@ def test_head_loss_metrics_and_gradients_match_autograd(dice):
     assert torch.allclose(sums.view(4, 64).sum(0), ref_s, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("node", [False, True])
+def test_fused_head_train_pass_matches_fwd_then_bwd(node):
+    """head_bwd(fused=1): the training step's head forward done inside the backward pass (one read of x) gives the
+    same logits and dx bits as head_fwd + head_bwd, the same metrics and weight / node sums up to atomic order; the
+    Dice loss (whole-batch sums needed first) is refused."""
+    C = hip()
+    g = torch.Generator().manual_seed(43)
+    B, Rr = 5, 40
+    S = 2 * Rr
+    xb, _ = bf(torch.randn(B, Rr, Rr, 32, generator=g))
+    w = (torch.randn(32, generator=g) * 0.3).to(DEV)
+    bias = (torch.randn(1, generator=g) * 0.1).to(DEV)
+    masks = (torch.rand(7, S, S, generator=g) > 0.7).to(torch.uint8).to(DEV)
+    idx = torch.tensor([3, 1, 4, 6, 0], dtype=torch.int32, device=DEV)
+    yb, _ = bf(torch.randn(B, Rr, Rr, 32, generator=g))
+    nab = ab_for(32, 52)[0]
+    nab[64:96], nab[96:] = torch.randn(32, generator=g) * 0.1, torch.rand(32, generator=g) + 0.5
+    nab = nab.to(DEV)
+    outs = []
+    for fused in (0, 1):
+        h = torch.zeros(B, Rr, Rr, device=DEV)
+        met = torch.zeros(10, dtype=torch.float64, device=DEV)
+        dx = torch.zeros(B, Rr, Rr, 32, dtype=torch.int16, device=DEV)
+        dw, db = torch.zeros(32, device=DEV), torch.zeros(1, device=DEV)
+        sums = torch.zeros(4 * 64, device=DEV)
+        args = (xb, w, bias, masks, idx, h, met)
+        nkw = dict(node_y=yb, node_ab=nab, node_sums=sums, node_reps=4) if node else {}
+        if not fused:
+            C.head_fwd(*args, B, Rr, 32, 0)
+        C.head_bwd(*args, dx, dw, db, B, Rr, 32, 0, fused=fused, **nkw)
+        torch.cuda.synchronize()
+        outs.append((h.cpu(), met.cpu(), dx.cpu(), dw.cpu(), db.cpu(), sums.view(4, 64).sum(0).cpu()))
+    (h0, m0, dx0, dw0, db0, s0), (h1, m1, dx1, dw1, db1, s1) = outs
+    assert torch.equal(h0, h1) and torch.equal(dx0, dx1)
+    assert torch.allclose(m0, m1, rtol=1e-12, atol=1e-9), (m0, m1)
+    assert torch.allclose(dw0, dw1, rtol=1e-5, atol=1e-7) and torch.allclose(db0, db1, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-5)
+    with pytest.raises(RuntimeError):
+        C.head_bwd(xb, w, bias, masks, idx, h0.to(DEV), m0.to(DEV), dx0.to(DEV), dw0.to(DEV), db0.to(DEV), B, Rr, 32,
+                   1, fused=1)
+
+
 @pytest.mark.parametrize("ks,H,Cin,N,B,tune", [
     (1, 32, 32, 64, 4, ""),          # generic implicit GEMM (pointwise conv)
     (3, 16, 64, 32, 2, ""),          # per-tile conv3x3 kernel
