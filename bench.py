@@ -67,6 +67,8 @@ def main() -> int:
                     help="launch-shape knobs for A/B sweeps, 'KEY=V,...' (csrc/kernels/launch.h TuneKey names without "
                          "the TUNE_ prefix, e.g. WGRAD3_BLOCKS=256); default: the built-in heuristics")
     args = ap.parse_args()
+    if os.environ.get("CFL_BENCH_TUNE"):                 # knob sweeps by name from the environment (tools/gpu_ab3.sh)
+        args.tune = ",".join(t for t in (args.tune, os.environ["CFL_BENCH_TUNE"]) if t)
 
     import numpy as np
     import torch

@@ -842,6 +842,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_PW_DEPTH") = (int)TUNE_PW_DEPTH;
   m.attr("TUNE_NODE_POOL_IPT") = (int)TUNE_NODE_POOL_IPT;
   m.attr("TUNE_WGRAD3_MINTILES32") = (int)TUNE_WGRAD3_MINTILES32;
+  m.attr("TUNE_WGRAD_MIX") = (int)TUNE_WGRAD_MIX;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);

@@ -13,6 +13,7 @@
 // WGRAD_REPLICAS replica rows summed by grad_finish), writing Keras layouts (HWIO for Conv2D / pointwise; (kh,kw,out,in) with the spatial flip for Conv2DTranspose).
 #include "common.h"
 #include "launch.h"
+#include "wgrad3_body.h"
 
 namespace {
 
@@ -27,7 +28,10 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
 // RM: pixels per pipeline stage (32 = one MFMA k-step; 128 = four k-steps per barrier and 4x the bytes in flight
 // per stage for the small K x N tiles, which are latency-bound at 32)
 template <int BKO, int BNO, int RM>
-CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int bz) {
+constexpr int wgrad_lds_bytes() { return 2 * RM * (BKO + 16) * 2 + 2 * RM * (BNO + 16) * 2; }
+
+template <int BKO, int BNO, int RM>
+CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int bz, unsigned char* smem) {
   constexpr int TK = BKO / 2, TN = BNO / 2;
   constexpr int FK = TK / 16, FN = TN / 16;
   // LDS rows of 96 / 160 / 288 bytes (32 x odd): the 32 lanes of each ds_read_b64_tr_b16 read 8 CONSECUTIVE pixel
@@ -37,8 +41,8 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
   constexpr int LDX = BKO + 16, LDG = BNO + 16;
   constexpr int XC = RM * BKO / 8, GC = RM * BNO / 8;   // 16-byte chunks per tile
   constexpr int XPT = (XC + NT - 1) / NT, GPT = (GC + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][RM][LDX];
-  __shared__ __attribute__((aligned(16))) bf16_t sG[2][RM][LDG];
+  bf16_t (*sX)[RM][LDX] = reinterpret_cast<bf16_t (*)[RM][LDX]>(smem);
+  bf16_t (*sG)[RM][LDG] = reinterpret_cast<bf16_t (*)[RM][LDG]>(smem + 2 * RM * LDX * 2);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid >> 1, wn = wid & 1;
@@ -200,7 +204,8 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
 
 template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
-  wgrad_body<BKO, BNO, RM>(p, chunk, blockIdx.x, blockIdx.y, blockIdx.z);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad_lds_bytes<BKO, BNO, RM>()];
+  wgrad_body<BKO, BNO, RM>(p, chunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // pixels per block (multiple of rm) and M splits of a generic weight gradient with a bko x bno output tile
@@ -248,12 +253,13 @@ struct WgradGroup {
 
 template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_group_kernel(const WgradGroup g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad_lds_bytes<BKO, BNO, RM>()];
   int k = 0;
   while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
   const WgradItem& I = g.it[k];
   const int local = blockIdx.x - I.block0;
   const int bx = local % I.gx, r = local / I.gx;
-  wgrad_body<BKO, BNO, RM>(I.p, I.chunk, bx, r % I.gy, r / I.gy);
+  wgrad_body<BKO, BNO, RM>(I.p, I.chunk, bx, r % I.gy, r / I.gy, smem);
 }
 
 // tile config of a generic weight gradient (see conv_wgrad) and its (BKO, BNO, RM)
@@ -295,6 +301,53 @@ int launch_group(const WgradParams* ps, int n, hipStream_t st) {
   return 0;
 }
 
+// Mixed launch: every deferred weight gradient of a step - the 3x3 halo ones (wgrad3_body.h) and the generic 1x1 /
+// strided ones of every tile config - in ONE grid. Alone (or grouped per config, five launches) each is a
+// latency-bound grid that leaves the chip part-idle in its tail; in one grid the blocks of all of them co-run and
+// the four launch boundaries between the groups are gone. One LDS buffer sized for the largest body (the 64-wide
+// halo config, 75.5 KB: 2 blocks per CU, as the halo groups had); the kernel's VGPR count is the largest body's.
+// kind: 0-3 halo config (conv3x3_wgrad_config), 10 + c generic config c (wgrad_config; c = 1, the 80 KB
+// 128-pixel-stage variant, is launched on its own)
+constexpr int MIX_MAX = 24;
+struct MixItem {
+  WgradParams p;
+  int kind;
+  int a, b;                 // halo: pixel tiles, pixel splits; generic: pixels per block, unused
+  int gx, gy, block0;
+};
+struct MixGroup {
+  MixItem it[MIX_MAX];
+  int n;
+};
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int MIX_LDS = cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wgrad_lds_bytes<128, 128, 32>()),
+                             cmax(cmax(wgrad_lds_bytes<64, 32, 128>(), wgrad_lds_bytes<32, 64, 128>()),
+                                  cmax(wgrad_lds_bytes<32, 32, 128>(), wgrad_lds_bytes<64, 64, 64>())));
+static_assert(MIX_LDS <= 80 * 1024, "two mixed blocks per CU");
+
+__global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[MIX_LDS];
+  int k = 0;
+  while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
+  // the item is copied out of the argument block first (a reference into it, indexed by a runtime k, made the
+  // compiler spill the whole 3 KB block to scratch)
+  const WgradParams P = g.it[k].p;
+  const int kind = g.it[k].kind, a = g.it[k].a, b = g.it[k].b, gx = g.it[k].gx, gy = g.it[k].gy;
+  const int local = blockIdx.x - g.it[k].block0;
+  const int bx = local % gx, r = local / gx, by = r % gy, bz = r / gy;
+  switch (kind) {
+    case 0: wg3::wgrad3_body<64, true>(P, a, b, bx, by, bz, smem); break;
+    case 1: wg3::wgrad3_body<64, false>(P, a, b, bx, by, bz, smem); break;
+    case 2: wg3::wgrad3_body<32, true>(P, a, b, bx, by, bz, smem); break;
+    case 3: wg3::wgrad3_body<32, false>(P, a, b, bx, by, bz, smem); break;
+    case 10: wgrad_body<128, 128, 32>(P, a, bx, by, bz, smem); break;
+    case 12: wgrad_body<64, 32, 128>(P, a, bx, by, bz, smem); break;
+    case 13: wgrad_body<32, 64, 128>(P, a, bx, by, bz, smem); break;
+    case 14: wgrad_body<32, 32, 128>(P, a, bx, by, bz, smem); break;
+    default: wgrad_body<64, 64, 64>(P, a, bx, by, bz, smem); break;   // 15
+  }
+}
+
 }  // namespace
 
 bool conv3x3_wgrad_supported(const WgradParams& p);
@@ -310,16 +363,83 @@ bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x
 
 int conv3x3_wgrad_config(const WgradParams& p);
 int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st);
+void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits);
 
 static bool generic_ok(const WgradParams& p) {
   return p.Cin % 8 == 0 && p.K == p.ks * p.ks * p.Cin && p.K % 32 == 0 && p.N % 32 == 0;
 }
+
+// the mixed launches of conv_wgrad_batch: halo items first (the longest blocks start first), MIX_MAX per launch
+static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
+  MixGroup g{};
+  int blocks = 0;
+  auto flush = [&]() -> int {
+    if (g.n == 0) return 0;
+    hipLaunchKernelGGL(wgrad_mix_kernel, dim3(blocks), dim3(NT), 0, st, g);
+    g = MixGroup{};
+    blocks = 0;
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  };
+  for (int pass = 0; pass < 2; ++pass)
+    for (int i = 0; i < n; ++i) {
+      const WgradParams& p = ps[i];
+      const bool halo = p.algo != 1 && conv3x3_wgrad_supported(p);
+      if (halo != (pass == 0)) continue;
+      if (g.n == MIX_MAX) {
+        const int rc = flush();
+        if (rc) return rc;
+      }
+      MixItem& it = g.it[g.n++];
+      it.p = p;
+      int zs;
+      if (halo) {
+        int bno;
+        conv3x3_wgrad_shape(p, bno, it.a, it.b);
+        if (p.slabs > 0 && p.slabs != it.b) return 2;
+        it.kind = conv3x3_wgrad_config(p);
+        it.gx = p.Cin / 32;
+        it.gy = p.N / bno;
+        zs = it.b;
+      } else {
+        int bko, bno, rm;
+        it.kind = 10 + wgrad_config(p, bko, bno, rm);
+        wgrad_shape(p, bko, bno, rm, it.a, zs);
+        it.b = 0;
+        it.gx = p.K / bko;
+        it.gy = p.N / bno;
+      }
+      it.block0 = blocks;
+      blocks += it.gx * it.gy * zs;
+    }
+  return flush();
+}
+
+static bool mix_ok(const WgradParams& p) {
+  if (p.algo != 1 && conv3x3_wgrad_supported(p)) return true;
+  int bko, bno, rm;
+  return generic_ok(p) && wgrad_config(p, bko, bno, rm) != 1;
+}
+
 
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
   static thread_local WgradParams by_cfg[4][16], gen_cfg[6][32];
   int cnt[4] = {0, 0, 0, 0}, gcnt[6] = {0, 0, 0, 0, 0, 0};
   const bool group = cfl_tune(TUNE_WGRAD_GROUP) != 1;
   const bool group1 = group && cfl_tune(TUNE_WGRAD_GROUP) != 2;
+  if (group1 && cfl_tune(TUNE_WGRAD_MIX) != 1) {            // default: one mixed launch (plus any odd ones out)
+    static thread_local WgradParams mix[64];
+    int nm = 0;
+    for (int i = 0; i < n; ++i) {
+      if (ps[i].slabs > 0 && ps[i].slabs != conv_wgrad_slabs(ps[i])) return 2;
+      if (mix_ok(ps[i]) && nm < 64) {
+        mix[nm++] = ps[i];
+      } else {
+        const int rc = conv_wgrad(ps[i], st);
+        if (rc) return rc;
+      }
+    }
+    return launch_mix(mix, nm, st);
+  }
   for (int i = 0; i < n; ++i) {
     const WgradParams& p = ps[i];
     if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;

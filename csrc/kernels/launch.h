@@ -418,7 +418,8 @@ enum TuneKey {
   TUNE_PW_DEPTH = 27,          // streaming 1x1 kernel: tiles in flight per wave (1 default, 2, 4 at K = 32)
   TUNE_NODE_POOL_IPT = 28,     // max-pool node gradient: 2x2 items per thread per trip (1 default, 2)
   TUNE_WGRAD3_MINTILES32 = 29, // halo wgrad, 32-wide output tiles: min pixel tiles per block (default 4)
-  TUNE_N = 30
+  TUNE_WGRAD_MIX = 30,         // conv_wgrad_batch: 0 = every deferred wgrad in ONE mixed launch, 1 = a launch per config
+  TUNE_N = 31
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -1282,12 +1282,15 @@ def test_training_parity_vs_plain_fp32():
         assert v >= min(0.85, cos_ac[k] - 0.05), (k, v, cos_ac[k])
 
 
-def test_conv_wgrad_batch_grouped_equals_individual():
-    """conv_wgrad_batch (the engine's deferred weight gradients): 3x3 halo wgrads of different layers grouped into
-    shared launches per tile config (bit-identical slabs to one call each) and generic 1x1 wgrads grouped per tile
-    config (replica-row atomics: equal up to float summation order)."""
+@pytest.mark.parametrize("mix", [0, 1])
+def test_conv_wgrad_batch_grouped_equals_individual(mix):
+    """conv_wgrad_batch (the engine's deferred weight gradients): every wgrad in ONE mixed launch (default, mix=0)
+    or 3x3 halo wgrads of different layers grouped into shared launches per tile config (mix=1) - bit-identical
+    slabs to one call each - and generic 1x1 wgrads in the same mixed launch or grouped per tile config
+    (replica-row atomics: equal up to float summation order)."""
     torch.manual_seed(41)
     C_ = hip()
+    C_.set_tune(C_.TUNE_WGRAD_MIX, mix)
     shapes = [  # (B, Hin, Cin, up, Ho, N, ks, dst_mode)
         (2, 16, 64, 0, 16, 32, 3, 1), (2, 8, 64, 1, 16, 32, 3, 1), (2, 16, 32, 0, 16, 64, 3, 1),
         (2, 16, 64, 0, 16, 64, 3, 1), (2, 16, 32, 0, 16, 64, 1, 0), (3, 8, 32, 0, 8, 32, 3, 0),
@@ -1301,7 +1304,10 @@ def test_conv_wgrad_batch_grouped_equals_individual():
         rows, _plain = C_.conv_wgrad_slabs(B, Hin, Hin, Cin, up, Ho, Ho, N, ks, 1, pad, pad)
         slab = torch.zeros(rows * ks * ks * Cin * N, device=DEV)
         calls.append((x, dy, slab, ab, 1, B, Hin, Hin, Cin, up, Ho, Ho, N, ks, 1, pad, pad, dm, 0, 0, rows))
-    C_.conv_wgrad_batch(calls)
+    try:
+        C_.conv_wgrad_batch(calls)
+    finally:
+        C_.set_tune(C_.TUNE_WGRAD_MIX, 0)
     batched = [c[2].clone() for c in calls]
     for c in calls:
         c[2].zero_()
