@@ -86,10 +86,6 @@ class UNetEngine:
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
         self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
-        # CFL_WGRAD_STREAM=1: weight gradients on a second HIP stream, concurrent with the dgrad chain. Off: the
-        # forked graph measured 9% SLOWER per step (8,670 -> 7,880 img/s, profiles/README.md)
-        self.side = torch.cuda.Stream(device=self.dev) if (self.dev.type == "cuda" and share is None and os.environ.get(
-            "CFL_WGRAD_STREAM", "0") == "1") else None
         self._build_pack()
         self._alloc()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -261,24 +257,12 @@ class UNetEngine:
         self._finish_dyn: List[tuple] = []
         self._wslabs: Dict[str, torch.Tensor] = {}
         self._build_finish()
-        # CFL_BN_TAIL=1: in-launch BN finalize (launch.h BnFinal; one ticket counter per BN layer, the producer's last
-        # block computes the coefficients). Off by default: the per-block ticket round trip (atomics drained, then a
-        # returning atomic) delays every block's retirement - measured 7.5% SLOWER per step than the 15 separate
-        # 1-block bn_finalize launches (8,730 -> 8,076 img/s, profiles/README.md)
-        self.bn_tail = os.environ.get("CFL_BN_TAIL", "0") == "1"
         # weight gradients (off the backward critical path: they read forward activations and incoming gradients
         # that are never overwritten within a step) deferred to the end of backward and issued as ONE batch, the 3x3
         # halo ones grouped per tile config into shared launches (conv_wgrad_batch) so their latency-bound grids
         # co-run (CFL_WGRAD_DEFER=0: each issued where it is computed)
         self.defer_wgrad = os.environ.get("CFL_WGRAD_DEFER", "1") != "0"
-        # BN-backward apply folded into the operand load of the data-gradient conv that consumes it (conv_igemm
-        # bwd=...; 14 of the 15 bn_bwd_apply passes - the entry BN's feeds only the entry weight gradient), which
-        # also stores dx for the weight gradient (CFL_BNB_FOLD=0: separate bn_bwd_apply launches)
-        self.fold_bnb = os.environ.get("CFL_BNB_FOLD", "0") == "1"
-        # ... or only at the levels whose side is <= CFL_BNB_FOLD_RES (the low-resolution bn_bwd_apply passes are
-        # launch-bound: 4.3 us for 1-6 MB, profiles/r2_final/roofline.txt)
-        self.fold_res = int(os.environ.get("CFL_BNB_FOLD_RES", "0"))
-        # ... and (default) into the encoder's pointwise data gradients: the streaming 1x1 kernel (pw.hip) applies it
+        # BN-backward apply folded into the encoder's pointwise data gradients: the streaming 1x1 kernel (pw.hip) applies it
         # to its B-fragment registers and stores dx from the first output slice's blocks - 6 bn_bwd_apply launches
         # fewer, whole step 1.4421-1.4524 -> 1.4358-1.4361 ms/iteration (CFL_BNB_FOLD_PW=0: separate passes)
         self.fold_pw = os.environ.get("CFL_BNB_FOLD_PW", "1") != "0"
@@ -302,11 +286,12 @@ class UNetEngine:
         # possible whenever the loss has no whole-batch term (the Dice gradient needs the forward's sums first)
         # (CFL_HEAD_FUSE=0: head_fwd at the end of forward + head_bwd)
         self.fuse_head = self.dice == 0 and os.environ.get("CFL_HEAD_FUSE", "1") != "0"
+        # SeparableConv forward in one pass (sepconv.hip; CFL_SEP_FUSE=0: dw_fwd + pointwise conv)
+        self.fuse_sep = os.environ.get("CFL_SEP_FUSE", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
-        self.bn_ctr = torch.zeros(16, dtype=torch.int32, device=self.dev)
         # per-step zeroing of gradients / statistics in one launch
-        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10], self.bn_ctr]
+        spans = [self.grad, self.stats_all, self.sums_all, self.metrics[4:10]]
         self.zero_table = self.C.make_zero_table(spans)
         self.n_zero, self.max_zero = len(spans), max(t.numel() * t.element_size() for t in spans)
         # inference BN coefficients of every layer (one launch per eval forward)
@@ -352,24 +337,6 @@ class UNetEngine:
         else:
             self.C.conv_wgrad(*args)
 
-    def _side(self, fn) -> None:
-        """Launch ``fn``'s kernels on the weight-gradient stream after everything issued so far on the current
-        stream (a forked graph branch under capture). Weight gradients only read forward activations and the
-        incoming gradient and write their own slabs, so the dgrad chain continues concurrently; the branch joins
-        before grad_finish. Buffers a wgrad reads are never rewritten later in the same backward (dc2 / dy2)."""
-        if self.side is None:
-            fn()
-            return
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.dev))
-        self.side.wait_event(ev)
-        with torch.cuda.stream(self.side):
-            fn()
-
-    def _join_side(self) -> None:
-        if self.side is not None:
-            torch.cuda.current_stream(self.dev).wait_stream(self.side)
-
     def bn_count(self, name: str) -> int:
         """Pixels per channel in the batch statistics of a BN layer."""
         i = self.bn_names.index(name)
@@ -401,20 +368,10 @@ class UNetEngine:
             ev.bind_data(self.images, self.masks)
 
     # ------------------------------------------------------------------------------------------------ schedule
-    def _fin(self, name: str, train: bool) -> Dict[str, object]:
-        """Producer kwargs that make the launch accumulating BN layer ``name``'s batch statistics also finalize
-        them (in its last block); empty in inference mode or with the tail disabled."""
-        if not train or not self.bn_tail:
-            return {}
-        b = self.bn[name]
-        i = self.bn_names.index(name)
-        return dict(fin_ab=b["ab"], fin_gamma=self.P(name, "gamma"), fin_beta=self.P(name, "beta"),
-                    fin_ctr=self.bn_ctr[i:i + 1], fin_count=float(self.bn_count(name)), fin_eps=self.bn_eps)
-
     def _xfin(self, name: str, train: bool) -> Dict[str, object]:
         """Consumer-side BN finalize kwargs: the consumer computes layer ``name``'s coefficients from its replica
         sums (and writes its ab rows) instead of a bn_finalize launch (empty: ab is final already)."""
-        if not train or self.bn_tail or not self.fin_in_consumer:
+        if not train or not self.fin_in_consumer:
             return {}
         return dict(xfin_stats=self.bn[name]["stats"], xfin_gamma=self.P(name, "gamma"),
                     xfin_beta=self.P(name, "beta"), xfin_count=float(self.bn_count(name)), xfin_eps=self.bn_eps)
@@ -426,8 +383,8 @@ class UNetEngine:
     def _bn_final(self, name: str, train: bool, consumer: bool = False) -> torch.Tensor:
         """ab of BN layer ``name``; consumer=True: its next consumer finalizes it (_xfin), nothing is launched."""
         b = self.bn[name]
-        if not train or self.bn_tail or (consumer and self.fin_in_consumer):
-            return b["ab"]          # inference: written by forward()'s bn_eval_coefs; train: by the producer's tail
+        if not train or (consumer and self.fin_in_consumer):
+            return b["ab"]          # inference: written by forward()'s bn_eval_coefs; train: by the next consumer
         self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
                            self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
                            float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
@@ -435,7 +392,7 @@ class UNetEngine:
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
-               join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None,
+               join: Optional[Dict[str, object]] = None,
                bwd: Optional[Tuple[torch.Tensor, str, torch.Tensor]] = None, **extra) -> None:
         """conv_igemm with the shared split-K workspace (grown on the eager warm-up pass, before graph capture).
 
@@ -456,8 +413,6 @@ class UNetEngine:
             kw = dict(node_y=ny, node_ab=bn["ab"], node_sums=bn["sums"], node_reps=self.RS, node_relu=nrelu)
         if join:
             kw.update(join)
-        if fin:
-            kw.update(fin)
         kw.update(extra)
         if bwd is not None:
             by, bname, bdx = bwd
@@ -469,11 +424,11 @@ class UNetEngine:
 
     def _conv(self, x: Lazy, layer: str, kind: int, y: torch.Tensor, N: int, ks: int, stride: int, up_in: int,
               Ho: int, bias: Optional[torch.Tensor], stats: Optional[torch.Tensor],
-              join: Optional[Dict[str, object]] = None, fin: Optional[Dict[str, object]] = None, **extra) -> None:
+              join: Optional[Dict[str, object]] = None, **extra) -> None:
         pad = (ks - 1) // 2 if stride == 1 else 0
         B = self.B
         self._igemm(x.t, self.W(layer, kind), bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho,
-                    N, ks, stride, pad, pad, join=join, fin=fin, **extra)
+                    N, ks, stride, pad, pad, join=join, **extra)
 
     def forward(self, train: bool = True) -> None:
         C, B, r, A = self.C, self.B, self.r, self.act
@@ -485,22 +440,18 @@ class UNetEngine:
         e_conv, e_bn = next(n), next(n)
         st = self.bn[e_bn]["stats"] if train else None
         C.entry_fwd(self.images, self.idx, self.P(e_conv, "kernel"), self.P(e_conv, "bias"), A["y0"], st, B, self.S,
-                    ENTRY_FILTERS, **self._fin(e_bn, train))
+                    ENTRY_FILTERS)
         ab0 = self._bn_final(e_bn, train, consumer=True)
         x = Lazy(A["y0"], ab0, 1, r[0], ENTRY_FILTERS)     # a0 = relu(BN0(y0))
         for k, F in enumerate(ENC_FILTERS):
             s1, b1, s2, b2, rc = (next(n) for _ in range(5))
             H = r[k]
-            # the depthwise conv is the first consumer of BN0 (k = 0): it finalizes it
-            C.dw_fwd(x.t, self.P(s1, "depthwise_kernel"), A[f"e{k}_d1"], x.ab, 1, B, H, H, x.C,
-                     **(self._xfin(e_bn, train) if k == 0 else {}))
-            self._conv(Lazy(A[f"e{k}_d1"], None, 0, H, x.C), s1, PK_PW, A[f"e{k}_y1"], F, 1, 1, 0, H,
-                       self.P(s1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
+            # SeparableConv 1: the depthwise conv is the first consumer of BN0 (k = 0): it finalizes it
+            self._sepconv(x.t, x.ab, s1, A[f"e{k}_d1"], A[f"e{k}_y1"], b1, H, x.C, F, train,
+                          self._xfin(e_bn, train) if k == 0 else {})
             ab1 = self._bn_final(b1, train, consumer=True)
-            C.dw_fwd(A[f"e{k}_y1"], self.P(s2, "depthwise_kernel"), A[f"e{k}_d2"], ab1, 1, B, H, H, F,
-                     **self._xfin(b1, train))
-            self._conv(Lazy(A[f"e{k}_d2"], None, 0, H, F), s2, PK_PW, A[f"e{k}_y2"], F, 1, 1, 0, H,
-                       self.P(s2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train))
+            self._sepconv(A[f"e{k}_y1"], ab1, s2, A[f"e{k}_d2"], A[f"e{k}_y2"], b2, H, F, F, train,
+                          self._xfin(b1, train))
             ab2 = self._bn_final(b2, train, consumer=self.fuse_join)
             if self.fuse_join:   # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
                 self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
@@ -517,10 +468,10 @@ class UNetEngine:
             Rk = r[3] << k
             up = 0 if k == 0 else 1
             self._convt(Lazy(prev.t, None, 1, prev.H, prev.C), t1, A[f"d{k}_c1"], F, up, Rk,
-                        self.P(t1, "bias"), self.bn[b1]["stats"] if train else None, fin=self._fin(b1, train))
+                        self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
             abA = self._bn_final(b1, train, consumer=True)       # finalized by the convT2 forward below
             self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
-                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None, fin=self._fin(b2, train),
+                        self.P(t2, "bias"), self.bn[b2]["stats"] if train else None,
                         **self._xfin(b1, train))
             abB = self._bn_final(b2, train, consumer=self.fuse_join)
             if self.fuse_join:   # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
@@ -538,6 +489,21 @@ class UNetEngine:
         C.head_fwd(prev.t, self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics if train else self.eval_metrics, B, r[0], DEC_FILTERS[-1], self.dice)
 
+    def _sepconv(self, x: torch.Tensor, ab: Optional[torch.Tensor], layer: str, d: torch.Tensor, y: torch.Tensor,
+                 bn: str, H: int, K: int, N: int, train: bool, xfin: Dict[str, object]) -> None:
+        """SeparableConv2D forward on relu(BN(x)) (client_fit_model.py:109,113): d = depthwise 3x3, y = pointwise(d)
+        + bias with BN ``bn``'s batch statistics. One fused launch (sepconv.hip: the depthwise output formed in the
+        pointwise MFMA's operand registers, d side-stored for the weight gradient) where the kernel covers the shape,
+        else dw_fwd + the streaming pointwise conv."""
+        C, B = self.C, self.B
+        stats = self.bn[bn]["stats"] if train else None
+        if self.fuse_sep and C.sep_fwd_supported(B, H, H, K, N):
+            C.sep_fwd(x, ab, 1, self.P(layer, "depthwise_kernel"), self.W(layer, PK_PW), self.P(layer, "bias"), d, y,
+                      stats, B, H, H, K, N, **xfin)
+            return
+        C.dw_fwd(x, self.P(layer, "depthwise_kernel"), d, ab, 1, B, H, H, K, **xfin)
+        self._conv(Lazy(d, None, 0, H, K), layer, PK_PW, y, N, 1, 1, 0, H, self.P(layer, "bias"), stats)
+
     def _dw_wgrad(self, *args) -> None:
         """Depthwise weight gradient: deferred with the conv weight gradients (its inputs - a forward activation and
         the depthwise dgrad's incoming gradient - are not rewritten later in backward) and issued in one grouped
@@ -545,11 +511,7 @@ class UNetEngine:
         if self._dwq is not None:
             self._dwq.append(args + (0,))
         else:
-            self._side(lambda: self.C.dw_wgrad(*args))
-
-    def _fold_at(self, res: int) -> bool:
-        """Fold the BN-backward apply of a level with side ``res`` into its data-gradient conv's operand load."""
-        return self.fold_bnb or res <= self.fold_res
+            self.C.dw_wgrad(*args)
 
     def backward(self) -> None:
         self._wq = [] if self.defer_wgrad else None
@@ -563,7 +525,6 @@ class UNetEngine:
             self.C.dw_wgrad_batch(dwq)
         if wq:
             self.C.conv_wgrad_batch(wq)
-        self._join_side()
         if self._finish_dirty:
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("grad_finish table changed during graph capture")
@@ -592,13 +553,12 @@ class UNetEngine:
             prevres = Rk if k == 0 else Rk // 2
             up = 0 if k == 0 else 1
             bnB, bnA = self.bn[b2], self.bn[b1]
-            fold = self._fold_at(Rk)
             # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. Its BN-backward sums were
-            # accumulated by the pass that produced dxlo: head_bwd (k = 3) or the plain node pass of level k+1
-            gB = dxlo
-            if not fold:
-                C.bn_bwd_apply(gB, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
-                               self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
+            # accumulated by the pass that produced dxlo: head_bwd (k = 3) or the convT1 dgrad join of level k+1.
+            # The BN-backward applies of the decoder run as streaming passes: folded into the latency-bound 3x3
+            # dgrads' operand loads they measured slower twice (profiles/README.md, the folds were removed)
+            C.bn_bwd_apply(dxlo, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
+                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
             # (k > 0, default) the 2x2 sum is formed by the dgrad's operand load, which also stores dq for the
             # weight gradient (issued after it)
@@ -612,19 +572,16 @@ class UNetEngine:
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
                          prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if s2 else {}))
-            self._side(lambda: self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
-                                           F, 1, 1, 0, 0, 0))
-            # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue; folded: its operand is
-            # BN_B's backward apply of g_B (it stores dc = that dx for the weight gradient)
-            self._igemm(gB if fold else D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None,
-                        0, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1),
-                        bwd=(A[f"d{k}_c2"], b2, D[f"d{k}_dc"]) if fold else None)
+            self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
+                        F, 1, 1, 0, 0, 0)
+            # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
+            self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None,
+                        0, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1))
             # convT2: input relu(BN_A(c1))
-            self._side(lambda: self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
-                                           F, 3, 1, 1, 1, 1))
-            if not fold:
-                C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
-                               self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
+            self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
+                        F, 3, 1, 1, 1, 1)
+            C.bn_bwd_apply(D[f"d{k}_g"], A[f"d{k}_c1"], bnA["ab"], bnA["sums"], D[f"d{k}_dc2"],
+                           self.G(b1, "gamma"), self.G(b1, "beta"), B * Rk * Rk, F, self.RS)
             # grad of prev (x_lo_{k-1} or x3): relu-masked main path (2x2 summed when upsampled) + residual path;
             # for k > 0 this gradient is also BN_B(k-1)'s node gradient (its BN-backward sums accumulate here) -
             # the join runs in the convT1 dgrad's epilogue at half resolution (dxin is never stored)
@@ -633,12 +590,11 @@ class UNetEngine:
                 bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
                 pjkw = dict(pj_v=prev_t, pj_add=D[f"d{k}_dres"], pj_out=D[f"d{k}_dprev"], pj_sy=A[f"d{k - 1}_c2"],
                             pj_sab=bprev["ab"], pj_sums=bprev["sums"], pj_reps=self.RS)
-            self._igemm(D[f"d{k}_g"] if fold else D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None,
-                        D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1,
-                        bwd=(A[f"d{k}_c1"], b1, D[f"d{k}_dc2"]) if fold else None, **pjkw)
+            self._igemm(D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None,
+                        D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1, **pjkw)
             # convT1: input relu(up?(prev))
-            self._side(lambda: self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
-                                           Rk, F, 3, 1, 1, 1, 1))
+            self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
+                        Rk, F, 3, 1, 1, 1, 1)
             if not pjkw and k > 0:
                 bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
                 C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
@@ -661,7 +617,7 @@ class UNetEngine:
             else:
                 xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
             bnb, bna = self.bn[b2], self.bn[b1]
-            fold = self._fold_at(H) or self.fold_pw
+            fold = self.fold_pw
             # BN_b node: routed through the max-pool (no ReLU)
             C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
                        bnb["sums"], B, H, H, F, self.RS)
@@ -672,8 +628,8 @@ class UNetEngine:
             self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None,
                         None, 0, B, H, H, F, 0, H, H, F, 1, 1, 0, 0,
                         bwd=(A[f"e{k}_y2"], b2, D[f"e{k}_dy"]) if fold else None)
-            self._side(lambda: self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
-                                           F, 0, H, H, F, 1, 1, 0, 0, 0))
+            self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
+                        F, 0, H, H, F, 1, 1, 0, 0, 0)
             # depthwise 2 on relu(BN_a(y1))
             # depthwise 2 on relu(BN_a(y1)): dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue,
             # and (fused pass) the weight gradient from the same dy rows
@@ -695,11 +651,11 @@ class UNetEngine:
             self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy2"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"],
                         None, None, 0, B, H, H, F, 0, H, H, cin, 1, 1, 0, 0,
                         bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]) if fold else None)
-            self._side(lambda: self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
-                                           H, cin, 0, H, H, F, 1, 1, 0, 0, 0))
+            self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
+                        H, cin, 0, H, H, F, 1, 1, 0, 0, 0)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
-            self._side(lambda: self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
-                                           1, 2, 0, 0, 0))
+            self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
+                        1, 2, 0, 0, 0)
             # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                          H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
@@ -783,13 +739,13 @@ class UNetEngine:
                             self.amax8 if step else None, self.n_views8)
 
     def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
-               bias: torch.Tensor, stats: Optional[torch.Tensor], fin: Optional[Dict[str, object]] = None,
+               bias: torch.Tensor, stats: Optional[torch.Tensor],
                **extra) -> None:
         """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled (maps of at least 8x8; smaller ones - only
         at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel. ``extra``: consumer-side
         finalize kwargs of the input's BN (bf16 path only)."""
         if not self.fp8 or Ho < 8:
-            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, fin=fin, **extra)
+            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra)
             return
         if extra:                              # the fp8 kernel reads a final ab
             xs = extra
@@ -807,7 +763,7 @@ class UNetEngine:
             self._await_all()                # the fp8 copies are repacked after the LAST FedAvg bucket
         self.C.conv3x3_fp8(x.t, self.packed8[off8:off8 + n8], self.scales8[soff:soff + cout], self.amax8[i],
                            bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho, N,
-                           self.ws if need > 1 else None, **(fin or {}))
+                           self.ws if need > 1 else None)
 
     def _fp8_calibrate(self) -> None:
         """Seed the delayed activation scales: one training-mode forward records every fp8 conv input's amax,

@@ -63,7 +63,7 @@ def buffer_shapes(B: int, S: int) -> Tuple[Dict[str, Tuple[Tuple[int, ...], int]
         prevres = Rk if k == 0 else Rk // 2
         D[f"d{k}_g"] = ((B, Rk, Rk, F), BF16)
         D[f"d{k}_dc"] = ((B, Rk, Rk, F), BF16)
-        D[f"d{k}_dc2"] = ((B, Rk, Rk, F), BF16)       # 2nd BN input-gradient (dc is still read by a side-stream wgrad)
+        D[f"d{k}_dc2"] = ((B, Rk, Rk, F), BF16)       # 2nd BN input-gradient (dc is still read by a deferred wgrad)
         D[f"d{k}_dxin"] = ((B, Rk, Rk, cprev), BF16)
         D[f"d{k}_dq"] = ((B, _qres(k, Rk), _qres(k, Rk), F), BF16)
         D[f"d{k}_dres"] = ((B, prevres, prevres, cprev), BF16)

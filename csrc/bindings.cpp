@@ -39,24 +39,6 @@ void ok(int rc, const char* what) {
 
 InXform xf(const OptT& ab, int C, int relu) { return InXform{optr<const float>(ab, "ab"), C, relu}; }
 
-// in-launch BN finalize arguments (launch.h BnFinal); fin_ab = None -> off (the engine launches nothing else then)
-BnFinal fin_args(const OptT& fin_ab, const OptT& fin_gamma, const OptT& fin_beta, const OptT& fin_ctr, double count,
-                 double eps, int C, bool has_stats) {
-  BnFinal f{};
-  if (!fin_ab) return f;
-  TORCH_CHECK(has_stats && fin_gamma && fin_beta && fin_ctr, "BN finalize: needs stats, fin_gamma, fin_beta, fin_ctr");
-  TORCH_CHECK(fin_ab->numel() >= 4 * C && fin_gamma->numel() >= C && fin_beta->numel() >= C &&
-              fin_ctr->numel() >= 1 && fin_ctr->element_size() == 4 && count > 0 && C <= 256,
-              "BN finalize: argument sizes");
-  f.ab = ptr<float>(*fin_ab, "fin_ab");
-  f.gamma = ptr<const float>(*fin_gamma, "fin_gamma");
-  f.beta = ptr<const float>(*fin_beta, "fin_beta");
-  f.counter = ptr<unsigned>(*fin_ctr, "fin_ctr");
-  f.count = (float)count;
-  f.eps = (float)eps;
-  return f;
-}
-
 // fused BN-node gradient epilogue arguments (launch.h BnNodeEpi); node_y = None -> off
 BnNodeEpi node_epi_args(const OptT& node_y, const OptT& node_ab, const OptT& node_sums, int reps, int relu,
                         int64_t out_numel, int C) {
@@ -93,8 +75,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
                    int node_relu, int join_mode, OptT join_y, OptT join_ab, OptT join_out, OptT join_argmax,
-                   int join_H, int join_W, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
-                   double fin_eps, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
+                   int join_H, int join_W, OptT bwd_y, OptT bwd_ab, OptT bwd_sums, int bwd_reps, OptT bwd_dx, OptT bwd_dgamma,
                    OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
                    int pj_reps, OptT jfin_stats, OptT jfin_gamma, OptT jfin_beta, double jfin_count,
                    double jfin_eps, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count,
@@ -120,7 +101,6 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv_igemm: stats size");
   p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, node_relu, y.numel(), N);
   TORCH_CHECK(!p.node.y || (!p.stats && !p.bias), "conv_igemm: the node epilogue excludes stats and bias");
-  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, N, p.stats != nullptr);
   if (join_mode) {
     TORCH_CHECK(join_mode >= JOIN_POOL && join_mode <= JOIN_ADD_UP && join_y && join_ab && join_out,
                 "conv_igemm: join needs join_y, join_ab, join_out");
@@ -264,6 +244,41 @@ std::tuple<int, bool> conv_wgrad_slabs_op(int B, int Hin, int Win, int Cin, int 
   return {conv_wgrad_slabs(p), conv_wgrad_plain_slabs(p)};
 }
 
+SepParams sepp(at::Tensor x, OptT ab, int relu, at::Tensor wdw, at::Tensor wpw, OptT bias, at::Tensor d, at::Tensor y,
+               OptT stats, int B, int H, int W, int K, int N, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta,
+               double xfin_count, double xfin_eps) {
+  SepParams p{};
+  p.x = ptr<const bf16_t>(x, "x");
+  p.xf = xf(ab, K, relu);
+  p.xfin = stats_in(xfin_stats, xfin_gamma, xfin_beta, xfin_count, xfin_eps, K, ab);
+  p.wdw = ptr<const float>(wdw, "wdw");
+  p.wpw = ptr<const bf16_t>(wpw, "wpw");
+  p.bias = optr<const float>(bias, "bias");
+  p.d = ptr<bf16_t>(d, "d");
+  p.y = ptr<bf16_t>(y, "y");
+  p.stats = optr<float>(stats, "stats");
+  p.B = B; p.H = H; p.W = W; p.K = K; p.N = N;
+  const int64_t px = (int64_t)B * H * W;
+  TORCH_CHECK(x.numel() == px * K && d.numel() == px * K && y.numel() == px * N && wdw.numel() == 9 * K &&
+              wpw.numel() == (int64_t)K * N && (!bias || bias->numel() == N) &&
+              (!stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N) && (!ab || ab->numel() >= 2 * K),
+              "sep_fwd sizes");
+  return p;
+}
+
+bool sep_fwd_supported_op(int B, int H, int W, int K, int N) {
+  SepParams p{};
+  p.B = B; p.H = H; p.W = W; p.K = K; p.N = N;
+  return sep_fwd_supported(p);
+}
+
+void sep_fwd_op(at::Tensor x, OptT ab, int relu, at::Tensor wdw, at::Tensor wpw, OptT bias, at::Tensor d, at::Tensor y,
+                OptT stats, int B, int H, int W, int K, int N, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta,
+                double xfin_count, double xfin_eps) {
+  ok(sep_fwd(sepp(x, ab, relu, wdw, wpw, bias, d, y, stats, B, H, W, K, N, xfin_stats, xfin_gamma, xfin_beta,
+                  xfin_count, xfin_eps), stream()), "sep_fwd");
+}
+
 DwParams dwp(int B, int H, int W, int C) {
   DwParams p{};
   p.B = B; p.H = H; p.W = W; p.C = C;
@@ -345,8 +360,7 @@ void dw_wgrad_batch_op(py::list calls) {
 }
 
 void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bias, at::Tensor y, OptT stats, int B,
-                  int S, int Cout, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
-                  double fin_eps) {
+                  int S, int Cout) {
   EntryParams p{};
   p.images = ptr<const uint8_t>(images, "images");
   p.idx = ptr<const int32_t>(idx, "idx");
@@ -356,7 +370,6 @@ void entry_fwd_op(at::Tensor images, at::Tensor idx, at::Tensor w, at::Tensor bi
   p.stats = optr<float>(stats, "stats");
   p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
   TORCH_CHECK(idx.numel() == B && y.numel() == (int64_t)B * p.Ho * p.Wo * Cout && w.numel() == 27 * Cout, "entry_fwd sizes");
-  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, Cout, p.stats != nullptr);
   ok(entry_fwd(p, stream()), "entry_fwd");
 }
 
@@ -701,8 +714,7 @@ void resize_batch_op(at::Tensor src, at::Tensor offs, at::Tensor dims, at::Tenso
 
 void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor amax, OptT bias, at::Tensor y,
                     OptT stats, OptT ab, int relu, int B, int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N,
-                    OptT ws, OptT fin_ab, OptT fin_gamma, OptT fin_beta, OptT fin_ctr, double fin_count,
-                    double fin_eps) {
+                    OptT ws) {
   Conv8Params q{};
   ConvParams& p = q.c;
   p.x = ptr<const bf16_t>(x, "x");
@@ -723,7 +735,6 @@ void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor 
   TORCH_CHECK(wt8.numel() >= (int64_t)N * p.K && wscale.numel() >= N && amax.numel() >= 2, "conv3x3_fp8: w sizes");
   TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv3x3_fp8: y size");
   TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv3x3_fp8: stats size");
-  p.fin = fin_args(fin_ab, fin_gamma, fin_beta, fin_ctr, fin_count, fin_eps, N, p.stats != nullptr);
   const int rc = conv3x3_fp8(q, stream());
   TORCH_CHECK(rc <= 0, "conv3x3_fp8 failed (code ", rc, ")");
   if (rc < 0) ok(splitk_epilogue(p, -rc, stream()), "conv3x3_fp8 split-K epilogue");
@@ -757,8 +768,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_ab") = py::none(), py::arg("node_sums") = py::none(), py::arg("node_reps") = 1,
         py::arg("node_relu") = 1, py::arg("join_mode") = 0, py::arg("join_y") = py::none(),
         py::arg("join_ab") = py::none(), py::arg("join_out") = py::none(), py::arg("join_argmax") = py::none(),
-        py::arg("join_H") = 0, py::arg("join_W") = 0, py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
-        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3,
+        py::arg("join_H") = 0, py::arg("join_W") = 0,
         py::arg("bwd_y") = py::none(), py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(),
         py::arg("bwd_reps") = 1, py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(),
         py::arg("bwd_dbeta") = py::none(), py::arg("pj_v") = py::none(), py::arg("pj_add") = py::none(),
@@ -784,6 +794,14 @@ PYBIND11_MODULE(_C, m) {
   m.attr("GF_SUM") = (int)GF_SUM;
   m.attr("TUNE_WGRAD3_BLOCKS") = (int)TUNE_WGRAD3_BLOCKS;
   m.attr("TUNE_WGRAD3_MINTILES") = (int)TUNE_WGRAD3_MINTILES;
+  m.def("sep_fwd_supported", &sep_fwd_supported_op, py::arg("B"), py::arg("H"), py::arg("W"), py::arg("K"),
+        py::arg("N"));
+  m.def("sep_fwd", &sep_fwd_op, py::arg("x"), py::arg("ab"), py::arg("relu"), py::arg("wdw"), py::arg("wpw"),
+        py::arg("bias"), py::arg("d"), py::arg("y"), py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"),
+        py::arg("K"), py::arg("N"), py::arg("xfin_stats") = py::none(), py::arg("xfin_gamma") = py::none(),
+        py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3);
+  m.attr("TUNE_SEP") = (int)TUNE_SEP;
+  m.attr("TUNE_SEP_BLOCKS") = (int)TUNE_SEP_BLOCKS;
   m.def("dw_fwd", &dw_fwd_op, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("ab"), py::arg("relu"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("C"), py::arg("algo") = 0, py::arg("xfin_stats") = py::none(),
         py::arg("xfin_gamma") = py::none(), py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0,
@@ -801,8 +819,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("node_relu") = 1,
         py::arg("add_half") = py::none(), py::arg("mask_x") = 0);
   m.def("entry_fwd", &entry_fwd_op, py::arg("images"), py::arg("idx"), py::arg("w"), py::arg("bias"), py::arg("y"),
-        py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
-        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
+        py::arg("stats"), py::arg("B"), py::arg("S"), py::arg("Cout"));
   m.def("entry_wgrad", &entry_wgrad_op, py::arg("images"), py::arg("idx"), py::arg("dy"), py::arg("dw"), py::arg("B"),
         py::arg("S"), py::arg("Cout"), py::arg("replicas") = 1, py::arg("bwd_y") = py::none(),
         py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(), py::arg("bwd_reps") = 1,
@@ -843,6 +860,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_NODE_POOL_IPT") = (int)TUNE_NODE_POOL_IPT;
   m.attr("TUNE_WGRAD3_MINTILES32") = (int)TUNE_WGRAD3_MINTILES32;
   m.attr("TUNE_WGRAD_MIX") = (int)TUNE_WGRAD_MIX;
+  m.attr("TUNE_CONV3_SPLIT_BLOCKS") = (int)TUNE_CONV3_SPLIT_BLOCKS;
+  m.attr("TUNE_CONV3_SPLIT_TARGET") = (int)TUNE_CONV3_SPLIT_TARGET;
   m.def("bn_finalize", &bn_finalize_op);
   m.def("make_bn_moving_table", &make_bn_moving_table);
   m.def("bn_moving_update", &bn_moving_update_op);
@@ -871,8 +890,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv3x3_fp8", &conv3x3_fp8_op, py::arg("x"), py::arg("wt8"), py::arg("wscale"), py::arg("amax"),
         py::arg("bias"), py::arg("y"), py::arg("stats"), py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"),
         py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"),
-        py::arg("ws") = py::none(), py::arg("fin_ab") = py::none(), py::arg("fin_gamma") = py::none(), py::arg("fin_beta") = py::none(),
-        py::arg("fin_ctr") = py::none(), py::arg("fin_count") = 0.0, py::arg("fin_eps") = 1e-3);
+        py::arg("ws") = py::none());
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
         py::arg("max_elems"), py::arg("step") = py::none(), py::arg("cursor") = py::none());
   m.def("render_cracks", &render_cracks_op);

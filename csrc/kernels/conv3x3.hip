@@ -33,14 +33,12 @@ __device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r
 // WB ("whole-chunk B"): the block stages all 9 taps' weight tiles of a chunk at once ([tap][n][LDB], single LDS
 // buffer, next chunk register-prefetched during the current chunk's 9 x FMxFN MFMAs): two barriers per CHUNK
 // instead of one per tap, and no per-tap global-load latency on the critical path. Used for BN <= 64.
-// BWD (WB only): the halo is the BN-backward apply of (x = g, p.bwd.y) (common.h BnBwdIn), loaded raw and applied
-// after the previous chunk's MFMAs; the N-block-0 blocks store the tile's interior dx (each input pixel once).
 // PJ: the decoder node join epilogue (launch.h PoolJoinEpi) - its own instantiation, so the registers of its
 // prefetched operands never cost the plain convs occupancy.
 // XFIN: consumer-side BN finalize of the input transform (p.xfin): every block turns the producer's replica sums
 // into the Cin channels' (a, b) in LDS (its loads in flight with the first chunk's); the first block writes the ab
 // rows for the layer's later consumers.
-template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool BWD = false, bool PJ = false, bool XFIN = false>
+template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool PJ = false, bool XFIN = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
@@ -56,9 +54,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SH + SB];
   __shared__ float sred[2][4][BN_];
-  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];
   __shared__ float sxab[XFIN ? 2 * 256 : 1];            // consumer-side finalize: (a, b) of every input channel
-  static_assert(!BWD || WB, "folded BN backward: whole-chunk path only");
   bf16_t* sH = smem;              // [2][HP][LDH]
   bf16_t* sB = smem + SH;         // [2][BN_][LDB]
 
@@ -86,7 +82,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   // The halo is loaded RAW (rh) and the producer's BN-apply + ReLU applied only right before it is written to LDS,
   // after the current chunk's MFMAs: a transform right after the load made every chunk wait for its own prefetch
   // first (tools/conv3_probe.py at 256^2 / B16: the transformed convs ran 1.1-5.4 us slower than untransformed ones).
-  uint4 rh[H_PER_T], ryh[BWD ? H_PER_T : 1];
+  uint4 rh[H_PER_T];
   uint32_t hvalid = 0;                                  // bit i = piece i inside the image
   float ha[8], hb[8];                                   // producer coefficients of the loaded chunk (quarter tid & 3)
   auto load_coefs = [&](int chunk) {
@@ -110,7 +106,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0), yv = v;
+      uint4 v = make_uint4(0, 0, 0, 0);
       if (e < HALO_CHUNKS) {
         const int hp = e >> 2, q = e & 3;
         const int hy = hp / HW, hx = hp - hy * HW;
@@ -119,19 +115,16 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
           const int c = cbase + q * 8;
           v = *reinterpret_cast<const uint4*>(
               p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + c);
-          if constexpr (BWD)
-            yv = *reinterpret_cast<const uint4*>(p.bwd.y + (((size_t)b * p.Hin + iy) * p.Win + ix) * p.Cin + c);
           hv |= 1u << i;
         }
       }
       rh[i] = v;
-      if constexpr (BWD) ryh[i] = yv;
     }
     hvalid = hv;
   };
   // producer BN-apply + ReLU of the raw halo in rh; padding stays exactly 0 (it is outside the transform)
   auto xform_halo = [&]() {
-    if (BWD || !(has_ab || relu)) return;
+    if (!(has_ab || relu)) return;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       if (!((hvalid >> i) & 1u)) continue;
@@ -143,21 +136,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
         if (relu) f[j] = fmaxf(f[j], 0.f);
       }
       rh[i] = pack8(f);
-    }
-  };
-  // BWD: dx of the raw halo of `chunk` in place (+ the interior's side store)
-  auto bwd_halo = [&](int chunk) {
-    const bool side = bn_idx == 0 && p.bwd.dx != nullptr;
-    const int c = chunk * BK + (tid & 3) * 8;
-#pragma unroll
-    for (int i = 0; i < H_PER_T; ++i) {
-      if (!((hvalid >> i) & 1u)) continue;
-      const int e = tid + i * NT, hp = e >> 2;
-      const int hy = hp / HW, hx = hp - hy * HW;
-      rh[i] = bnb_apply8(rh[i], ryh[i], sco, p.Cin, c);
-      if (side && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW)
-        *reinterpret_cast<uint4*>(p.bwd.dx + (((size_t)b * p.Hin + ty0 + hy - 1) * p.Win + tx0 + hx - 1) * p.Cin +
-                                  c) = rh[i];
     }
   };
   auto store_halo = [&](int buf) {
@@ -272,10 +250,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       __syncthreads();
       load_coefs(ch0);
     }
-    if constexpr (BWD) {          // the first chunk's loads are in flight during the replica reduction
-      bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
-      if (ch0 < ch1) bwd_halo(ch0);
-    }
     if (ch0 < ch1) {
       xform_halo();
       store_halo(0);
@@ -307,7 +281,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
       __syncthreads();
       if (next_chunk) {
-        if constexpr (BWD) bwd_halo(ch + 1);
         xform_halo();
         store_halo(0);
         store_bw();
@@ -460,7 +433,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
-    if (!node && !pj) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -474,8 +446,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 // only when it is written to LDS (after the MFMAs), so the loads are never waited for early. BN statistics /
 // BN-node sums accumulate in registers across the block's tiles: one set of channel atomics per block.
 // LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
-template <int TH, int TW, int CH, bool BWD = false, bool PJ = false, bool XFIN = false>
-__global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
+template <int TH, int TW, int CH, bool PJ = false, bool XFIN = false>
+__global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
   constexpr int BN_ = 32, WM = 4;
   constexpr int BM = TH * TW;
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
@@ -489,7 +461,6 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SW + SH + BM * LDC];
   __shared__ float sred[2][4][BN_];
-  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];   // BN-backward coefficients (BWD: see conv3x3_kernel)
   bf16_t* sB = smem;                 // [CH][9][BN_][32]
   bf16_t* sH = smem + SW;            // [CH][HP][32]
   bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem + SW + SH);
@@ -551,15 +522,11 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
     tx0 = (t % tiles_w) * TW;
   };
   // raw halo of a tile into registers (no use of the values here: the loads stay in flight)
-  uint4 rh[CH][H_PER_T], ry[BWD ? CH : 1][BWD ? H_PER_T : 1];
+  uint4 rh[CH][H_PER_T];
   uint32_t rvalid = 0;                                  // bit i: piece i lies inside the image
-  int hb = 0, hty0 = 0, htx0 = 0;                       // tile of the halo in rh (BWD side store)
   auto load_halo = [&](int item) {
     int b, ty0, tx0;
     tile_of(item, b, ty0, tx0);
-    hb = b;
-    hty0 = ty0;
-    htx0 = tx0;
     rvalid = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
@@ -572,13 +539,9 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
       const bf16_t* src = p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + q * 8;
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
-        uint4 v = make_uint4(0, 0, 0, 0), yv = v;
-        if (ok) {
-          v = *reinterpret_cast<const uint4*>(src + ch * BK);
-          if constexpr (BWD) yv = *reinterpret_cast<const uint4*>(p.bwd.y + (src - p.x) + ch * BK);
-        }
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok) v = *reinterpret_cast<const uint4*>(src + ch * BK);
         rh[ch][i] = v;
-        if constexpr (BWD) ry[ch][i] = yv;
       }
     }
   };
@@ -589,19 +552,10 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
       const int e = tid + i * NT;
       if (e >= HALO_CHUNKS) continue;
       const bool ok = (rvalid >> i) & 1u;
-      const int hp = e >> 2, hy = hp / HW, hx = hp - hy * HW;
-      const bool side = BWD && ok && nBlock == 0 && p.bwd.dx != nullptr && hy >= 1 && hy <= TH && hx >= 1 &&
-                        hx <= TW;
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
         uint4 v = rh[ch][i];
-        if constexpr (BWD) {
-          const int c = ch * BK + (e & 3) * 8;
-          v = ok ? bnb_apply8(v, ry[ch][i], sco, p.Cin, c) : make_uint4(0, 0, 0, 0);
-          if (side)
-            *reinterpret_cast<uint4*>(p.bwd.dx + (((size_t)hb * p.Hin + hty0 + hy - 1) * p.Win + htx0 + hx - 1) *
-                                      p.Cin + c) = v;
-        } else if (has_ab || relu) {
+        if (has_ab || relu) {
           float f[8];
           unpack8(v, f);
           if (has_ab) {
@@ -643,7 +597,6 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
 
   int item = blockIdx.x;
   if (item < n_items) load_halo(item);
-  if constexpr (BWD) bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, blockIdx.x == 0);
   if (item < n_items) store_halo();
   __syncthreads();
   for (; item < n_items; item += gridDim.x) {
@@ -756,7 +709,6 @@ __global__ __launch_bounds__(NT, CH == 1 && !BWD && !PJ ? 3 : 2) void conv3x3_ws
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
-    if (!node && !pj) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -782,10 +734,8 @@ void launch_ws(const ConvParams& p, hipStream_t st) {
   grid = grid / nb * nb;
   if (grid < nb) grid = nb;
   if (grid > items) grid = items;
-  if (p.xfin.stats) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
-  else if (p.pj.v && p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true, true>), dim3(grid), dim3(NT), 0, st, p, items);
-  else if (p.pj.v) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
-  else if (p.bwd.y) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  if (p.xfin.stats) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, false, true>), dim3(grid), dim3(NT), 0, st, p, items);
+  else if (p.pj.v) hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH, true>), dim3(grid), dim3(NT), 0, st, p, items);
   else hipLaunchKernelGGL((conv3x3_ws_kernel<TH, TW, CH>), dim3(grid), dim3(NT), 0, st, p, items);
 }
 
@@ -798,22 +748,13 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
   dim3 grid(tiles, p.N / BN_, splits);
   if constexpr (WB) {
     if (p.xfin.stats) {
-      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, false, false, true>), grid, dim3(NT), 0, st, p,
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, false, true>), grid, dim3(NT), 0, st, p,
                          per, splits > 1 ? p.ws : nullptr);
       return splits;
     }
-    if (p.pj.v && p.bwd.y) {
-      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
-      return 1;
-    }
     if (p.pj.v) {
-      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, false, true>), grid, dim3(NT), 0, st, p, per, nullptr);
+      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
       return 1;
-    }
-    if (p.bwd.y) {
-      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per,
-                         splits > 1 ? p.ws : nullptr);
-      return splits;
     }
   }
   hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, WB>), grid, dim3(NT), 0, st, p, per,
@@ -855,7 +796,7 @@ static bool small_tiles(const ConvParams& p) {
 
 bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_splits(const ConvParams& p) {
-  return small_tiles(p) || ws_eligible(p) || (conv3x3_deep_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y)
+  return small_tiles(p) || ws_eligible(p) || conv3x3_deep_eligible(p)
              ? 1 : conv3x3_split_k(p);
 }
 
@@ -866,8 +807,10 @@ int conv3x3_split_k(const ConvParams& p) {
   const int bn = use_wb(p) ? wb_bn(p) : (p.N >= 128 ? 128 : p.N);
   const int blocks = ((p.Ho + th - 1) / th) * ((p.Wo + tw - 1) / tw) * p.B * (p.N / bn);
   const int chunks = p.Cin / BK;
-  if (blocks >= 192 || chunks < 2) return 1;
-  int s = (384 + blocks - 1) / blocks;
+  const int below = cfl_tune(TUNE_CONV3_SPLIT_BLOCKS) > 0 ? cfl_tune(TUNE_CONV3_SPLIT_BLOCKS) : 192;
+  const int target = cfl_tune(TUNE_CONV3_SPLIT_TARGET) > 0 ? cfl_tune(TUNE_CONV3_SPLIT_TARGET) : 384;
+  if (blocks >= below || chunks < 2) return 1;
+  int s = (target + blocks - 1) / blocks;
   if (s > chunks) s = chunks;
   const int per = (chunks + s - 1) / s;
   return (chunks + per - 1) / per;
@@ -881,13 +824,10 @@ bool conv3x3_supported(const ConvParams& p) {
 bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_deep(const ConvParams& p, hipStream_t st);
 
-bool conv3x3_bwd_foldable(const ConvParams& p) {
-  return conv3x3_supported(p) && !p.up_in && (ws_eligible(p) || use_wb(p));
-}
-
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
-  if (p.xfin.stats && (p.bwd.y || p.pj.v || p.xf.C > 256 || !(ws_eligible(p) || use_wb(p)))) {
+  if (p.bwd.y) return 6;                    // the BN-backward operand is applied by a separate pass (conv_igemm)
+  if (p.xfin.stats && (p.pj.v || p.xf.C > 256 || !(ws_eligible(p) || use_wb(p)))) {
     // a kernel without the consumer-side finalize: finalize first, then the plain call
     const int rc = bn_finalize(p.xfin.stats, p.xfin.gamma, p.xfin.beta, nullptr, nullptr, const_cast<float*>(p.xf.ab),
                                p.Cin, p.xfin.count, p.xfin.eps, 1, st);
@@ -896,9 +836,8 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
     q.xfin = BnStatsIn{};
     return conv3x3(q, st);
   }
-  // LDS-DMA ring, no split-K (it has no in-launch BN-finalize tail: a BnFinal request keeps the other kernels)
-  // (the folded BN backward, p.bwd, runs on the whole-chunk / weight-stationary kernels: conv3x3_bwd_foldable)
-  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && p.fin.gamma == nullptr && !p.bwd.y && !p.pj.v)
+  // LDS-DMA ring, no split-K
+  if (conv3x3_deep_eligible(p) && !ws_eligible(p) && !p.pj.v)
     return conv3x3_deep(p, st);
   if (ws_eligible(p)) {                     // weight-stationary persistent tiles (no split-K)
     const bool w16 = p.Wo >= 16;

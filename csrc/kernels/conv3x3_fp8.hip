@@ -285,7 +285,6 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_fp8_kernel(Conv8Params p, int c
       const int st = e / BN_, cc = e - st * BN_;
       atomicAdd(&rep[st * c.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
     }
-    bn_final_tail(c.fin, c.stats, c.N, gridDim.x * gridDim.y * gridDim.z);   // (split-K launches returned above)
   }
 }
 

@@ -70,7 +70,9 @@ void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits
   // >= 16 pixel tiles per block: the engine launches the decoder's halo wgrads grouped (conv3x3_wgrad_grouped), so
   // long blocks still fill the chip, and every pixel split is one plain-stored slab row that grad_finish must read
   // (whole-step A/B on one MI355X: 4 / 8 / 16 / 24 / 32 -> 1.733 / 1.706 / 1.691 / 1.729 / 1.782 ms/iteration)
-  int min_tiles = cfl_tune(TUNE_WGRAD3_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_MINTILES) : 16;
+  // (mixed launch, round 3: 16 / 32 tiles -> 1.3718 / 1.3554 ms per iteration: fewer, longer blocks co-run with the
+  // other weight gradients and leave a third of the slab rows for grad_finish)
+  int min_tiles = cfl_tune(TUNE_WGRAD3_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_MINTILES) : 32;
   // the 32-wide output tiles (the N = 32 layers at 128^2: 1-2 channel blocks, so few blocks per pixel split): alone
   // in their group launch they took shorter blocks (4 tiles); in the mixed launch (conv_wgrad.hip wgrad_mix_kernel),
   // co-running with the other layers, longer blocks - a quarter of the slab rows for grad_finish - measured faster:

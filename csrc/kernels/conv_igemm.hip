@@ -104,9 +104,7 @@ CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv, const fl
   }
 }
 
-// BWD: the operand is the BN-backward apply of (x = g, p.bwd.y) (common.h BnBwdIn; 1x1 / stride 1 only, so every
-// A chunk is one input pixel and the N-block-0 blocks store each dx element exactly once).
-template <int BM_, int BN_, int WM, int WN, bool JN = false, bool BWD = false>
+template <int BM_, int BN_, int WM, int WN, bool JN = false>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_per_split, float* __restrict__ ws) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM_ / WM, TN = BN_ / WN;
@@ -120,7 +118,6 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
   __shared__ float sred[2][NT / 64][BN_];
-  __shared__ float sco[BWD ? 5 * BNB_MAX_C + NT : 1];   // BN-backward coefficients (bnb_prologue)
   bf16_t* sA = smem;                 // [2][BM_][32] swizzled
   bf16_t* sB = smem + SA;            // [2][BN_][32] swizzled
 
@@ -162,7 +159,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   // The next K-tile's operands are loaded RAW into registers (ra / rb) and only transformed (producer BN-apply +
   // ReLU) in store_tiles, after the current tile's MFMAs: nothing consumes the loads early, so they stay in flight
   // across the MFMAs (a transform right after the load made every K-step wait for its own loads first).
-  uint4 ra[A_PER_T], rb[B_PER_T], ry[BWD ? A_PER_T : 1];
+  uint4 ra[A_PER_T], rb[B_PER_T];
   uint32_t avalid = 0;                 // bit i: A chunk i lies inside the (padded) input
   int c_ld = 0;                        // channel of the chunks in ra (their BN coefficients)
   auto load_tiles = [&](int kt) {
@@ -175,7 +172,6 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
         const size_t off = ((size_t)a_off[i] + (size_t)(ih >> p.up_in) * p.Win + (iw >> p.up_in)) * p.Cin + c;
         v = *reinterpret_cast<const uint4*>(p.x + off);
-        if constexpr (BWD) ry[i] = *reinterpret_cast<const uint4*>(p.bwd.y + off);
         avalid |= 1u << i;
       }
       ra[i] = v;
@@ -202,17 +198,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   };
 
   auto store_tiles = [&](int buf) {
-    if constexpr (BWD) {
-      const bool side = blockIdx.y == 0 && p.bwd.dx != nullptr;
-#pragma unroll
-      for (int i = 0; i < A_PER_T; ++i) {
-        if ((avalid >> i) & 1u) {
-          ra[i] = bnb_apply8(ra[i], ry[i], sco, p.Cin, c_ld);
-          if (side)        // 1x1 / stride 1: input pixel == output pixel m
-            *reinterpret_cast<uint4*>(p.bwd.dx + (size_t)(mBlock + (tid >> 2) + i * 64) * p.Cin + c_ld) = ra[i];
-        }
-      }
-    } else if (has_ab || relu) {
+    if (has_ab || relu) {
       float ca[8], cb[8];
       load_f8_or(p.xf.ab + c_ld, has_ab, 1.f, ca);
       load_f8_or(p.xf.ab + p.xf.C + c_ld, has_ab, 0.f, cb);
@@ -270,8 +256,6 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
     }
   }
 
-  if constexpr (BWD)                   // the first tile's loads are in flight during the replica reduction
-    bnb_prologue<NT>(p.bwd, p.Cin, sco, sco + 5 * BNB_MAX_C, (blockIdx.x | blockIdx.y | blockIdx.z) == 0);
   if (kt0 < kt1) store_tiles(0);
   __syncthreads();
 
@@ -381,7 +365,6 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
       atomicAdd(&rep[st * p.N + nBlock + cc], v);
     }
-    if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -447,7 +430,6 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
     for (int w = 0; w < NT / 64; ++w) v += red[st][w][cc];
     atomicAdd(&rep[st * p.N + cc], v);
   }
-  if (!node) bn_final_tail(p.fin, p.stats, p.N, gridDim.x);
 }
 
 template <int BM_, int BN_, int WM, int WN>
@@ -455,10 +437,7 @@ void launch(const ConvParams& p, int splits, float* ws, hipStream_t st) {
   const int KT = p.K / BK;
   const int per = (KT + splits - 1) / splits;
   dim3 grid((p.M + BM_ - 1) / BM_, p.N / BN_, splits);
-  if (p.bwd.y)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN, false, true>), grid, dim3(NT), 0, st, p, per,
-                       splits > 1 ? ws : nullptr);
-  else if (p.join.mode)   // separate instantiation: the join epilogue's registers must not cost the plain convs occupancy
+  if (p.join.mode)   // separate instantiation: the join epilogue's registers must not cost the plain convs occupancy
     hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN, true>), grid, dim3(NT), 0, st, p, per, nullptr);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, WM, WN>), grid, dim3(NT), 0, st, p, per, splits > 1 ? ws : nullptr);
@@ -470,15 +449,10 @@ bool conv3x3_supported(const ConvParams& p);
 int conv3x3(const ConvParams& p, hipStream_t st);
 
 static bool use3x3(const ConvParams& p) { return p.algo != 1 && conv3x3_supported(p); }
-bool conv3x3_bwd_foldable(const ConvParams& p);
-
-// Can the kernel that serves p fold its BN-backward operand (p.bwd)? 1x1 / stride 1 generic tiles (default tile
-// configs) and the 3x3 halo kernels (conv3x3_bwd_foldable).
-static bool bwd_foldable(const ConvParams& p) {
-  if (use3x3(p)) return conv3x3_bwd_foldable(p);
-  return p.ks == 1 && p.stride == 1 && p.pad_t == 0 && p.pad_l == 0 && !p.up_in && p.Ho == p.Hin &&
-         p.Wo == p.Win && cfl_tune(TUNE_IGEMM_CFG) == 0;
-}
+// The BN-backward operand (p.bwd) is folded into the streaming 1x1 kernel's B-fragment load only (pw.hip BWD). Folds
+// into the latency-bound tile kernels (3x3 halo, generic igemm) measured slower than the streaming bn_bwd_apply
+// pass twice (profiles/README.md) and were removed; those shapes run unfolded.
+static bool bwd_foldable(const ConvParams& p) { return !use3x3(p) && pw_conv_supported(p); }
 
 // Unfolded form of a p.bwd request: bn_bwd_apply into bwd.dx, then the plain conv of dx (identical results).
 static int bwd_unfolded(ConvParams p, hipStream_t st) {

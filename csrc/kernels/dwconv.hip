@@ -160,213 +160,6 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) 
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// LDS halo-tile kernels (every C % 32 == 0 layer). A block owns a TH x 32 pixel tile (TH = 4 for CT = 64, 8 for 32) of one image and a CT-channel
-// slice (CT = 64, or 32 when C = 32). The (TH+2) x 34 input halo is staged in LDS once (16-byte loads, the
-// producer's BN-apply + ReLU applied on the way in; pixel pitch padded by 16 B so the strided strip reads spread
-// over the banks). Thread = (8-channel group, 4-pixel horizontal strip): per kernel row it reads the strip's 6
-// halo pixels once and applies all 3 horizontal taps from registers.
-//   MODE 0 fwd:   y  = dw(T(x), w)                MODE 1 dgrad: dx = dw(dy, flip(w))
-//   MODE 2 wgrad: dW[tap][c] += sum_p T(x)[p + tap][c] * dy[p][c]   (block partial -> one replica row, atomics)
-// Tiles are ordered XCD-aware (neighbouring tiles share halo rows through the XCD's L2).
-template <int CT, int MODE>
-__global__ __launch_bounds__(NT) void dw_tile_kernel(DwParams p, int replicas) {
-  constexpr int G = CT / 8;                 // channel groups
-  constexpr int P = NT / G;                 // pixel threads
-  constexpr int SL = 4, TW = 32, TH = P / (TW / SL);
-  constexpr int HWp = TW + 2, HHp = TH + 2;
-  constexpr int LDP = CT + 8;               // padded pixel pitch (bf16)
-  constexpr int HALO_CH = HHp * HWp * G;
-  __shared__ __attribute__((aligned(16))) bf16_t sH[HHp * HWp * LDP];
-
-  const int tid = threadIdx.x;
-  const int cg = tid % G, pt = tid / G;
-  const int sr = pt / (TW / SL), sc = (pt % (TW / SL)) * SL;     // strip row / first column in the tile
-  const int nslices = p.C / CT;
-  const int tiles_w = (p.W + TW - 1) / TW, tiles_h = (p.H + TH - 1) / TH;
-  int lin = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int cs = lin % nslices;
-  lin /= nslices;
-  const int tw = lin % tiles_w;
-  lin /= tiles_w;
-  const int th = lin % tiles_h;
-  const int b = lin / tiles_h;
-  const int y0 = th * TH, x0 = tw * TW, cbase = cs * CT;
-  const int c0 = cbase + cg * 8;
-
-  // ---- stage the halo (transform on load for x; dy is used raw) ----
-  const bool tx = MODE != 1;
-  const bool has_ab = tx && p.xf.ab != nullptr;
-  const int relu = tx ? p.xf.relu : 0;
-  const bf16_t* src = MODE == 1 ? p.dy : p.x;
-  // all of this thread's halo loads issue back to back (unconditional register staging), then transform + LDS
-  // writes; NT is a multiple of G, so the thread's channel group (and its BN coefficients) is fixed
-  constexpr int NIT = (HALO_CH + NT - 1) / NT;
-  const int q = tid % G;
-  float a8[8], b8[8];
-  load_f8_or(p.xf.ab + cbase + q * 8, has_ab, 1.f, a8);
-  load_f8_or(p.xf.ab + p.xf.C + cbase + q * 8, has_ab, 0.f, b8);
-  uint4 hv[NIT];
-  uint32_t okm = 0;
-#pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int e = tid + k * NT, hp = e / G;
-    const int hy = hp / HWp, hx = hp - hy * HWp;
-    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-    const bool ok = e < HALO_CH && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (ok) v = *reinterpret_cast<const uint4*>(src + (((size_t)b * p.H + iy) * p.W + ix) * p.C + cbase + q * 8);
-    hv[k] = v;
-    okm |= (uint32_t)ok << k;
-  }
-#pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int e = tid + k * NT;
-    if (e >= HALO_CH) break;
-    uint4 v = hv[k];
-    if ((has_ab || relu) && ((okm >> k) & 1u)) {              // padding stays zero (TF SAME pads the input)
-      float f[8];
-      unpack8(v, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f[j] = fmaf(a8[j], f[j], b8[j]);
-        if (relu) f[j] = fmaxf(f[j], 0.f);
-      }
-      v = pack8(f);
-    }
-    *reinterpret_cast<uint4*>(&sH[(e / G) * LDP + q * 8]) = v;
-  }
-  __syncthreads();
-
-  const int oy = y0 + sr;                                    // this thread's output row
-  const bool row_ok = oy < p.H;
-  if (MODE != 2) {
-    float wt[9][8];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) load_f8(p.w + (MODE == 1 ? 8 - t : t) * p.C + c0, wt[t]);
-    float acc[SL][8];
-#pragma unroll
-    for (int i = 0; i < SL; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const bf16_t* hrow = &sH[((sr + ky) * HWp + sc) * LDP + cg * 8];
-#pragma unroll
-      for (int cx = 0; cx < SL + 2; ++cx) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(hrow + cx * LDP), f);
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int o = cx - kx;
-          if (o < 0 || o >= SL) continue;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wt[ky * 3 + kx][j], acc[o][j]);
-        }
-      }
-    }
-    const bool node = MODE == 1 && p.node.y != nullptr;     // fused BN-node gradient epilogue (dgrad)
-    float s0[8], s1[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
-    if (row_ok) {
-      NodeCoef nk;
-      if (node) node_coef_load(p.node.ab, p.C, c0, nk);
-      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
-#pragma unroll
-      for (int i = 0; i < SL; ++i)
-        if (x0 + sc + i < p.W) {
-          uint4 v = pack8(acc[i]);
-          if (node) v = node_epi(v, p.node.y + off0 + (size_t)i * p.C, nk, p.node.relu, s0, s1);
-          *reinterpret_cast<uint4*>(p.y + off0 + (size_t)i * p.C) = v;
-        }
-    }
-    if (node) {                                              // block-reduce the BN sums, one atomic per channel
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        for (int o = G; o < 64; o <<= 1) {
-          s0[j] += __shfl_xor(s0[j], o, 64);
-          s1[j] += __shfl_xor(s1[j], o, 64);
-        }
-      __syncthreads();                                       // halo reads done: reuse it for the partials
-      float* red = reinterpret_cast<float*>(sH);             // [4 waves][2][CT]
-      const int lane = tid & 63, wid = tid >> 6;
-      if (lane < G) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          red[(wid * 2 + 0) * CT + cg * 8 + j] = s0[j];
-          red[(wid * 2 + 1) * CT + cg * 8 + j] = s1[j];
-        }
-      }
-      __syncthreads();
-      const int reps = p.node.reps > 1 ? p.node.reps : 1;
-      float* dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * p.C;
-      for (int e = tid; e < 2 * CT; e += NT) {
-        const int k = e / CT, c = e % CT;
-        const float v = red[(0 * 2 + k) * CT + c] + red[(1 * 2 + k) * CT + c] + red[(2 * 2 + k) * CT + c] +
-                        red[(3 * 2 + k) * CT + c];
-        atomicAdd(&dst[k * p.C + cbase + c], v);
-      }
-    }
-  } else {
-    float g[SL][8];
-#pragma unroll
-    for (int i = 0; i < SL; ++i) {
-      const bool ok = row_ok && x0 + sc + i < p.W;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) v = *reinterpret_cast<const uint4*>(p.dy + (((size_t)b * p.H + oy) * p.W + x0 + sc + i) * p.C + c0);
-      unpack8(v, g[i]);
-    }
-    float acc[9][8];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const bf16_t* hrow = &sH[((sr + ky) * HWp + sc) * LDP + cg * 8];
-#pragma unroll
-      for (int cx = 0; cx < SL + 2; ++cx) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(hrow + cx * LDP), f);
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int o = cx - kx;
-          if (o < 0 || o >= SL) continue;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[ky * 3 + kx][j] = fmaf(f[j], g[o][j], acc[ky * 3 + kx][j]);
-        }
-      }
-    }
-    // reduce over the block's pixel threads: lanes of one channel group (lane % G) within the wave, then waves
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = acc[t][j];
-        for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-        acc[t][j] = v;
-      }
-    __syncthreads();                                         // halo no longer needed: reuse it for the partials
-    float* red = reinterpret_cast<float*>(sH);               // [4 waves][9][CT]
-    const int lane = tid & 63, wid = tid >> 6;
-    if (lane < G) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) red[(wid * 9 + t) * CT + cg * 8 + j] = acc[t][j];
-    }
-    __syncthreads();
-    float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
-    for (int e = tid; e < 9 * CT; e += NT) {
-      const int t = e / CT, c = e % CT;
-      const float v = red[(0 * 9 + t) * CT + c] + red[(1 * 9 + t) * CT + c] + red[(2 * 9 + t) * CT + c] +
-                      red[(3 * 9 + t) * CT + c];
-      atomicAdd(&dst[t * p.C + cbase + c], v);
-    }
-  }
-}
-
 // ---- row-streaming variant (default) ----
 // A block owns a 32-pixel column strip x 32 channels x a segment of rows and walks down it 4 output rows per step.
 // Input rows live in an LDS ring of 10 rows: each input row is fetched once per segment (halo overhead
@@ -949,16 +742,6 @@ int launch_stream(const DwParams& p, int replicas, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-template <int MODE>
-int launch_tile(const DwParams& p, int replicas, hipStream_t st) {
-  const int ct = p.C % 64 == 0 ? 64 : 32;
-  const int th = (NT / (ct / 8)) / (32 / 4);           // = TH of dw_tile_kernel (SL = 4, TW = 32)
-  const int tiles = p.B * ((p.H + th - 1) / th) * ((p.W + 31) / 32) * (p.C / ct);
-  if (ct == 64) hipLaunchKernelGGL((dw_tile_kernel<64, MODE>), dim3(tiles), dim3(NT), 0, st, p, replicas);
-  else hipLaunchKernelGGL((dw_tile_kernel<32, MODE>), dim3(tiles), dim3(NT), 0, st, p, replicas);
-  return hipGetLastError() == hipSuccess ? 0 : 3;
-}
-
 bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
 int launch_dw(const bf16_t* x, const float* w, bf16_t* y, InXform xf, int B, int H, int W, int C, int flip,
@@ -972,8 +755,8 @@ int launch_dw(const bf16_t* x, const float* w, bf16_t* y, InXform xf, int B, int
 
 }  // namespace
 
-static bool tiled(const DwParams& p) { return p.C % 32 == 0 && p.algo != 1; }
-static bool streamed(const DwParams& p) { return tiled(p) && p.algo != 2; }
+// algo 0 (default): the row-streaming LDS-ring kernels for C % 32 == 0; 1 (or other C): the generic strip kernels
+static bool streamed(const DwParams& p) { return p.C % 32 == 0 && p.algo != 1; }
 
 int dw_fwd(const DwParams& p, hipStream_t st) {
   if (streamed(p)) return launch_stream<0>(p, 1, st);
@@ -985,14 +768,12 @@ int dw_fwd(const DwParams& p, hipStream_t st) {
     q.xfin = BnStatsIn{};
     return dw_fwd(q, st);
   }
-  if (tiled(p)) return launch_tile<0>(p, 1, st);
   return launch_dw(p.x, p.w, p.y, p.xf, p.B, p.H, p.W, p.C, 0, st);
 }
 
 int dw_dgrad(const DwParams& p, hipStream_t st) {
   if (streamed(p)) return launch_stream<1>(p, 1, st);
-  if (tiled(p)) return launch_tile<1>(p, 1, st);
-  if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the halo-tile path only
+  if (p.node.y) return 2;                        // the fused BN-node epilogue exists on the streaming path only
   return launch_dw(p.dy, p.w, p.y, InXform{nullptr, p.C, 0}, p.B, p.H, p.W, p.C, 1, st);
 }
 
@@ -1044,7 +825,6 @@ int dw_wgrad_batch(const DwParams* ps, int n, hipStream_t st) {
 
 int dw_wgrad(const DwParams& p, hipStream_t st) {
   if (streamed(p)) return launch_stream<2>(p, p.replicas > 1 ? p.replicas : 1, st);
-  if (tiled(p)) return launch_tile<2>(p, p.replicas > 1 ? p.replicas : 1, st);
   if (p.C % 8 || p.C > 256 || !pow2(p.C / 8)) return 1;
   const int sw = (p.W % 4 == 0) ? 4 : 1;
   const int64_t items = (int64_t)p.B * p.H * (p.W / sw) * (p.C / 8);

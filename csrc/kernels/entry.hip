@@ -79,7 +79,6 @@ __global__ __launch_bounds__(NT) void entry_fwd_kernel(EntryParams p) {
   }
   if (p.stats) {
     block_channel_atomics<2>(s, G, p.Cout, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.Cout, red);
-    bn_final_tail(p.fin, p.stats, p.Cout, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 
@@ -278,7 +277,6 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
   }
   if (p.stats) {
     block_channel_atomics<2>(s, 4, 32, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 64, red);
-    bn_final_tail(p.fin, p.stats, 32, gridDim.x * gridDim.y * gridDim.z);
   }
 }
 

@@ -13,21 +13,6 @@
 // replicas measured 1.548 vs 1.521 ms for 8.
 #define STAT_REPLICAS 8
 
-// In-launch BatchNorm finalize ("last workgroup done"): the producer of a BN layer's batch statistics turns them into
-// the layer's (a, b, mean, rstd) rows itself instead of a separate 1-block bn_finalize launch (15 per step). Every
-// block adds its statistics with agent-scope float atomics (executed memory-side, never cached in an XCD's L2),
-// waits for them (vmcnt 0), then one lane draws a ticket from `counter`; the block that draws the last ticket reads
-// the replica rows with sc1 loads (L1 bypass) and writes ab (cdna_hip_programming.md §6 Guideline 16: counter form
-// with write-through payload). The last block re-zeroes the counter (the engine also zeroes it every step).
-struct BnFinal {
-  const float* gamma;      // nullptr = off
-  const float* beta;
-  float* ab;               // [4][C]
-  unsigned* counter;
-  float count;             // pixels per channel
-  float eps;
-};
-
 // Consumer-side BatchNorm finalize: the first kernel that applies a BN layer computes the layer's coefficients
 // itself from the producer's replica sums (no separate 1-block bn_finalize launch in between); the blocks that own a
 // channel range also write that range's ab rows (a, b, mean, rstd) for the later consumers of the layer.
@@ -124,7 +109,6 @@ struct ConvParams {
   PoolJoinEpi pj;      // optional decoder node join (3x3 s1 dgrads, even tiles); excludes stats / bias / node / split
   BnStatsIn xfin;      // optional consumer-side finalize of xf's BN (xf.ab computed here from the sums, rows written)
   ConvJoin join;       // optional residual join (forward 1x1 residual convs); excludes stats / node / split-K
-  BnFinal fin;         // optional in-launch finalize of `stats` (run by the launch that completes them)
   BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;
                        // common.h). Data-gradient convs only: 1x1/s1 or 3x3/s1, no upsample, no xf; shapes a kernel
                        // does not fold fall back to bn_bwd_apply into bwd.dx + the plain conv (same results)
@@ -179,6 +163,24 @@ int conv_wgrad_slabs(const WgradParams& p);
 bool conv_wgrad_plain_slabs(const WgradParams& p);   // slab rows are plain-stored (else atomic replica rows)
 #define WGRAD_REPLICAS 16
 
+// ---------------------------------------------------------------- fused SeparableConv forward (sepconv.hip)
+// y = pointwise(depthwise3x3(T(x))) + bias with the BN statistics of y; d = the depthwise output (side-stored for the
+// pointwise weight gradient). T = xf (BN-apply + ReLU; xfin: computed here from the producer's replica sums).
+struct SepParams {
+  const bf16_t* x;     // [B,H,W,K]
+  InXform xf;
+  BnStatsIn xfin;
+  const float* wdw;    // depthwise taps, Keras (3,3,K,1) = [tap][K]
+  const bf16_t* wpw;   // pointwise weights packed [N][K] (pack_weights PK_PW)
+  const float* bias;   // [N]
+  bf16_t* d;           // [B,H,W,K]
+  bf16_t* y;           // [B,H,W,N]
+  float* stats;        // [STAT_REPLICAS][2][N] or nullptr
+  int B, H, W, K, N;
+};
+bool sep_fwd_supported(const SepParams& p);
+int sep_fwd(const SepParams& p, hipStream_t st);
+
 // ---------------------------------------------------------------- depthwise 3x3 (dwconv.hip)
 struct DwParams {
   const bf16_t* x;     // [B,H,W,C] (transform applied on load)
@@ -218,7 +220,6 @@ struct EntryParams {
   float* dw;               // wgrad destination (3,3,3,Cout) fp32: [replicas][27*Cout]
   int B, S, Cout, Ho, Wo;
   int replicas;            // wgrad: >1 = spread block atomics over that many row copies (summed by grad_finish)
-  BnFinal fin;             // forward: in-launch finalize of `stats`
   BnBwdIn bwd;             // wgrad: dy is the gradient g w.r.t. the entry BN's output and the operand its BN-backward
                            // apply (common.h; y = the conv output, computed on load; dx stored only on the fallback)
 };
@@ -392,7 +393,7 @@ int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStrea
 enum TuneKey {
   TUNE_NODE_BWD_BLOCKS = 0, TUNE_DW_WGRAD_BLOCKS = 1, TUNE_ENTRY_WGRAD_BLOCKS = 2,
   TUNE_WGRAD3_BLOCKS = 3,      // halo wgrad: target grid size (default 512)
-  TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 16)
+  TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 32)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
   TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 512)
@@ -417,9 +418,13 @@ enum TuneKey {
   TUNE_PW_BLOCKS = 26,         // streaming 1x1 kernel: resident-grid cap (default 512 = 2 blocks per CU)
   TUNE_PW_DEPTH = 27,          // streaming 1x1 kernel: tiles in flight per wave (1 default, 2, 4 at K = 32)
   TUNE_NODE_POOL_IPT = 28,     // max-pool node gradient: 2x2 items per thread per trip (1 default, 2)
-  TUNE_WGRAD3_MINTILES32 = 29, // halo wgrad, 32-wide output tiles: min pixel tiles per block (default 4)
+  TUNE_WGRAD3_MINTILES32 = 29, // halo wgrad, 32-wide output tiles: min pixel tiles per block (default 16)
   TUNE_WGRAD_MIX = 30,         // conv_wgrad_batch: 0 = every deferred wgrad in ONE mixed launch, 1 = a launch per config
-  TUNE_N = 31
+  TUNE_CONV3_SPLIT_BLOCKS = 31, // conv3x3 8x16 tiles: split K when the grid has fewer blocks than this (default 192)
+  TUNE_CONV3_SPLIT_TARGET = 32, // ... into about this many blocks (default 384)
+  TUNE_SEP = 33,               // SeparableConv forward: 0 = fused depthwise + pointwise (sepconv.hip), 1 = two passes
+  TUNE_SEP_BLOCKS = 34,        // fused SeparableConv forward: target grid size (default 512)
+  TUNE_N = 35
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
@@ -435,58 +440,3 @@ int render_cracks(const float* segs, const float* params, uint8_t* images, uint8
 int resize_batch(const uint8_t* src, const int64_t* offs, const int* dims, uint8_t* dst, int n, int dh, int dw, int c,
                  int binarize, hipStream_t st);
 
-// Tail of a statistics producer (see BnFinal). EVERY thread of EVERY block of the launch calls it after issuing its
-// block's statistics atomics into stats[STAT_REPLICAS][2][C] (C <= 256, blockDim.x <= 256); `nblocks` = the
-// launch's grid size. The last block computes ab.
-__device__ __forceinline__ void bn_final_tail(const BnFinal& f, const float* stats, int C, int nblocks) {
-  __shared__ float spart[2 * 256];
-  __shared__ int sflag[1];
-  if (f.gamma == nullptr) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's atomics have completed
-  __syncthreads();                                          // ... and every other wave's
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(f.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *sflag = old == (unsigned)nblocks - 1;
-  }
-  __syncthreads();
-  if (!*sflag) return;
-  // thread -> (channel c, replica phase j): all of a channel's 2 * STAT_REPLICAS loads in one round
-  const int nt = blockDim.x, per = nt >= C ? nt / C : 1;
-  const int c = threadIdx.x % C, j = threadIdx.x / C;
-  float a = 0.f, b = 0.f;
-  if (j < per) {
-    float va[STAT_REPLICAS], vb[STAT_REPLICAS];
-#pragma unroll
-    for (int k = 0; k < STAT_REPLICAS; ++k) {
-      const int r = j + k * per;
-      va[k] = r < STAT_REPLICAS ? __hip_atomic_load(stats + (size_t)r * 2 * C + c, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-      vb[k] = r < STAT_REPLICAS ? __hip_atomic_load(stats + (size_t)r * 2 * C + C + c, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < STAT_REPLICAS; ++k) {
-      a += va[k];
-      b += vb[k];
-    }
-  }
-  spart[threadIdx.x] = a;
-  spart[nt + threadIdx.x] = b;
-  __syncthreads();
-  for (int cc = threadIdx.x; cc < C; cc += nt) {
-    float s = 0.f, s2 = 0.f;
-    for (int k = 0; k < per; ++k) {
-      s += spart[k * C + cc];
-      s2 += spart[nt + k * C + cc];
-    }
-    const float mean = s / f.count;
-    const float var = fmaxf(s2 / f.count - mean * mean, 0.f);
-    const float rstd = rsqrtf(var + f.eps);
-    const float sa = f.gamma[cc] * rstd;
-    f.ab[cc] = sa;
-    f.ab[C + cc] = f.beta[cc] - mean * sa;
-    f.ab[2 * C + cc] = mean;
-    f.ab[3 * C + cc] = rstd;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(f.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}

@@ -300,7 +300,7 @@ bool pw_conv_supported(const ConvParams& p) {
          p.xf.ab == nullptr && !p.xf.relu && p.node.y == nullptr && p.join.mode == JOIN_NONE &&
          (p.bwd.y == nullptr || (p.bwd.dx != nullptr && p.bwd.reps <= BNB_MAX_REPS)) &&
          (p.sum2x2 == nullptr || (p.bwd.y == nullptr && p.bias == nullptr && p.stats == nullptr)) && p.pj.v == nullptr &&
-         p.xfin.stats == nullptr && p.fin.gamma == nullptr && p.M > 0;
+         p.xfin.stats == nullptr && p.M > 0;
 }
 
 int pw_conv(const ConvParams& p, hipStream_t st) {

@@ -144,16 +144,76 @@ def test_conv_wgrad_1x1_and_up(stride, up):
 
 
 # algo 0 = row-streaming LDS ring (stream_blocks = grid target: 1 -> one segment per column strip, so a block walks
-# every row step of the image), 1 = row strips, 2 = independent halo tiles
+# every row step of the image), 1 = generic row strips
 @pytest.mark.parametrize("B,H,C,algo,stream_blocks", [(2, 10, 64, 0, 0), (2, 10, 64, 1, 0), (3, 37, 32, 0, 0),
-                                                      (2, 18, 128, 0, 0), (1, 9, 256, 0, 0), (3, 37, 32, 2, 0),
-                                                      (2, 18, 128, 2, 0), (2, 45, 64, 0, 1), (1, 70, 32, 0, 3)])
+                                                      (2, 18, 128, 0, 0), (1, 9, 256, 0, 0), (3, 37, 32, 1, 0),
+                                                      (2, 45, 64, 0, 1), (1, 70, 32, 0, 3)])
 def test_depthwise_fwd_dgrad_wgrad(B, H, C, algo, stream_blocks):
     hip().set_tune(hip().TUNE_DW_STREAM_BLOCKS, stream_blocks)
     try:
         _depthwise_case(B, H, C, algo)
     finally:
         hip().set_tune(hip().TUNE_DW_STREAM_BLOCKS, 0)
+
+
+@pytest.mark.parametrize("B,H,K,N,mode", [(2, 32, 32, 64, "ab"), (2, 64, 64, 64, "xfin"), (1, 32, 64, 128, "ab"),
+                                            (3, 32, 64, 128, "relu"), (2, 32, 64, 64, "eval")])
+def test_fused_sepconv_matches_dw_then_pw(B, H, K, N, mode):
+    """sepconv.hip (SeparableConv forward in one pass: the depthwise output formed in the pointwise MFMA's operand
+    registers): d and y bit-identical to dw_fwd + the streaming pointwise conv, BN statistics equal up to float
+    summation order, the consumer-side finalize writing the same ab rows; and y against the fp32 PyTorch
+    depthwise + pointwise of relu(BN(x))."""
+    torch.manual_seed(61)
+    C_ = hip()
+    assert C_.sep_fwd_supported(B, H, H, K, N)
+    xb, xf = bf(torch.randn(B, H, H, K))
+    wd = (torch.randn(3, 3, K, 1) * 0.2).reshape(-1).to(DEV)
+    wp = torch.randn(1, 1, K, N) * 0.1
+    wpb = pack(PK_PW, wp, 1, K, N)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    R_ = C_.STAT_REPLICAS
+    ab, a, b = ab_for(K, 62)
+    kw, xst = {}, None
+    if mode == "xfin":                         # input BN finalized by the consumer from producer replica sums
+        g = torch.Generator().manual_seed(63)
+        mean, var = torch.randn(K, generator=g) * 0.2, torch.rand(K, generator=g) + 0.5
+        cnt = float(B * H * H)
+        xst = torch.zeros(R_, 2, K)
+        xst[:, 0] = mean * cnt / R_
+        xst[:, 1] = (var + mean * mean) * cnt / R_
+        gam, bet = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1
+        kw = dict(xfin_stats=xst.reshape(-1).to(DEV), xfin_gamma=gam.to(DEV), xfin_beta=bet.to(DEV),
+                  xfin_count=cnt, xfin_eps=1e-3)
+    abd = None if mode == "relu" else ab.to(DEV)
+    outs = []
+    for fused in (True, False):
+        d = torch.zeros(B, H, H, K, dtype=torch.int16, device=DEV)
+        y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+        st = None if mode == "eval" else torch.zeros(R_ * 2 * N, device=DEV)
+        abx = abd.clone() if abd is not None else None
+        if fused:
+            C_.sep_fwd(xb, abx, 1, wd, wpb, bias, d, y, st, B, H, H, K, N, **kw)
+        else:
+            C_.dw_fwd(xb, wd, d, abx, 1, B, H, H, K, **kw)
+            C_.conv_igemm(d, wpb, bias, y, st, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0)
+        torch.cuda.synchronize()
+        outs.append((d.cpu(), y.cpu(), None if st is None else st.view(R_, 2, N).sum(0).cpu(),
+                     None if abx is None else abx.cpu()))
+    (d1, y1, s1, ab1), (d0, y0, s0, ab0) = outs
+    assert torch.equal(d1, d0) and torch.equal(y1, y0)
+    if s0 is not None:
+        assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-3)
+    if mode == "xfin":
+        assert torch.equal(ab1, ab0)
+        a, b = ab0[:K], ab0[K:2 * K]
+    t = xf if mode == "relu" else xf * a + b
+    t = t.relu().to(torch.bfloat16).float()
+    dref = F.conv2d(F.pad(t.permute(0, 3, 1, 2), (1, 1, 1, 1)), wd.cpu().view(3, 3, K, 1).permute(2, 3, 0, 1), None,
+                    groups=K)
+    yref = F.conv2d(dref.to(torch.bfloat16).float(), wp.to(torch.bfloat16).float().permute(3, 2, 0, 1),
+                    bias.cpu()).permute(0, 2, 3, 1)
+    assert rel(from_bits(d1), dref.permute(0, 2, 3, 1)) < 1e-2
+    assert rel(from_bits(y1), yref) < 1e-2
 
 
 def _depthwise_case(B, H, C, algo):
@@ -1156,48 +1216,6 @@ def test_fused_head_train_pass_matches_fwd_then_bwd(node):
                    1, fused=1)
 
 
-@pytest.mark.parametrize("ks,H,Cin,N,B,tune", [
-    (1, 32, 32, 64, 4, ""),          # generic implicit GEMM (pointwise conv)
-    (3, 16, 64, 32, 2, ""),          # per-tile conv3x3 kernel
-    (3, 16, 64, 32, 2, "ws"),        # weight-stationary persistent conv3x3 kernel
-    (3, 8, 256, 256, 4, "split"),    # split-K: the tail runs in the split-K epilogue launch
-])
-def test_in_launch_bn_finalize_matches_bn_finalize(ks, H, Cin, N, B, tune):
-    """launch.h BnFinal: the statistics producer's last block writes the BN coefficients (a, b, mean, rstd) exactly
-    as a separate bn_finalize launch over the same replica rows would, and re-arms its ticket counter (two calls)."""
-    torch.manual_seed(31)
-    C_ = hip()
-    xb, _ = bf(torch.randn(B, H, H, Cin))
-    wb = pack(PK_CONV, torch.randn(ks, ks, Cin, N) * 0.05, ks, Cin, N)
-    bias = (torch.randn(N) * 0.1).to(DEV)
-    gamma, beta = (torch.rand(N) + 0.5).to(DEV), (torch.randn(N) * 0.2).to(DEV)
-    mm, mv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
-    ctr = torch.zeros(1, dtype=torch.int32, device=DEV)
-    if tune == "ws":
-        C_.set_tune(C_.TUNE_CONV3_WS, 2)
-    if tune == "split":
-        C_.set_tune(C_.TUNE_CONV3_SMALL, 1)
-        C_.set_tune(C_.TUNE_CONV3_DEEP, 1)
-    try:
-        for _ in range(2):
-            y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
-            stats = torch.zeros(C_.STAT_REPLICAS * 2 * N, device=DEV)
-            ab_tail = torch.zeros(4 * N, device=DEV)
-            ws = torch.zeros(16 * B * H * H * N, device=DEV)
-            C_.conv_igemm(xb, wb, bias, y, stats, None, 0, B, H, H, Cin, 0, H, H, N, ks, 1, (ks - 1) // 2,
-                          (ks - 1) // 2, ws, 0, fin_ab=ab_tail, fin_gamma=gamma, fin_beta=beta, fin_ctr=ctr,
-                          fin_count=float(B * H * H), fin_eps=1e-3)
-            ab_ref = torch.zeros(4 * N, device=DEV)
-            C_.bn_finalize(stats, gamma, beta, mm, mv, ab_ref, N, float(B * H * H), 1e-3, 1)
-            torch.cuda.synchronize()
-            assert int(ctr.item()) == 0                                   # re-armed by the last block
-            assert torch.allclose(ab_tail, ab_ref, rtol=1e-5, atol=1e-6), (ab_tail - ab_ref).abs().max()
-    finally:
-        C_.set_tune(C_.TUNE_CONV3_WS, 0)
-        C_.set_tune(C_.TUNE_CONV3_SMALL, 0)
-        C_.set_tune(C_.TUNE_CONV3_DEEP, 0)
-
-
 def _first_layer_cos(g_a, g_b, table, names=("conv2d", "separable_conv2d", "conv2d_transpose_7", "conv2d_8")):
     out = {}
     for e in table.entries:
@@ -1380,21 +1398,19 @@ def test_folder_dataset_device_resize_matches_host(tmp_path):
     (1, 128, 128, 128, 4, None, False, False),       # 1x1: streaming kernel, 2 output slices, long persistent loop
     (1, 256, 128, 10, 3, None, False, False),        # 1x1: streaming kernel, K = 256, ragged last tile (M = 300)
     (1, 32, 64, 33, 2, None, False, False),          # 1x1: streaming kernel, K = 32, ragged rows
-    (1, 64, 32, 16, 2, "pw_off", False, False),      # 1x1 generic, 128x32 tiles
+    (1, 64, 32, 16, 2, "pw_off", False, False),      # unfolded fallback from here on: 1x1 generic, 128x32 tiles
     (1, 128, 128, 128, 4, "pw_off", False, False),   # 1x1 generic, 128x128 tiles (M >= 65536)
-    (1, 64, 64, 24, 2, "igemm_cfg", False, False),   # forced tile config: not folded -> bn_bwd_apply + conv
+    (1, 64, 64, 24, 2, "igemm_cfg", False, False),   # forced tile config
     (3, 64, 64, 16, 2, None, False, True),           # halo tile kernel (whole-chunk B) + BN-node epilogue
     (3, 64, 64, 16, 2, None, True, False),           # ... split over the 2 input chunks
-    (3, 128, 64, 12, 2, None, False, False),         # ragged 8x16 tiles (side store bounds)
     (3, 32, 32, 16, 2, "ws", False, True),           # weight-stationary kernel, CH 1
-    (3, 64, 128, 16, 2, "ws", False, False),         # weight-stationary kernel, CH 2, 4 column blocks
     (3, 256, 256, 8, 4, "small", False, True),       # 8x8-pixel tiles on the deep 16x16-level shape family
 ])
 def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
-    """BN-backward apply folded into the data-gradient conv's operand load (conv_igemm bwd=...): the conv output,
-    the side-stored dx and dgamma / dbeta equal bn_bwd_apply + the plain conv bit for bit on every kernel that folds
-    it (1x1 generic tiles, 3x3 halo / weight-stationary / small tiles, split-K) and on the unfolded fallback; dx also
-    vs the fp32 formula."""
+    """BN-backward apply requested with a data-gradient conv (conv_igemm bwd=...): folded into the streaming 1x1
+    kernel's operand load (pw.hip), or run as bn_bwd_apply + the plain conv on every other kernel (generic tiles, the
+    3x3 halo kernels - their folds measured slower and were removed): the conv output, the side-stored dx and
+    dgamma / dbeta equal the two-pass form bit for bit; dx also vs the fp32 formula."""
     torch.manual_seed(41)
     C_ = hip()
     keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "igemm_cfg": (C_.TUNE_IGEMM_CFG, 3),
@@ -1455,9 +1471,9 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_BNB_FOLD", "1"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_SUM2X2_FOLD", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_SEP_FUSE", "0"), ("CFL_HEAD_FUSE", "0"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_SUM2X2_FOLD", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
-    """Engine variants - BN-backward passes folded into the data-gradient convs (CFL_BNB_FOLD=1), weight gradients
+    """Engine variants - two-pass SeparableConv forward / head (CFL_SEP_FUSE=0, CFL_HEAD_FUSE=0), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
     of the statistics (a second default run bounds it)."""
     import os

@@ -121,7 +121,7 @@ def main():
             line = (f"{t:8.1f}  {floor:7.1f} {100 * floor / max(t, 1e-9):5.0f}%  {by / 1e6:8.2f} MB {by / t / 1e6:6.2f} "
                     f"TB/s  {fl / t / 1e6:7.1f} TF/s  {shape_key(name, a, k)}")
         if args.variants and name in ("conv_wgrad", "conv_igemm", "dw_fwd", "dw_dgrad", "dw_wgrad"):
-            for algo in ((1, 2, 0) if name.startswith("dw_") else (1, 0)):
+            for algo in (1, 0):
                 a2, kk = list(a), dict(k)
                 if name == "conv_wgrad":      # (..., dst_mode, m_chunk, algo, slabs): direct atomics variant
                     a2[-2], a2[-1] = algo, 0
