@@ -4,7 +4,8 @@
 // (pw.hip) reading it back.
 //
 // A block owns a TW-pixel column strip of one image and a segment of rows, and walks down it RS output rows per
-// step (4 waves, one 16-pixel tile each). The transformed input rows live in an LDS ring (row-streaming as in
+// step (4 waves, TPW 16-pixel tiles each: RS rows of input in flight per step - with one tile per wave and 2-row
+// steps the block held too few bytes in flight to cover HBM latency). The transformed input rows live in an LDS ring (row-streaming as in
 // dwconv.hip: each input row fetched once per segment, the next step's rows in flight in registers during the
 // current step's compute, one barrier per step). Per 16-pixel tile a lane (r16, q) forms the depthwise output of
 // pixel r16, channels s*32 + 8q .. +7 of every 32-channel k-step s - exactly the B-fragment layout of pw.hip's
@@ -29,14 +30,14 @@ CFL_DEVICE int wswz(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3);
 template <int K, int N, int TW>
 struct Sep {
   static constexpr int WT = TW / 16;                  // wave tiles per row
-  static constexpr int RS = 4 / WT;                   // output rows per step
+  static constexpr int TPW = N <= 64 ? 2 : 1;         // tiles per wave per step (N = 128: registers)
+  static constexpr int RS = 4 * TPW / WT;             // output rows per step
   static constexpr int NRING = 2 * RS + 2;            // rows read by a step + rows prefetched for the next
   static constexpr int HWp = TW + 2;                  // halo pixels per row
-  static constexpr int LDP = K + 8;                   // LDS pixel pitch (bf16): 16 B pad
   static constexpr int CQ = K / 8;                    // 16-byte channel pieces per pixel
   static constexpr int PIECES = HWp * CQ;             // per row
   static constexpr int KS = K / 32, NF = N / 16;
-  static constexpr int RING = NRING * HWp * LDP;      // bf16 elements
+  static constexpr int RING = NRING * HWp * K;        // bf16 elements
   static_assert(NT % CQ == 0, "a thread's pieces share one channel group");
 };
 
@@ -59,6 +60,14 @@ CFL_DEVICE void sep_fetch(const SepParams& p, const bf16_t* img, int x0, int row
     v[i] = t;
     okm |= (uint32_t)ok << i;
   }
+}
+
+// Ring layout: [row slot][32-channel plane][pixel][32 channels], 64 B per pixel per plane with conv3x3.hip's XOR
+// swizzle of the four 16-byte quarters (quarter q of pixel r at q ^ ((r >> 1) & 2)): a B-fragment read - 16
+// consecutive pixels x 4 quarters, any start pixel - then covers all 64 banks (a padded [pixel][K] row left 2-way
+// conflicts in the ds_read_b128 lane groups).
+CFL_DEVICE int sep_off(int slot_plane, int hwp, int px, int q) {
+  return (slot_plane * hwp + px) * 32 + ((q ^ ((px >> 1) & 2)) << 3);
 }
 
 // ... and into their ring slots, with the producer transform (padding stays zero: TF SAME pads the conv input)
@@ -85,7 +94,7 @@ CFL_DEVICE void sep_put(bf16_t* ring, const uint4 (&v)[(R * Sep<K, N, TW>::PIECE
       t = pack8(f);
     }
     const int slot = (row0 + r + S::NRING) % S::NRING;      // row0 >= -1
-    *reinterpret_cast<uint4*>(ring + (slot * S::HWp + px) * S::LDP + cq * 8) = t;
+    *reinterpret_cast<uint4*>(ring + sep_off(slot * S::KS + (cq >> 2), S::HWp, px, cq & 3)) = t;
   }
 }
 
@@ -159,14 +168,16 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
 #pragma unroll
     for (int r = 0; r < 4; ++r) s1[nf][r] = s2[nf][r] = 0.f;
 
-  const int wr = wid / S::WT, px0 = (wid % S::WT) * 16;     // this wave's row within the step and tile column
+  const int px0 = (wid % S::WT) * 16;                        // this wave's tile column
   uint4 vn[PPT];
   uint32_t okn = 0;
   for (int s = 0; s < nsteps; ++s) {
     const int a = ybeg + s * RS;
     const bool more = s + 1 < nsteps;
     sep_fetch<K, N, TW, RS>(p, img, x0, a + RS + 1, more, vn, okn);
-    const int oy = a + wr;
+#pragma unroll 1
+    for (int ti = 0; ti < S::TPW; ++ti) {
+    const int oy = a + (wid + 4 * ti) / S::WT;                 // tile wid + 4 ti of the step's RS x WT tiles
     if (oy < yend) {
       const int ox = x0 + px0 + r16;
       const size_t m = ((size_t)b * p.H + oy) * p.W + ox;
@@ -183,15 +194,16 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int slot = (oy - 1 + ky + S::NRING) % S::NRING;
-          const bf16_t* hrow = ring + (slot * S::HWp + px0 + r16) * S::LDP + c0;
+          const int sp = slot * KS + ks;
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
             float f[8], w[8];
-            unpack8(*reinterpret_cast<const uint4*>(hrow + kx * S::LDP), f);
+            unpack8(*reinterpret_cast<const uint4*>(ring + sep_off(sp, S::HWp, px0 + r16 + kx, q)), f);
             load_f8(&sWd[(ky * 3 + kx) * K + c0 + wo], w);
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[j] = fmaf(f[j], w[j], acc[j]);
           }
+          __builtin_amdgcn_sched_barrier(0);   // one input row's reads in flight at a time (register pressure)
         }
         const uint4 dv = pack8(acc);
         *reinterpret_cast<uint4*>(p.d + m * K + c0) = dv;           // the pointwise weight gradient's input
@@ -234,6 +246,7 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
         }
       }
     }
+    }
     if (more) sep_put<K, N, TW, RS>(ring, vn, okn, a + RS + 1, has_ab || relu, a8, b8, relu);
     __syncthreads();
   }
@@ -275,7 +288,8 @@ int launch(const SepParams& p, hipStream_t st) {
   using S = Sep<K, N, TW>;
   const int steps = (p.H + S::RS - 1) / S::RS;
   const int strips = p.B * (p.W / TW);
-  int target = cfl_tune(TUNE_SEP_BLOCKS) > 0 ? cfl_tune(TUNE_SEP_BLOCKS) : 512;   // one round at 2 blocks per CU
+  // one round of resident blocks: 3 per CU at K = 32 (155 VGPRs, 27 KB LDS), else 2 (LDS / VGPRs)
+  int target = cfl_tune(TUNE_SEP_BLOCKS) > 0 ? cfl_tune(TUNE_SEP_BLOCKS) : (K == 32 ? 768 : 512);
   int nseg = (target + strips - 1) / strips;
   nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
   const int seg_rows = ((steps + nseg - 1) / nseg) * S::RS;

@@ -20,7 +20,7 @@ from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine 
 from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  # noqa: E402
 
 SKIP = {"conv_splits", "conv_wgrad_slabs", "make_pack_table", "make_bn_moving_table", "make_grad_finish_table",
-        "make_zero_table", "adam_step_done"}
+        "make_zero_table", "adam_step_done", "sep_fwd_supported"}
 
 
 class Recorder:
