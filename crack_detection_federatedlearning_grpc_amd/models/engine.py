@@ -288,6 +288,7 @@ class UNetEngine:
         self.fuse_head = self.dice == 0 and os.environ.get("CFL_HEAD_FUSE", "1") != "0"
         # SeparableConv forward in one pass (sepconv.hip; CFL_SEP_FUSE=0: dw_fwd + pointwise conv)
         self.fuse_sep = os.environ.get("CFL_SEP_FUSE", "1") != "0"
+        self.eager_after_fedavg = os.environ.get("CFL_EAGER_AFTER_FEDAVG", "0") == "1"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         # per-step zeroing of gradients / statistics in one launch
@@ -815,9 +816,12 @@ class UNetEngine:
         self.graph = g
 
     def train_step(self, use_graph: bool = True) -> None:
-        """One training iteration. The first step after an overlapped FedAvg (``defer_until``) runs eagerly so
-        each layer waits only for the bucket holding its parameters (the early layers' kernels start while the
-        late buckets are still reducing); every other step replays the captured hipGraph."""
+        """One training iteration: a replay of the captured hipGraph. After an overlapped FedAvg (``defer_until``)
+        the stream first waits (device-side event waits, no host sync) for every bucket's reduce + repack, then
+        replays: the ~70 Python-issued launches of an eager step cost milliseconds, the wait at most the tail of an
+        8 MB all-reduce (CFL_EAGER_AFTER_FEDAVG=1: the eager first step that waits per layer instead)."""
+        if use_graph and self.graph is not None and self._pending and not self.eager_after_fedavg:
+            self._await_all()
         if use_graph and self.graph is not None and not self._pending:
             self.graph.replay()
         elif use_graph and self.graph is None:

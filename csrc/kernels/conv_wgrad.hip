@@ -318,6 +318,7 @@ struct MixItem {
 struct MixGroup {
   MixItem it[MIX_MAX];
   int n;
+  int xcd;                  // XCD-grouped block order (TUNE_WGRAD_MIX_XCD != 1)
 };
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int MIX_LDS = cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wgrad_lds_bytes<128, 128, 32>()),
@@ -327,13 +328,18 @@ static_assert(MIX_LDS <= 80 * 1024, "two mixed blocks per CU");
 
 __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[MIX_LDS];
+  // XCD grouping: within every 64 dispatch slots, each XCD runs 8 consecutive logical blocks - the (up to 8) input-
+  // channel blocks of one pixel split, which read the same dy tile, share an XCD's L2 and run at the same time (round-
+  // robin dispatch spread them over 8 L2s: FETCH_SIZE of the mixed launch ~850 MB per step)
+  const int base = blockIdx.x & ~63, span = imin(64, (int)gridDim.x - base);
+  const int vb = base + (g.xcd ? xcd_swizzle(blockIdx.x & 63, span) : (blockIdx.x & 63));
   int k = 0;
-  while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
+  while (k + 1 < g.n && g.it[k + 1].block0 <= vb) ++k;
   // the item is copied out of the argument block first (a reference into it, indexed by a runtime k, made the
   // compiler spill the whole 3 KB block to scratch)
   const WgradParams P = g.it[k].p;
   const int kind = g.it[k].kind, a = g.it[k].a, b = g.it[k].b, gx = g.it[k].gx, gy = g.it[k].gy;
-  const int local = blockIdx.x - g.it[k].block0;
+  const int local = vb - g.it[k].block0;
   const int bx = local % gx, r = local / gx, by = r % gy, bz = r / gy;
   switch (kind) {
     case 0: wg3::wgrad3_body<64, true>(P, a, b, bx, by, bz, smem); break;
@@ -375,6 +381,7 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
   int blocks = 0;
   auto flush = [&]() -> int {
     if (g.n == 0) return 0;
+    g.xcd = cfl_tune(TUNE_WGRAD_MIX_XCD) != 1;
     hipLaunchKernelGGL(wgrad_mix_kernel, dim3(blocks), dim3(NT), 0, st, g);
     g = MixGroup{};
     blocks = 0;

@@ -424,7 +424,8 @@ enum TuneKey {
   TUNE_CONV3_SPLIT_TARGET = 32, // ... into about this many blocks (default 384)
   TUNE_SEP = 33,               // SeparableConv forward: 0 = fused depthwise + pointwise (sepconv.hip), 1 = two passes
   TUNE_SEP_BLOCKS = 34,        // fused SeparableConv forward: target grid size (default 512)
-  TUNE_N = 35
+  TUNE_WGRAD_MIX_XCD = 35,     // mixed wgrad launch: 0 = XCD-grouped block order, 1 = dispatch order
+  TUNE_N = 36
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

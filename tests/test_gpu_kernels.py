@@ -1,4 +1,6 @@
 """HIP kernel numerics vs plain fp32 PyTorch references (run on an MI355X via gpurun; marked gpu)."""
+import json
+
 import numpy as np
 import pytest
 import torch
@@ -1226,78 +1228,59 @@ def _first_layer_cos(g_a, g_b, table, names=("conv2d", "separable_conv2d", "conv
 
 
 def test_training_parity_vs_plain_fp32():
-    """Training parity: the HIP engine (bf16 activations / gradients, fp32 master weights) and the
-    plain fp32 PyTorch oracle (RefTrainer: Keras semantics, fp32 everywhere, no bf16 emulation) trained from the SAME
-    init on the SAME batches, 128^2 / batch 16, 160 steps, then both evaluated on the same held-out images.
-    Tolerances are set against what bf16 itself costs: the same oracle under torch.autocast(bf16) is the yardstick
-    for the first step's per-layer gradient cosines (printed). Reference: client_fit_model.py:157,166."""
+    """Training parity, pinned on accuracy: the HIP engine (bf16 activations / gradients, fp32 master
+    weights, hipGraph steps) and the plain fp32 PyTorch oracle (RefTrainer: Keras semantics, fp32 everywhere, no bf16
+    emulation) trained from the SAME init on the SAME batches (128^2, batch 16, 1,200 steps over 896 synthetic
+    images), both evaluated on the same 128 held-out images (train/parity.py). The oracle must actually segment cracks
+    (val IoU >= 0.5, measured 0.53 at 800 steps: profiles/r3_parity) and the engine must land with it: |dIoU| <= 0.05,
+    val loss within 10 %. The first step's per-layer gradient cosines are checked against what bf16 itself costs (the
+    same oracle under torch.autocast(bf16)). Reference: client_fit_model.py:157,166."""
     from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
     from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
     from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
     from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
+    from crack_detection_federatedlearning_grpc_amd.train.parity import run
     table = ParamTable()
-    S, B, steps = 128, 16, 160
-    data = make_synthetic_device(320, S, seed=21, split=256)
+    S, B = 128, 16
+    # first-step gradients: engine vs plain fp32 vs fp32-under-autocast(bf16)
+    data = make_synthetic_device(64, S, seed=21, split=48)
     flat0 = table.init_flat(3)
     eng = UNetEngine(table, B, S)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(flat0)
-    ref = R.RefTrainer(table, flat0, "cuda")
-    batches = epoch_batches(data.train_idx, B, steps, seed=5)
-
-    def xy(ids):
-        t = torch.as_tensor(ids, dtype=torch.long, device=DEV)
-        return data.images[t].float() / 255.0, data.masks[t].float()[..., None]
-
-    # first-step gradients: engine vs plain fp32 vs fp32-under-autocast(bf16)
-    eng.idx.copy_(torch.as_tensor(batches[0], dtype=torch.int32, device=DEV))
+    ids = epoch_batches(data.train_idx, B, 1, seed=5)[0]
+    eng.idx.copy_(torch.as_tensor(ids, dtype=torch.int32, device=DEV))
     eng._zero_step()
     eng.forward(True)
     eng.backward()
     g_eng = eng.grad.clone()
-    eng.read_metrics("train")
-    x0, y0 = xy(batches[0])
+    l_eng0 = eng.read_metrics("train")["loss"]
+    t = torch.as_tensor(ids, dtype=torch.long, device=DEV)
+    x0, y0 = data.images[t].float() / 255.0, data.masks[t].float()[..., None]
     p = torch.as_tensor(flat0, device=DEV).clone().requires_grad_(True)
-    g32, = torch.autograd.grad(R.bce_with_logits_mean(R.unet_forward(p, x0, table)[0], y0), p)
+    l32 = R.bce_with_logits_mean(R.unet_forward(p, x0, table)[0], y0)
+    g32, = torch.autograd.grad(l32, p)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         lg = R.unet_forward(p, x0, table)[0]
     gac, = torch.autograd.grad(R.bce_with_logits_mean(lg.float(), y0), p)
     cos_eng, cos_ac = _first_layer_cos(g_eng, g32, table), _first_layer_cos(gac, g32, table)
     print(f"\nfirst-step gradient cosine vs plain fp32: engine {cos_eng}\n  torch autocast(bf16) {cos_ac}")
-    # trajectories
-    l_eng, l_ref = [], []
-    for ids in batches:
-        eng.idx.copy_(torch.as_tensor(ids, dtype=torch.int32, device=DEV))
-        eng.train_step(use_graph=True)
-        l_eng.append(eng.read_metrics("train")["loss"])
-        l_ref.append(ref.train_step(*xy(ids))["loss"])
-    l_eng, l_ref = np.array(l_eng), np.array(l_ref)
-    # held-out evaluation of both models on the same 64 images (inference-mode BN)
-    vb = epoch_batches(data.val_idx, B, 0, 0)
-    ev, tp, pp, tt = [], 0.0, 0.0, 0.0
-    eng.eval_metrics.zero_()
-    for ids in vb:
-        eng.idx.copy_(torch.as_tensor(ids, dtype=torch.int32, device=DEV))
-        eng.eval_step(use_graph=False)
-        m = ref.evaluate(*xy(ids))
-        ev.append(m["loss"])
-        tp, pp, tt = tp + m["tp"], pp + m["pp"], tt + m["t"]
-    me = eng.read_metrics("eval")
-    iou_ref = tp / (pp + tt - tp) if pp + tt - tp > 0 else 1.0
-    w = 20
-    print(f"loss engine {l_eng[:3].round(4)} .. {l_eng[-3:].round(4)}\n     fp32  {l_ref[:3].round(4)} .. "
-          f"{l_ref[-3:].round(4)}\nmean |diff| first {w}: {np.abs(l_eng[:w] - l_ref[:w]).mean():.4f}, "
-          f"last {w}: {np.abs(l_eng[-w:] - l_ref[-w:]).mean():.4f}; last-{w} means {l_eng[-w:].mean():.4f} / "
-          f"{l_ref[-w:].mean():.4f}\nval loss {me['loss']:.4f} / {np.mean(ev):.4f}, val IoU {me['iou']:.4f} / "
-          f"{iou_ref:.4f}, val acc {me['accuracy']:.4f}")
-    assert abs(l_eng[0] - l_ref[0]) < 0.02 * l_ref[0]                       # same init, same batch
-    assert np.abs(l_eng[:w] - l_ref[:w]).mean() < 0.05 * l_ref[:w].mean()   # trajectories coincide early
-    assert l_eng[-w:].mean() < 0.5 * l_eng[:w].mean() and l_ref[-w:].mean() < 0.5 * l_ref[:w].mean()   # both learn
-    assert abs(l_eng[-w:].mean() - l_ref[-w:].mean()) < 0.15 * l_ref[-w:].mean()   # and land together
-    assert abs(me["loss"] - np.mean(ev)) < 0.2 * np.mean(ev) + 0.01
-    assert abs(me["iou"] - iou_ref) < 0.1
+    assert abs(l_eng0 - float(l32)) < 0.02 * float(l32)                       # same init, same batch
     for k, v in cos_eng.items():                                            # gradient fidelity >= bf16 autocast's
         assert v >= min(0.85, cos_ac[k] - 0.05), (k, v, cos_ac[k])
+    del eng, data
+    # trained to segmentation quality, side by side
+    recs = run(img=S, batch=B, steps=1200, every=200, samples=1024, val=128, quiet=True)
+    for r in recs:
+        print(json.dumps(r))
+    first, last = recs[0], recs[-1]
+    te, tr = first["train_loss_engine"], first["train_loss_fp32"]
+    assert abs(te - tr) < 0.05 * tr                                         # trajectories coincide early
+    e, f = last["engine"], last["fp32"]
+    assert f["val_iou"] >= 0.5, f"the fp32 oracle does not segment yet: val IoU {f['val_iou']:.3f}"
+    assert abs(e["val_iou"] - f["val_iou"]) <= 0.05, (e, f)
+    assert abs(e["val_loss"] - f["val_loss"]) <= 0.10 * f["val_loss"], (e, f)
+    assert abs(e["val_acc"] - f["val_acc"]) <= 0.005, (e, f)
 
 
 @pytest.mark.parametrize("mix", [0, 1])
