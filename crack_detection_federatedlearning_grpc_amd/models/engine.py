@@ -289,6 +289,9 @@ class UNetEngine:
         # SeparableConv forward in one pass (sepconv.hip; CFL_SEP_FUSE=0: dw_fwd + pointwise conv)
         self.fuse_sep = os.environ.get("CFL_SEP_FUSE", "1") != "0"
         self.eager_after_fedavg = os.environ.get("CFL_EAGER_AFTER_FEDAVG", "0") == "1"
+        # independent streaming BN-backward passes co-launched with the residual convs' 1x1 dgrads that read the
+        # same incoming gradient (launch.h SideJob; CFL_SIDE_FUSE=0: separate launches)
+        self.side_fuse = os.environ.get("CFL_SIDE_FUSE", "1") != "0"
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         # per-step zeroing of gradients / statistics in one launch
@@ -556,10 +559,13 @@ class UNetEngine:
             bnB, bnA = self.bn[b2], self.bn[b1]
             # BN_B node: x_lo = BN_B(c2) + up?(q)  (no ReLU) -> its gradient IS dxlo. Its BN-backward sums were
             # accumulated by the pass that produced dxlo: head_bwd (k = 3) or the convT1 dgrad join of level k+1.
-            # The BN-backward applies of the decoder run as streaming passes: folded into the latency-bound 3x3
-            # dgrads' operand loads they measured slower twice (profiles/README.md, the folds were removed)
-            C.bn_bwd_apply(dxlo, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"],
-                           self.G(b2, "gamma"), self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
+            # The BN-backward applies of the decoder run as streaming passes (folded into the latency-bound 3x3
+            # dgrads' operand loads they measured slower twice, profiles/README.md); this one is independent of the
+            # residual conv's dgrad below, which reads the same dxlo: it runs as that launch's side job
+            bba_B = (dxlo, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"], self.G(b2, "gamma"),
+                     self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
+            if not self.side_fuse:
+                C.bn_bwd_apply(*bba_B)
             # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
             # (k > 0, default) the 2x2 sum is formed by the dgrad's operand load, which also stores dq for the
             # weight gradient (issued after it)
@@ -572,7 +578,8 @@ class UNetEngine:
                     C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
-                         prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if s2 else {}))
+                        prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if s2 else {}),
+                        **({"side_bba": bba_B} if self.side_fuse else {}))
             self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
                         F, 1, 1, 0, 0, 0)
             # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
@@ -619,9 +626,17 @@ class UNetEngine:
                 xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
             bnb, bna = self.bn[b2], self.bn[b1]
             fold = self.fold_pw
-            # BN_b node: routed through the max-pool (no ReLU)
-            C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0, D[f"e{k}_g"],
-                       bnb["sums"], B, H, H, F, self.RS)
+            # BN_b node: routed through the max-pool (no ReLU); independent of the residual 1x1 stride-2 conv's
+            # dgrad on x_in (dres = W^T dx_out, read only by the last depthwise backward of this level), which reads
+            # the same dx_out: the routing pass runs as that launch's side job
+            pool_b = (dx_out, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], D[f"e{k}_g"], bnb["sums"], B, H, H, F, self.RS)
+            # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
+            self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
+                        H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0,
+                        **({"side_pool": pool_b} if self.side_fuse else {}))
+            if not self.side_fuse:
+                C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0,
+                           D[f"e{k}_g"], bnb["sums"], B, H, H, F, self.RS)
             if not fold:
                 C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"],
                                self.G(b2, "gamma"), self.G(b2, "beta"), B * H * H, F, self.RS)
@@ -657,9 +672,6 @@ class UNetEngine:
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                         1, 2, 0, 0, 0)
-            # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
-            self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
-                         H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0)
             # depthwise 1 on relu(x_in), and the gradient of x_in itself: the depthwise branch (ReLU-masked) plus the
             # stride-2 scatter of dres; for k = 0 x_in is relu(BN0(y0)), a BN node (mask + sums)
             bn0 = self.bn[names[1]]

@@ -71,6 +71,61 @@ BnStatsIn stats_in(const OptT& stats, const OptT& gamma, const OptT& beta, doubl
   return f;
 }
 
+BnBwdApplyParams bba_params(at::Tensor g, at::Tensor y, at::Tensor ab, at::Tensor sums, at::Tensor dy, OptT dgamma,
+                            OptT dbeta, int M, int C, int sum_reps) {
+  BnBwdApplyParams p{};
+  p.sum_reps = sum_reps < 1 ? 1 : sum_reps;
+  TORCH_CHECK(sums.numel() >= (int64_t)p.sum_reps * 2 * C, "bn_bwd_apply: sums size");
+  p.g = ptr<const bf16_t>(g, "g");
+  p.y = ptr<const bf16_t>(y, "y");
+  p.ab = ptr<const float>(ab, "ab");
+  p.sums = ptr<const float>(sums, "sums");
+  p.dy = ptr<bf16_t>(dy, "dy");
+  p.dgamma = optr<float>(dgamma, "dgamma");
+  p.dbeta = optr<float>(dbeta, "dbeta");
+  p.M = M; p.C = C;
+  TORCH_CHECK(g.numel() == (int64_t)M * C && y.numel() == g.numel() && dy.numel() == g.numel(), "bn_bwd_apply sizes");
+  return p;
+}
+
+OptT opt_at(const py::tuple& t, int i) { return t[i].is_none() ? OptT() : OptT(t[i].cast<at::Tensor>()); }
+
+// side jobs of a streaming 1x1 dgrad (launch.h SideJob), as tuples of the standalone ops' arguments:
+//   side_bba  = (g, y, ab, sums, dy, dgamma, dbeta, M, C, reps)               (bn_bwd_apply)
+//   side_pool = (src, argmax, v, ab, out, sums, B, H, W, C, reps)            (node_bwd, GM_MAXPOOL routing)
+SideJob side_job(const py::object& side_bba, const py::object& side_pool) {
+  SideJob j{};
+  TORCH_CHECK(side_bba.is_none() || side_pool.is_none(), "conv_igemm: one side job at most");
+  if (!side_bba.is_none()) {
+    const py::tuple t = side_bba.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 10, "side_bba: (g, y, ab, sums, dy, dgamma, dbeta, M, C, reps)");
+    j.kind = SIDE_BBA;
+    j.bba = bba_params(t[0].cast<at::Tensor>(), t[1].cast<at::Tensor>(), t[2].cast<at::Tensor>(),
+                       t[3].cast<at::Tensor>(), t[4].cast<at::Tensor>(), opt_at(t, 5), opt_at(t, 6), t[7].cast<int>(),
+                       t[8].cast<int>(), t[9].cast<int>());
+  } else if (!side_pool.is_none()) {
+    const py::tuple t = side_pool.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 11, "side_pool: (src, argmax, v, ab, out, sums, B, H, W, C, reps)");
+    const at::Tensor src = t[0].cast<at::Tensor>(), am = t[1].cast<at::Tensor>(), v = t[2].cast<at::Tensor>();
+    const at::Tensor ab = t[3].cast<at::Tensor>(), out = t[4].cast<at::Tensor>(), sums = t[5].cast<at::Tensor>();
+    NodeBwdParams& q = j.pool;
+    q.src[0] = GradSrc{ptr<const bf16_t>(src, "src"), GM_MAXPOOL, 0};
+    q.src[1] = GradSrc{nullptr, GM_NONE, 0};
+    q.argmax = ptr<const uint8_t>(am, "argmax");
+    q.v = ptr<const bf16_t>(v, "v");
+    q.ab = ptr<const float>(ab, "ab");
+    q.out = ptr<bf16_t>(out, "out");
+    q.sums = ptr<float>(sums, "sums");
+    q.B = t[6].cast<int>(); q.H = t[7].cast<int>(); q.W = t[8].cast<int>(); q.C = t[9].cast<int>();
+    q.sum_reps = t[10].cast<int>() < 1 ? 1 : t[10].cast<int>();
+    const int64_t n = (int64_t)q.B * q.H * q.W * q.C, half = (int64_t)q.B * ((q.H + 1) / 2) * ((q.W + 1) / 2) * q.C;
+    TORCH_CHECK(v.numel() == n && out.numel() == n && src.numel() == half && am.numel() == half &&
+                ab.numel() >= 4 * q.C && sums.numel() >= (int64_t)q.sum_reps * 2 * q.C, "side_pool sizes");
+    j.kind = SIDE_POOL;
+  }
+  return j;
+}
+
 void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT stats, OptT ab, int relu, int B,
                    int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N, int ks, int stride, int pad_t,
                    int pad_l, OptT ws, int algo, OptT node_y, OptT node_ab, OptT node_sums, int node_reps,
@@ -79,7 +134,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
                    int pj_reps, OptT jfin_stats, OptT jfin_gamma, OptT jfin_beta, double jfin_count,
                    double jfin_eps, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count,
-                   double xfin_eps, OptT sum2x2) {
+                   double xfin_eps, OptT sum2x2, py::object side_bba, py::object side_pool) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -162,6 +217,7 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                 !p.bias && !p.stats && !node_y && !join_mode && !pj_v, "conv_igemm: sum2x2 is a plain 1x1 dgrad input");
     p.sum2x2 = ptr<const bf16_t>(*sum2x2, "sum2x2");
   }
+  p.side = side_job(side_bba, side_pool);
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
@@ -501,19 +557,7 @@ void node_bwd_op(OptT src0, int mode0, int mask0, OptT src1, int mode1, int mask
 
 void bn_bwd_apply_op(at::Tensor g, at::Tensor y, at::Tensor ab, at::Tensor sums, at::Tensor dy, OptT dgamma,
                      OptT dbeta, int M, int C, int sum_reps) {
-  BnBwdApplyParams p{};
-  p.sum_reps = sum_reps < 1 ? 1 : sum_reps;
-  TORCH_CHECK(sums.numel() >= (int64_t)p.sum_reps * 2 * C, "bn_bwd_apply: sums size");
-  p.g = ptr<const bf16_t>(g, "g");
-  p.y = ptr<const bf16_t>(y, "y");
-  p.ab = ptr<const float>(ab, "ab");
-  p.sums = ptr<const float>(sums, "sums");
-  p.dy = ptr<bf16_t>(dy, "dy");
-  p.dgamma = optr<float>(dgamma, "dgamma");
-  p.dbeta = optr<float>(dbeta, "dbeta");
-  p.M = M; p.C = C;
-  TORCH_CHECK(g.numel() == (int64_t)M * C && y.numel() == g.numel() && dy.numel() == g.numel(), "bn_bwd_apply sizes");
-  ok(bn_bwd_apply(p, stream()), "bn_bwd_apply");
+  ok(bn_bwd_apply(bba_params(g, y, ab, sums, dy, dgamma, dbeta, M, C, sum_reps), stream()), "bn_bwd_apply");
 }
 
 void pool_res_fwd_op(at::Tensor y, at::Tensor ab, at::Tensor res, at::Tensor out, at::Tensor argmax, int B, int H,
@@ -777,7 +821,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("jfin_gamma") = py::none(), py::arg("jfin_beta") = py::none(), py::arg("jfin_count") = 0.0,
         py::arg("jfin_eps") = 1e-3, py::arg("xfin_stats") = py::none(), py::arg("xfin_gamma") = py::none(),
         py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3,
-        py::arg("sum2x2") = py::none());
+        py::arg("sum2x2") = py::none(), py::arg("side_bba") = py::none(), py::arg("side_pool") = py::none());
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
@@ -861,6 +905,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD3_MINTILES32") = (int)TUNE_WGRAD3_MINTILES32;
   m.attr("TUNE_WGRAD_MIX") = (int)TUNE_WGRAD_MIX;
   m.attr("TUNE_WGRAD_MIX_XCD") = (int)TUNE_WGRAD_MIX_XCD;
+  m.attr("TUNE_SIDE") = (int)TUNE_SIDE;
   m.attr("TUNE_CONV3_SPLIT_BLOCKS") = (int)TUNE_CONV3_SPLIT_BLOCKS;
   m.attr("TUNE_CONV3_SPLIT_TARGET") = (int)TUNE_CONV3_SPLIT_TARGET;
   m.def("bn_finalize", &bn_finalize_op);

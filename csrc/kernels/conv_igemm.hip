@@ -498,6 +498,13 @@ int conv_igemm_splits(const ConvParams& p) {
 
 int conv_igemm(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 32 != 0 || p.K % BK != 0 || p.K != p.ks * p.ks * p.Cin || p.N % 32 != 0) return 1;
+  if (p.side.kind != SIDE_NONE && !pw_conv_supported(p)) {   // not on the streaming kernel: the side job alone, first
+    const int rc = p.side.kind == SIDE_BBA ? bn_bwd_apply(p.side.bba, st) : node_bwd(p.side.pool, st);
+    if (rc) return rc;
+    ConvParams q = p;
+    q.side = SideJob{};
+    return conv_igemm(q, st);
+  }
   if (p.sum2x2 && !pw_conv_supported(p)) {   // 2x2-sum input on another kernel: node_bwd(GM_SUM2X2) into x first
     NodeBwdParams q{};
     q.src[0] = GradSrc{p.sum2x2, GM_SUM2X2, 0};

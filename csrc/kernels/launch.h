@@ -92,6 +92,46 @@ struct PoolJoinEpi {
   int reps;
 };
 
+struct GradSrc {
+  const bf16_t* p;
+  int mode;
+  int mask;                // multiply this source by [v > 0]
+};
+struct NodeBwdParams {
+  GradSrc src[2];
+  const uint8_t* argmax;   // GM_MAXPOOL: [B, ceil(H/2), ceil(W/2), C] in 0..8
+  const bf16_t* v;         // node value source: raw y (BN node: v = a*y+b) or plain x
+  const float* ab;         // BN coefficients (4 rows) or nullptr for a plain node
+  int relu_node;           // mask the total by [v > 0]
+  bf16_t* out;             // gradient w.r.t. the BN output (BN node) or w.r.t. x (plain node)
+  float* sums;             // [sum_reps][2][C]: sum g, sum g*xhat (BN node) / [sum_reps][C] sum g (plain) / nullptr
+  const bf16_t* sy;        // optional: xhat for the sums from THIS tensor + sab (mean, rstd rows) instead of v / ab -
+  const float* sab;        //   the gradient of a plain node that is also the (unmasked) gradient of a BN node
+  int B, H, W, C;
+  int sum_reps;            // replica rows of sums (block b adds into row b % sum_reps); <= 1: one row
+};
+struct BnBwdApplyParams {
+  const bf16_t* g;         // gradient w.r.t. BN output (masked)
+  const bf16_t* y;         // raw BN input
+  const float* ab;         // 4 rows: a, b, mean, rstd
+  const float* sums;       // [sum_reps][2][C] (node_bwd replica rows, summed here)
+  bf16_t* dy;              // gradient w.r.t. y
+  float* dgamma;           // flat-grad slots (written, not accumulated) or nullptr
+  float* dbeta;
+  int M, C;
+  int sum_reps;
+};
+// A streaming BN-backward pass run as the "side job" of a streaming 1x1 data gradient (pw.hip) that reads the same
+// incoming gradient and does not depend on it: its blocks are interleaved with the conv's in ONE launch (two
+// latency-bound passes co-run instead of back to back). kind 0 = none; shapes pw.hip does not take run it first,
+// alone (conv_igemm).
+enum SideKind { SIDE_NONE = 0, SIDE_BBA = 1, SIDE_POOL = 2 };
+struct SideJob {
+  int kind;
+  BnBwdApplyParams bba;    // SIDE_BBA: bn_bwd_apply
+  NodeBwdParams pool;      // SIDE_POOL: node_bwd routed through the max-pool (node_pool_eligible)
+};
+
 struct ConvParams {
   const bf16_t* x;     // [B, Hin, Win, Cin] NHWC (physical; logical = upsample2 if up_in)
   const bf16_t* wt;    // [N][K] packed bf16 weights, K = ks*ks*Cin, k = (ky*ks + kx)*Cin + ci
@@ -112,6 +152,7 @@ struct ConvParams {
   BnBwdIn bwd;         // optional BN-backward apply folded into the operand load (x = the BN node gradient g;
                        // common.h). Data-gradient convs only: 1x1/s1 or 3x3/s1, no upsample, no xf; shapes a kernel
                        // does not fold fall back to bn_bwd_apply into bwd.dx + the plain conv (same results)
+  SideJob side;        // optional independent streaming pass co-launched with a streaming 1x1 conv (pw.hip)
   const bf16_t* sum2x2;  // optional: x = the 2x2-block sums of this [B, 2*Hin, 2*Win, Cin] gradient (node_bwd
                          // GM_SUM2X2 order), formed on load by the streaming 1x1 kernel and stored into x (const cast)
                          // for the weight gradient; other kernels run node_bwd into x first (same results)
@@ -254,38 +295,13 @@ struct BnEval {             // one BatchNorm layer's inference coefficients (mov
 int bn_eval_coefs(const BnEval* d_layers, int n_layers, hipStream_t st);
 
 enum GradMode { GM_NONE = 0, GM_SAME = 1, GM_SCATTER2 = 2, GM_SUM2X2 = 3, GM_MAXPOOL = 4 };
-struct GradSrc {
-  const bf16_t* p;
-  int mode;
-  int mask;                // multiply this source by [v > 0]
-};
-struct NodeBwdParams {
-  GradSrc src[2];
-  const uint8_t* argmax;   // GM_MAXPOOL: [B, ceil(H/2), ceil(W/2), C] in 0..8
-  const bf16_t* v;         // node value source: raw y (BN node: v = a*y+b) or plain x
-  const float* ab;         // BN coefficients (4 rows) or nullptr for a plain node
-  int relu_node;           // mask the total by [v > 0]
-  bf16_t* out;             // gradient w.r.t. the BN output (BN node) or w.r.t. x (plain node)
-  float* sums;             // [sum_reps][2][C]: sum g, sum g*xhat (BN node) / [sum_reps][C] sum g (plain) / nullptr
-  const bf16_t* sy;        // optional: xhat for the sums from THIS tensor + sab (mean, rstd rows) instead of v / ab -
-  const float* sab;        //   the gradient of a plain node that is also the (unmasked) gradient of a BN node
-  int B, H, W, C;
-  int sum_reps;            // replica rows of sums (block b adds into row b % sum_reps); <= 1: one row
-};
 int node_bwd(const NodeBwdParams& p, hipStream_t st);
 
-struct BnBwdApplyParams {
-  const bf16_t* g;         // gradient w.r.t. BN output (masked)
-  const bf16_t* y;         // raw BN input
-  const float* ab;         // 4 rows: a, b, mean, rstd
-  const float* sums;       // [sum_reps][2][C] (node_bwd replica rows, summed here)
-  bf16_t* dy;              // gradient w.r.t. y
-  float* dgamma;           // flat-grad slots (written, not accumulated) or nullptr
-  float* dbeta;
-  int M, C;
-  int sum_reps;
-};
 int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st);
+bool bn_bwd_apply_ok(const BnBwdApplyParams& p);
+int bn_bwd_apply_grid(const BnBwdApplyParams& p);
+bool node_pool_eligible(const NodeBwdParams& p);
+int node_pool_grid(const NodeBwdParams& p);
 
 struct PoolResParams {     // x = maxpool3x3s2_same(a*y + b) + res ; argmax recorded
   const bf16_t* y;
@@ -425,7 +441,8 @@ enum TuneKey {
   TUNE_SEP = 33,               // SeparableConv forward: 0 = fused depthwise + pointwise (sepconv.hip), 1 = two passes
   TUNE_SEP_BLOCKS = 34,        // fused SeparableConv forward: target grid size (default 512)
   TUNE_WGRAD_MIX_XCD = 35,     // mixed wgrad launch: 0 = XCD-grouped block order, 1 = dispatch order
-  TUNE_N = 36
+  TUNE_SIDE = 36,              // streaming 1x1 dgrads: 0 = co-launch their side job (SideJob), 1 = run it alone first
+  TUNE_N = 37
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -24,6 +24,7 @@
 //   S2  - the 2x2-block sum of a full-resolution gradient (the decoder residual conv's upsample gradient).
 #include "common.h"
 #include "launch.h"
+#include "side_bodies.h"
 
 namespace {
 
@@ -45,8 +46,9 @@ constexpr int pw_rows() { return K >= 128 ? 4096 / K : (S2 ? 32 : 64); }
 // S2: the input is the 2x2-block sum of p.sum2x2 (the decoder residual conv's upsample gradient): the four full-
 // resolution pixels of each B-fragment pixel are loaded and summed ((o00 + o01) + (o10 + o11), rounded once: node_bwd's
 // GM_SUM2X2), and the slice-0 blocks store the sums into x for the weight gradient.
-template <int NB, int K, int D, bool BWD, bool S2 = false>
-__global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices) {
+// bid / nblocks: this block's index among, and the number of, the launch's conv blocks (a multiple of 8)
+template <int NB, int K, int D, bool BWD, bool S2>
+CFL_DEVICE void pw_body(const ConvParams& p, int nslices, int bid, int nblocks) {
   constexpr int WR = pw_rows<K, S2>();
   constexpr int MF = WR / 16, NF = NB / 16, KS = K / 32;
   __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
@@ -58,9 +60,9 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
   const int r16 = lane & 15, q = lane >> 4;
   // block -> (output-channel slice, block within the slice); the slices of one pixel range sit on one XCD
   // (dispatch order b, b + 8, ... share an XCD and its L2, which then serves the second slice's input reads)
-  const int j = blockIdx.x >> 3;
-  const int slice = j % nslices, bs = (j / nslices) * 8 + (blockIdx.x & 7);
-  const int bps = gridDim.x / nslices;
+  const int j = bid >> 3;
+  const int slice = j % nslices, bs = (j / nslices) * 8 + (bid & 7);
+  const int bps = nblocks / nslices;
   const int n0 = slice * NB;
   const int tiles = (p.M + WR - 1) / WR;
   const int wstride = bps * (NT / 64);
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
         *reinterpret_cast<const uint4*>(p.wt + (size_t)(n0 + n) * K + kc * 8);
   }
   if (tid < NB) sBias[tid] = p.bias ? p.bias[n0 + tid] : 0.f;
-  if constexpr (BWD) bnb_prologue<NT>(p.bwd, K, sco, sco + 5 * K, blockIdx.x == 0);   // ends with a barrier
+  if constexpr (BWD) bnb_prologue<NT>(p.bwd, K, sco, sco + 5 * K, bid == 0);   // ends with a barrier
   else __syncthreads();
 
   const bool stats = p.stats != nullptr;
@@ -240,13 +242,41 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
       }
   }
   __syncthreads();
-  float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+  float* rep = p.stats + (size_t)(bid % STAT_REPLICAS) * 2 * p.N;
   for (int e = tid; e < 2 * NB; e += NT) {
     const int st = e / NB, cc = e - st * NB;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
     atomicAdd(&rep[st * p.N + n0 + cc], v);
+  }
+}
+
+// The conv's blocks and (SIDE) the side job's blocks of one launch, interleaved in groups of 8 so a conv block keeps
+// its dispatch-order XCD (block b -> XCD b % 8, which pw_body's slice mapping relies on) and both kinds are resident
+// on every CU from the start: conv groups at even, side groups at odd group positions while both last, then the
+// remaining conv blocks, then the remaining side blocks.
+template <int NB, int K, int D, bool BWD, bool S2 = false, int SIDE = SIDE_NONE>
+__global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices, int conv_blocks) {
+  if constexpr (SIDE == SIDE_NONE) {
+    pw_body<NB, K, D, BWD, S2>(p, nslices, blockIdx.x, conv_blocks);
+  } else {
+    const int side_blocks = gridDim.x - conv_blocks;
+    const int pairs = imin(conv_blocks >> 3, side_blocks >> 3);
+    const int b = blockIdx.x, grp = b >> 3;
+    bool conv;
+    int idx;
+    if (grp < 2 * pairs) {
+      conv = (grp & 1) == 0;
+      idx = (grp >> 1) * 8 + (b & 7);
+    } else {                                           // the rest: conv blocks first, then side blocks
+      const int rb = b - 16 * pairs, conv_rest = conv_blocks - 8 * pairs;
+      conv = rb < conv_rest;
+      idx = pairs * 8 + (conv ? rb : rb - conv_rest);
+    }
+    if (conv) pw_body<NB, K, D, BWD, S2>(p, nslices, idx, conv_blocks);
+    else if constexpr (SIDE == SIDE_BBA) side::bba_body(p.side.bba, idx, side_blocks);
+    else side::node_pool_body<1>(p.side.pool, idx, side_blocks);
   }
 }
 
@@ -266,23 +296,35 @@ void launch_d(const ConvParams& p, hipStream_t st) {
   tpw = (tpw + D - 1) / D * D;
   const int waves = (tiles + tpw - 1) / tpw;
   const int bps = ((waves + 3) / 4 + 7) / 8 * 8;
+  const int cb = bps * nslices;
   if constexpr (D == 1) {
+    if (p.side.kind == SIDE_BBA) {                 // the decoder residual dgrads + the BN_B backward apply
+      const dim3 g(cb + bn_bwd_apply_grid(p.side.bba));
+      if (p.sum2x2) hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true, SIDE_BBA>), g, dim3(NT), 0, st, p, nslices, cb);
+      else hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, false, SIDE_BBA>), g, dim3(NT), 0, st, p, nslices, cb);
+      return;
+    }
+    if (p.side.kind == SIDE_POOL) {                // the encoder residual dgrads + the max-pool node gradient
+      const dim3 g(cb + node_pool_grid(p.side.pool));
+      hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, false, SIDE_POOL>), g, dim3(NT), 0, st, p, nslices, cb);
+      return;
+    }
     if (p.sum2x2) {
-      hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+      hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true>), dim3(cb), dim3(NT), 0, st, p, nslices, cb);
       return;
     }
     if (bwd) {
-      hipLaunchKernelGGL((pw_kernel<NB, K, 1, true>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+      hipLaunchKernelGGL((pw_kernel<NB, K, 1, true>), dim3(cb), dim3(NT), 0, st, p, nslices, cb);
       return;
     }
   }
-  hipLaunchKernelGGL((pw_kernel<NB, K, D, false>), dim3(bps * nslices), dim3(NT), 0, st, p, nslices);
+  hipLaunchKernelGGL((pw_kernel<NB, K, D, false>), dim3(cb), dim3(NT), 0, st, p, nslices, cb);
 }
 
 template <int NB, int K>
 void launch(const ConvParams& p, hipStream_t st) {
   int d = cfl_tune(TUNE_PW_DEPTH);
-  if (d <= 0 || p.bwd.y || p.sum2x2) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration; the
+  if (d <= 0 || p.bwd.y || p.sum2x2 || p.side.kind) d = 1;   // whole-step A/B: depth 1 / 2 (4 at K = 32) 1.459 / 1.478 ms per iteration; the
                                   // BN-backward form holds y as well and runs at depth 1 only (deeper rings spill)
   if constexpr (K == 32) {                                // deeper rings spill at K >= 64
     if (d >= 4) return launch_d<NB, K, 4>(p, st);
@@ -300,7 +342,10 @@ bool pw_conv_supported(const ConvParams& p) {
          p.xf.ab == nullptr && !p.xf.relu && p.node.y == nullptr && p.join.mode == JOIN_NONE &&
          (p.bwd.y == nullptr || (p.bwd.dx != nullptr && p.bwd.reps <= BNB_MAX_REPS)) &&
          (p.sum2x2 == nullptr || (p.bwd.y == nullptr && p.bias == nullptr && p.stats == nullptr)) && p.pj.v == nullptr &&
-         p.xfin.stats == nullptr && p.M > 0;
+         p.xfin.stats == nullptr && p.M > 0 &&
+         (p.side.kind == SIDE_NONE || (p.bwd.y == nullptr && cfl_tune(TUNE_SIDE) != 1 &&
+                                       (p.side.kind == SIDE_BBA ? bn_bwd_apply_ok(p.side.bba)
+                                                                : node_pool_eligible(p.side.pool))));
 }
 
 int pw_conv(const ConvParams& p, hipStream_t st) {

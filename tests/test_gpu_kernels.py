@@ -1283,6 +1283,74 @@ def test_training_parity_vs_plain_fp32():
     assert abs(e["val_acc"] - f["val_acc"]) <= 0.005, (e, f)
 
 
+@pytest.mark.parametrize("kind,B,H,K,N,s2,off", [
+    ("bba", 2, 8, 256, 256, False, False),     # decoder level 0: plain residual dgrad + BN_B backward apply
+    ("bba", 2, 16, 128, 256, True, False),     # decoder levels 1-3: 2x2-sum residual dgrad + BN_B backward apply
+    ("bba", 3, 32, 32, 64, True, False),
+    ("bba", 2, 16, 128, 256, True, True),      # TUNE_SIDE=1: the side job alone, first
+    ("pool", 2, 32, 64, 32, False, False),     # encoder: residual dgrad + the max-pool routed node gradient
+    ("pool", 2, 16, 256, 128, False, False),
+])
+def test_conv_side_job_matches_separate_passes(kind, B, H, K, N, s2, off):
+    """launch.h SideJob: a streaming BN-backward pass co-launched with the streaming 1x1 dgrad that reads the same
+    incoming gradient (blocks interleaved in groups of 8) writes exactly what the standalone pass writes, and the
+    conv output is unchanged: bn_bwd_apply (dx, dgamma, dbeta) bit-equal; node_bwd max-pool routing (g) bit-equal,
+    its BN sums up to float-atomic order."""
+    torch.manual_seed(71)
+    C_ = hip()
+    reps = 4
+    wt, _ = bf(torch.randn(N, K) * 0.05)
+    if kind == "bba":
+        Hf = 2 * H if s2 else H                             # the incoming gradient's resolution
+        gb, _ = bf(torch.randn(B, Hf, Hf, K))
+        yb, _ = bf(torch.randn(B, Hf, Hf, K) * 0.7 + 0.1)
+        ab = ab_for(K, 72)[0]
+        ab[2 * K:3 * K], ab[3 * K:] = torch.randn(K) * 0.1, torch.rand(K) + 0.6
+        ab = ab.to(DEV)
+        M = B * Hf * Hf
+        sums = (torch.randn(reps, 2, K) * (M / reps) ** 0.5).reshape(-1).to(DEV)
+    else:
+        Hf = 2 * H                                          # node at full resolution, dx_out pooled
+        gb, _ = bf(torch.randn(B, H, H, K))                 # dx_out: the conv input and the routed gradient
+        yb, _ = bf(torch.randn(B, Hf, Hf, K))
+        am = torch.randint(0, 9, (B, H, H, K), dtype=torch.uint8, device=DEV)
+        ab = ab_for(K, 73)[0]
+        ab[2 * K:3 * K], ab[3 * K:] = torch.randn(K) * 0.1, torch.rand(K) + 0.6
+        ab = ab.to(DEV)
+    outs = []
+    for fused in (True, False):
+        x = torch.zeros(B, H, H, K, dtype=torch.int16, device=DEV) if s2 else gb
+        out = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+        side_out = torch.zeros(B, Hf, Hf, K, dtype=torch.int16, device=DEV)
+        dgam, dbet = torch.zeros(K, device=DEV), torch.zeros(K, device=DEV)
+        psums = torch.zeros(reps * 2 * K, device=DEV)
+        if kind == "bba":
+            job = (gb, yb, ab, sums, side_out, dgam, dbet, B * Hf * Hf, K, reps)
+        else:
+            job = (gb, am, yb, ab, side_out, psums, B, Hf, Hf, K, reps)
+        kw = {"sum2x2": gb} if s2 else {}
+        if fused:
+            if off:
+                C_.set_tune(C_.TUNE_SIDE, 1)
+            try:
+                C_.conv_igemm(x, wt, None, out, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0,
+                              **kw, **({"side_bba": job} if kind == "bba" else {"side_pool": job}))
+            finally:
+                C_.set_tune(C_.TUNE_SIDE, 0)
+        else:
+            if kind == "bba":
+                C_.bn_bwd_apply(*job)
+            else:
+                C_.node_bwd(gb, 4, 0, None, 0, 0, am, yb, ab, 0, side_out, psums, B, Hf, Hf, K, reps)
+            C_.conv_igemm(x, wt, None, out, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0, **kw)
+        torch.cuda.synchronize()
+        outs.append((out.cpu(), side_out.cpu(), dgam.cpu(), dbet.cpu(), psums.view(reps, 2, K).sum(0).cpu()))
+    f, u = outs
+    assert torch.equal(f[0], u[0]) and torch.equal(f[1], u[1])
+    assert torch.equal(f[2], u[2]) and torch.equal(f[3], u[3])
+    assert torch.allclose(f[4], u[4], rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("mix", [0, 1])
 def test_conv_wgrad_batch_grouped_equals_individual(mix):
     """conv_wgrad_batch (the engine's deferred weight gradients): every wgrad in ONE mixed launch (default, mix=0)
@@ -1454,7 +1522,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
             C_.set_tune(keys[tune][0], 0)
 
 
-@pytest.mark.parametrize("var,val", [("CFL_SEP_FUSE", "0"), ("CFL_HEAD_FUSE", "0"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_SUM2X2_FOLD", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
+@pytest.mark.parametrize("var,val", [("CFL_SIDE_FUSE", "0"), ("CFL_SEP_FUSE", "0"), ("CFL_HEAD_FUSE", "0"), ("CFL_BNB_FOLD_PW", "0"), ("CFL_BNB_FOLD_ENTRY", "0"), ("CFL_SUM2X2_FOLD", "0"), ("CFL_WGRAD_DEFER", "0"), ("CFL_DW_BWD_FUSE", "0"), ("CFL_POOL_JOIN", "0"), ("CFL_FIN_CONSUMER", "0")])
 def test_engine_switch_matches_default(var, val):
     """Engine variants - two-pass SeparableConv forward / head (CFL_SEP_FUSE=0, CFL_HEAD_FUSE=0), weight gradients
     issued where computed (CFL_WGRAD_DEFER=0) - match the default step: same loss, same gradients up to the run-to-run atomic-order noise
