@@ -88,6 +88,11 @@ class UNetEngine:
         self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
         self._build_pack()
         self._alloc()
+        # the optimizer tail (Adam + BN moving statistics + bf16 repack + step / cursor advance) as ONE opt_step
+        # launch (CFL_OPT_FUSE=0: adam_update, bn_moving_update and pack_weights launches)
+        self.fuse_opt = share is None and os.environ.get("CFL_OPT_FUSE", "1") != "0"
+        if self.fuse_opt:
+            self._build_opt()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.eval_graph: Optional[torch.cuda.CUDAGraph] = None
         self._retired: List[torch.Tensor] = []   # replaced workspaces a captured graph may still reference
@@ -186,6 +191,42 @@ class UNetEngine:
         self._view_src = {(v[0], ly): v for ly, v in zip([k[0] for k in self.packed_at], views)}
         self._bucket_packs: Dict[Tuple[int, int], object] = {}
         self.n_views, self.max_pack = len(views), max_el
+
+    def _build_opt(self) -> None:
+        """Work items of opt_step (launch.h): 64x64 Adam tiles of every GEMM weight, each writing both bf16 views of
+        its tile (the same layouts pack_weights writes), 1024-element Adam items over the other trainable arrays,
+        one moving-statistics item per BN layer."""
+        C = self.C
+        items, tiled = [], set()
+        for ly in self.table.weighted_layers():
+            if ly.kind == "sepconv":         # (1,1,C,F) as [C][F]: PK_PW = transpose, PK_PW_DGRAD = copy
+                wn, kt, kc, rows, cols = "pointwise_kernel", PK_PW, PK_PW_DGRAD, ly.cin, ly.cout
+                rmap = (rows, cols, 0, 0)
+            elif ly.kind == "convt":         # (3,3,out,in) as [9 out][in]: PK_CONVT_DGRAD = transpose, PK_CONVT = flip
+                wn, kt, kc, rows, cols = "kernel", PK_CONVT_DGRAD, PK_CONVT, 9 * ly.cout, ly.cin
+                rmap = (ly.cout, 9 * ly.cin, -ly.cin, 8 * ly.cin)
+            elif ly.kind == "conv" and ly.ksize == 1 and ly.cout > 1:   # [cin][cout]: PK_CONV = transpose
+                wn, kt, kc, rows, cols = "kernel", PK_CONV, PK_CONV_DGRAD1x1, ly.cin, ly.cout
+                rmap = (rows, cols, 0, 0)
+            else:
+                continue
+            e = self.table.entry(ly.name, wn)
+            if not e.trainable or e.size != rows * cols:
+                raise RuntimeError(f"opt table: {ly.name}/{wn} is not a trainable [{rows}][{cols}] weight")
+            dt, dc = self.packed_at[(ly.name, kt)][0], self.packed_at[(ly.name, kc)][0]
+            for r0 in range(0, rows, 64):
+                for c0 in range(0, cols, 64):
+                    items.append((C.OI_TILE, 0, r0, c0, rows, cols) + rmap + (e.offset, dt, dc))
+            tiled.add((ly.name, wn))
+        for e in self.table.entries:
+            if e.trainable and (e.layer, e.wname) not in tiled:
+                for i in range(0, e.size, 1024):
+                    items.append((C.OI_FLAT, min(1024, e.size - i), 0, 0, 0, 0, 0, 0, 0, 0, e.offset + i, 0, 0))
+        moving = [(self.bn[n]["stats"], self.P(n, "moving_mean"), self.P(n, "moving_variance"), self.bn[n]["C"],
+                   float(self.bn_count(n))) for n in self.bn_names]
+        self.opt_table = C.make_opt_table(items, moving, self.flat)
+        self.n_opt = len(items) + len(moving)
+        self.opt_ticket = torch.zeros(1, dtype=torch.int32, device=self.dev)
 
     def W(self, layer: str, kind: int) -> torch.Tensor:
         off, n = self.packed_at[(layer, kind)]
@@ -328,11 +369,15 @@ class UNetEngine:
                 raise RuntimeError("weight-gradient slabs must be allocated before graph capture")
             if key in self._wslabs:
                 self._retired.append(self._wslabs[key])
-            slab = torch.zeros(rows * n, dtype=torch.float32, device=self.dev)
-            self._wslabs[key] = slab
             dst = self.G(*key)
             self._finish_dyn = [e for e in self._finish_dyn if e[1].data_ptr() != dst.data_ptr()]
-            self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
+            if rows == 1 and plain:
+                # one plainly-stored row (the 16^2 decoder layers) IS the gradient: stored in place, no finish pass
+                slab = dst
+            else:
+                slab = torch.zeros(rows * n, dtype=torch.float32, device=self.dev)
+                self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
+            self._wslabs[key] = slab
             self._finish_dirty = True
         args = (x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l, dst_mode, 0, 0,
                 rows)
@@ -709,6 +754,14 @@ class UNetEngine:
     def optimizer_step(self) -> None:
         self._await_all()
         C = self.C
+        if self.fuse_opt:
+            cursor = self.batch_cursor if self.batch_table is not None else None
+            C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
+                       self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
+            if self.fp8:
+                self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8,
+                                self.max_rows8, self.amax8, self.n_views8)
+            return
         C.adam_update(self.flat, self.grad, self.m, self.v, self.trainable, self.lr, self.b1, self.b2, self.adam_eps,
                       self.step_t)
         C.bn_moving_update(self.moving_table, len(self.bn_names), self.momentum)

@@ -661,6 +661,64 @@ void pack_weights_op(at::Tensor flat, at::Tensor packed, at::Tensor table, int n
      "pack_weights");
 }
 
+// items: list of (kind, n, r0, c0, rows, cols, q, s1, s2, base2, src, dst_t, dst_b) for OI_FLAT / OI_TILE, then one
+// OI_MOVING item per (stats, moving_mean, moving_variance, C, count)
+at::Tensor make_opt_table(std::vector<std::tuple<int, int, int, int, int, int, int, int, int, int, int64_t, int64_t,
+                                                 int64_t>> items,
+                          std::vector<std::tuple<at::Tensor, at::Tensor, at::Tensor, int, double>> moving,
+                          at::Tensor like) {
+  std::vector<OptItem> h;
+  for (auto& t : items) {
+    OptItem o{};
+    o.kind = std::get<0>(t); o.n = std::get<1>(t); o.r0 = std::get<2>(t); o.c0 = std::get<3>(t);
+    o.rows = std::get<4>(t); o.cols = std::get<5>(t); o.q = std::get<6>(t); o.s1 = std::get<7>(t);
+    o.s2 = std::get<8>(t); o.base2 = std::get<9>(t); o.src = std::get<10>(t); o.dst_t = std::get<11>(t);
+    o.dst_b = std::get<12>(t);
+    TORCH_CHECK(o.kind == OI_FLAT || o.kind == OI_TILE, "opt table: kind");
+    TORCH_CHECK(o.kind != OI_FLAT || (o.n > 0 && o.n <= 1024), "opt table: flat items hold 1..1024 elements");
+    TORCH_CHECK(o.kind != OI_TILE || (o.q > 0 && o.rows > 0 && o.cols > 0 && o.r0 % 64 == 0 && o.c0 % 64 == 0 &&
+                                      o.r0 < o.rows && o.c0 < o.cols), "opt table: tile geometry");
+    h.push_back(o);
+  }
+  for (auto& l : moving) {
+    OptItem o{};
+    o.kind = OI_MOVING;
+    o.stats = ptr<const float>(std::get<0>(l), "stats");
+    o.mmean = ptr<float>(std::get<1>(l), "mmean");
+    o.mvar = ptr<float>(std::get<2>(l), "mvar");
+    o.n = std::get<3>(l);
+    o.count = (float)std::get<4>(l);
+    TORCH_CHECK(std::get<0>(l).numel() >= (int64_t)STAT_REPLICAS * 2 * o.n && std::get<1>(l).numel() >= o.n &&
+                std::get<2>(l).numel() >= o.n, "opt table: moving sizes");
+    h.push_back(o);
+  }
+  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(OptItem))}, torch::kUInt8);
+  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(OptItem));
+  return cpu.to(like.device());
+}
+
+void opt_step_op(at::Tensor table, int n_items, at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
+                 at::Tensor trainable, at::Tensor packed, double lr, double b1, double b2, double eps, double momentum,
+                 at::Tensor step, OptT cursor, at::Tensor ticket) {
+  TORCH_CHECK(table.numel() == (int64_t)n_items * (int64_t)sizeof(OptItem), "opt_step: table size");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel() &&
+              trainable.numel() == p.numel(), "opt_step sizes");
+  OptParams o{};
+  o.p = ptr<float>(p, "p");
+  o.g = ptr<const float>(g, "g");
+  o.m = ptr<float>(m, "m");
+  o.v = ptr<float>(v, "v");
+  o.trainable = ptr<const uint8_t>(trainable, "trainable");
+  o.packed = ptr<bf16_t>(packed, "packed");
+  o.items = ptr<const OptItem>(table, "table");
+  o.n_items = n_items;
+  o.lr = (float)lr; o.b1 = (float)b1; o.b2 = (float)b2; o.eps = (float)eps; o.momentum = (float)momentum;
+  o.step = ptr<int>(step, "step");
+  o.cursor = optr<int>(cursor, "cursor");
+  o.ticket = ptr<int>(ticket, "ticket");
+  ok(opt_step(o, stream()), "opt_step");
+}
+
 // entries: list of (src, dst, n, replicas, mode) -> (device table, grid size)
 std::tuple<at::Tensor, int> make_grad_finish_table(std::vector<std::tuple<at::Tensor, at::Tensor, int, int, int>> entries) {
   std::vector<GradFinish> h;
@@ -939,6 +997,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ws") = py::none());
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
         py::arg("max_elems"), py::arg("step") = py::none(), py::arg("cursor") = py::none());
+  m.def("make_opt_table", &make_opt_table);
+  m.def("opt_step", &opt_step_op, py::arg("table"), py::arg("n_items"), py::arg("p"), py::arg("g"), py::arg("m"),
+        py::arg("v"), py::arg("trainable"), py::arg("packed"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
+        py::arg("eps"), py::arg("momentum"), py::arg("step"), py::arg("cursor"), py::arg("ticket"));
+  m.attr("OI_FLAT") = (int)OI_FLAT;
+  m.attr("OI_TILE") = (int)OI_TILE;
   m.def("render_cracks", &render_cracks_op);
   m.def("resize_batch", &resize_batch_op, py::arg("src"), py::arg("offs"), py::arg("dims"), py::arg("dst"),
         py::arg("binarize") = 0);

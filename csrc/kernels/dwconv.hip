@@ -196,28 +196,36 @@ CFL_DEVICE void load_f4_or(const float* p, bool cond, float dflt, float* f) {
 // one element of the two right-halo columns 32, 33 (row t / (2G)); q = t % G in both cases. Addresses are then a
 // per-thread constant plus a per-row stride, so staging NR rows costs NR + 1 loads and almost no address registers.
 // src_b: image b's base + this thread's channel offset; offsets are 32-bit (every tensor < 2^31 elements).
+// Every lane issues its loads (padding positions read a clamped in-image address; okm marks them and put() zeroes
+// them when the rows are written to LDS, not here - a select right after a load made the compiler wait for it on
+// the spot): per-lane branches around loads made the compiler's wait counting give up (vmcnt(0) at the first use of
+// any load, draining the prefetch in flight); only block / wave-uniform conditions branch.
 template <int NR>
 CFL_DEVICE void fetch(const bf16_t* src_b, const DwParams& p, int x0, int row0, bool on, uint2 (&v)[NR + 1],
                       uint32_t& okm) {
   const int tid = threadIdx.x;
+  okm = 0;
+  v[NR] = make_uint2(0, 0);
+  // (on == false - past the segment's last step - still loads, all marked invalid: straight-line code keeps the
+  // wait counts exact)
   const int ix = x0 + tid / G - 1;
   const bool colok = on && (unsigned)ix < (unsigned)p.W;
-  okm = 0;
+  const int ixc = min(max(ix, 0), p.W - 1);
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int iy = row0 + r;
     const bool ok = colok && (unsigned)iy < (unsigned)p.H;
-    uint2 t = make_uint2(0, 0);
-    if (ok) t = *reinterpret_cast<const uint2*>(src_b + (iy * p.W + ix) * p.C);
-    v[r] = t;
+    const int iyc = min(max(iy, 0), p.H - 1);
+    v[r] = *reinterpret_cast<const uint2*>(src_b + (iyc * p.W + ixc) * p.C);
     okm |= (uint32_t)ok << r;
   }
-  const int iye = row0 + tid / (2 * G), ixe = x0 + TW - 1 + (tid % (2 * G)) / G;
-  const bool ok = on && tid < 2 * G * NR && (unsigned)iye < (unsigned)p.H && (unsigned)ixe < (unsigned)p.W;
-  uint2 t = make_uint2(0, 0);
-  if (ok) t = *reinterpret_cast<const uint2*>(src_b + (iye * p.W + ixe) * p.C);
-  v[NR] = t;
-  okm |= (uint32_t)ok << NR;
+  if (__builtin_amdgcn_readfirstlane(tid) < 2 * G * NR) {    // the right-halo elements (whole waves branch)
+    const int iye = row0 + tid / (2 * G), ixe = x0 + TW - 1 + (tid % (2 * G)) / G;
+    const bool ok = on && tid < 2 * G * NR && (unsigned)iye < (unsigned)p.H && (unsigned)ixe < (unsigned)p.W;
+    const int iyc = min(max(iye, 0), p.H - 1), ixc2 = min(ixe, p.W - 1);
+    v[NR] = *reinterpret_cast<const uint2*>(src_b + (iyc * p.W + ixc2) * p.C);
+    okm |= (uint32_t)ok << NR;
+  }
 }
 
 CFL_DEVICE uint2 xform4(uint2 t, bool on, const float* a4, const float* b4, int relu) {
@@ -241,13 +249,15 @@ CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int slot = slot0 + r >= NRING ? slot0 + r - NRING : slot0 + r;
-    *reinterpret_cast<uint2*>(col + slot * HWp * LDP) = xform4(v[r], xform && ((okm >> r) & 1u), a4, b4, relu);
+    const bool ok = (okm >> r) & 1u;
+    *reinterpret_cast<uint2*>(col + slot * HWp * LDP) = xform4(ok ? v[r] : make_uint2(0, 0), xform && ok, a4, b4, relu);
   }
   if (tid < 2 * G * NR) {
     const int re = tid / (2 * G), hxe = TW + (tid % (2 * G)) / G;
     const int slot = slot0 + re >= NRING ? slot0 + re - NRING : slot0 + re;
+    const bool ok = (okm >> NR) & 1u;
     *reinterpret_cast<uint2*>(sH + (slot * HWp + hxe) * LDP + q * CPT) =
-        xform4(v[NR], xform && ((okm >> NR) & 1u), a4, b4, relu);
+        xform4(ok ? v[NR] : make_uint2(0, 0), xform && ok, a4, b4, relu);
   }
 }
 }  // namespace dws
@@ -556,10 +566,23 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     fetch<SR + 2>(g_b, p, x0, ybeg - 1, true, v, okv);
     fetch<SR + 2>(x_b, p, x0, ybeg - 1, true, u, oku);
     put<SR + 2>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
-    put<SR + 2>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);
+    put<SR + 2>(sX, u, oku, ybeg - 1, false, a4, b4, 0);        // raw x: transformed where read (xt below)
   }
   __syncthreads();
 
+  // the producer's BN-apply + ReLU of an x ring value at image position (iy, ix), rounded to bf16 exactly as the
+  // single-pass kernels' staging does (put / xform4); zero padding outside the image
+  auto xt = [&](float* f, bool inside) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = fmaf(a4[j], f[j], b4[j]);
+      if (relu) t = fmaxf(t, 0.f);
+      f[j] = t;
+    }
+    uint2 r = pack4(f);
+    if (!inside) r = make_uint2(0, 0);
+    unpack4(r, f);
+  };
   float accw[9][4], s0[4], s1[4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -569,12 +592,25 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
   for (int j = 0; j < 4; ++j) s0[j] = s1[j] = 0.f;
   uint2 rg[SR + 1], rx[SR + 1];
   uint32_t okg = 0, okx = 0;
+  const bf16_t* hsrc = p.add_half ? p.add_half : p.dy;
   for (int s = 0; s < nsteps; ++s) {
     const int a = ybeg + s * SR;
     const bool more = s + 1 < nsteps;
+    const int oy = a + sr;
+    // this step's residual half-resolution gradient (even pixels) is loaded BEFORE the ring prefetch: the epilogue's
+    // wait for it then leaves the next step's rows in flight (the node's y is the raw x ring's centre row)
+    const size_t eoff = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+    uint2 hr[SL / 2];
+#pragma unroll
+    for (int i = 0; i < SL / 2; ++i) {                      // x0 + sc is a multiple of 4: even pixels are i = 0, 2
+      // loaded unconditionally (clamped; from dy - a larger tensor - when there is no residual): see fetch
+      const int xx = x0 + sc + 2 * i;
+      const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
+      const int hy = min(oy, p.H - 1) >> 1, hx = min(xx, p.W - 1) >> 1;
+      hr[i] = *reinterpret_cast<const uint2*>(hsrc + (((size_t)b * Hh + hy) * Wh + hx) * p.C + c0);
+    }
     fetch<SR>(g_b, p, x0, a + SR + 1, more, rg, okg);       // next step's rows, in flight during this step
     fetch<SR>(x_b, p, x0, a + SR + 1, more, rx, okx);
-    const int oy = a + sr;
     const float live = oy < yend ? 1.f : 0.f;              // rows past the segment belong to the next block
     float acc[SL][4], g[SL][4];
 #pragma unroll
@@ -612,10 +648,12 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     for (int ky = 0; ky < 3; ++ky) {
       const int slot = (oy - 1 + ky + NRING) % NRING;
       const bf16_t* hrow = &sX[(slot * HWp + sc) * LDP + cg * CPT];
+      const bool rin = (unsigned)(oy - 1 + ky) < (unsigned)p.H;
 #pragma unroll
       for (int cx = 0; cx < SL + 2; ++cx) {
         float f[4];
         unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+        xt(f, rin && (unsigned)(x0 + sc + cx - 1) < (unsigned)p.W);
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int o = cx - kx;
@@ -627,7 +665,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       __builtin_amdgcn_sched_barrier(0);
     }
     if (oy < yend) {
-      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+      const size_t off0 = eoff;
 #pragma unroll
       for (int i = 0; i < SL; ++i)
         if (x0 + sc + i < p.W) {
@@ -636,17 +674,15 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
             float o[4];
             unpack4(v, o);
             if (p.mask_x) {                                  // transformed x at this pixel: the x ring's centre row
-              float xt[4];
-              unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), xt);
+              float xv[4];
+              unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), xv);
+              xt(xv, true);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) o[j] = xt[j] > 0.f ? o[j] : 0.f;
+              for (int j = 0; j < 4; ++j) o[j] = xv[j] > 0.f ? o[j] : 0.f;
             }
-            const int xx = x0 + sc + i;
-            if (p.add_half && ((oy | xx) & 1) == 0) {
-              const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
+            if (p.add_half && (i & 1) == 0 && (oy & 1) == 0) {   // (oy < yend, x < W hold here)
               float r[4];
-              unpack4(*reinterpret_cast<const uint2*>(
-                          p.add_half + (((size_t)b * Hh + (oy >> 1)) * Wh + (xx >> 1)) * p.C + c0), r);
+              unpack4(hr[i / 2], r);
 #pragma unroll
               for (int j = 0; j < 4; ++j) o[j] += r[j];
             }
@@ -660,7 +696,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
             load_f4(nc + 2 * CT, nmean);
             load_f4(nc + 3 * CT, nrstd);
             unpack4(v, o);
-            unpack4(*reinterpret_cast<const uint2*>(p.node.y + off0 + (size_t)i * p.C), y);
+            unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), y);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float gg = (!p.node.relu || fmaf(na[j], y[j], nb[j]) > 0.f) ? o[j] : 0.f;
@@ -675,7 +711,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     }
     if (more) {
       put<SR>(sG, rg, okg, a + SR + 1, false, a4, b4, 0);
-      put<SR>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
+      put<SR>(sX, rx, okx, a + SR + 1, false, a4, b4, 0);
     }
     __syncthreads();
   }
@@ -783,8 +819,10 @@ int dw_bwd(const DwParams& p, hipStream_t st) {
     const int rc = dw_dgrad(p, st);
     return rc ? rc : dw_wgrad(p, st);
   }
-  // two rings (56 KB LDS) and 247 VGPRs: 2 blocks per CU, so one round of resident blocks is 512 (the single-
-  // pass kernels' 768 left a half-empty second round)
+  // the fused pass takes the BN node's y from its raw x ring: the node must be the layer input itself
+  if (p.node.y != nullptr && p.node.y != p.x) return 1;
+  // two rings (56 KB LDS): 2 blocks per CU, so one round of resident blocks is 512 (the single-pass kernels' 768
+  // left a half-empty second round)
   int blocks, seg_rows;
   stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 512);
   hipLaunchKernelGGL(dw_bwd_stream_kernel, dim3(blocks), dim3(NT), 0, st, p, p.replicas > 1 ? p.replicas : 1,

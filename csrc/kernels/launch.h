@@ -374,6 +374,45 @@ int pack_fp8(const float* flat, uint8_t* packed8, float* scales, const PackView*
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
                  hipStream_t st, int* step = nullptr, int* cursor = nullptr);   // cursor: BatchSelect's, += 1
 
+// opt_step: the whole optimizer tail of a training step in ONE launch (adam_update + bn_moving_update + pack_weights
+// + the step / cursor advance), one block per work item:
+//   OI_FLAT    Adam over flat[src, src + n) (n <= 1024), trainable entries only (the params without GEMM views)
+//   OI_TILE    Adam over a 64x64 tile of a GEMM weight seen as a row-major [rows][cols] matrix at flat + src, then
+//              both bf16 views of the updated tile: the transpose (packed + dst_t)[c * rows + r] and the row-mapped
+//              copy (packed + dst_b)[(r % q) * s1 + (r / q) * s2 + base2 + c] - every pack_weights view is one of
+//              the two (1x1 conv / pointwise [cin][cout]: PK_CONV / PK_PW transpose, the dgrad views copies; ConvT
+//              (3,3,out,in) as [9 cout][cin]: PK_CONVT_DGRAD the transpose, PK_CONVT the tap-flipped row map)
+//   OI_MOVING  the BN moving statistics of one layer from its replica batch sums
+// The last block to finish (ticket) advances the Adam step and the batch cursor: every block has read the step.
+enum OptKind { OI_FLAT = 0, OI_TILE = 1, OI_MOVING = 2 };
+struct OptItem {
+  int kind;
+  int n;                   // flat: elements; moving: channels
+  int r0, c0, rows, cols;  // tile
+  int q, s1, s2, base2;    // tile: row map of the copy view
+  int64_t src;             // flat / tile: offset into the flat master buffer
+  int64_t dst_t, dst_b;    // tile: offsets into the bf16 pack buffer
+  const float* stats;      // moving: [STAT_REPLICAS][2][C] batch sums
+  float* mmean;
+  float* mvar;
+  float count;
+};
+struct OptParams {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  const uint8_t* trainable;
+  bf16_t* packed;
+  const OptItem* items;
+  int n_items;
+  float lr, b1, b2, eps, momentum;
+  int* step;
+  int* cursor;             // nullable
+  int* ticket;             // one int, zero between launches
+};
+int opt_step(const OptParams& p, hipStream_t st);
+
 // ---------------------------------------------------------------- step bookkeeping (optim.hip)
 // grad_finish: ONE launch at the end of backward for every gradient that was accumulated into replica rows
 // (GF_REDUCE: dst[i] += sum_r src[r*n + i], then the replicas are re-zeroed for the next step; GF_SUM: the same

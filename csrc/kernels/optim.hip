@@ -13,9 +13,21 @@ namespace {
 
 constexpr int NT = 256;
 
+// THE Adam element update (adam_kernel and opt_step share it). The moment updates are explicit fmas: left as
+// a*b + c*d, the compiler contracted them differently in the vectorised and the scalar kernel (m differed by an ulp
+// on ~5% of the elements); every other operation here feeds a division or a square root, nothing to contract.
+CFL_DEVICE void adam_elem(float& w, float g, float& m, float& v, float lr_t, float b1, float b2, float eps) {
+  m = fmaf(b1, m, (1.f - b1) * g);
+  v = fmaf(b2, v, (1.f - b2) * g * g);
+  w -= lr_t * m / (sqrtf(v) + eps);
+}
+CFL_DEVICE float adam_lr(const int* step, float lr, float b1, float b2) {
+  const int t = *step + 1;
+  return lr * sqrtf(1.f - powf(b2, (float)t)) / (1.f - powf(b1, (float)t));
+}
+
 __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
-  const int t = *p.step + 1;
-  const float lr_t = p.lr * sqrtf(1.f - powf(p.b2, (float)t)) / (1.f - powf(p.b1, (float)t));
+  const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
   const int64_t n4 = p.n / 4;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
     const uint32_t tm = *reinterpret_cast<const uint32_t*>(p.trainable + 4 * i);
@@ -31,9 +43,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!((tm >> (8 * j)) & 0xffu)) continue;
-      mp[j] = p.b1 * mp[j] + (1.f - p.b1) * gp[j];
-      vp[j] = p.b2 * vp[j] + (1.f - p.b2) * gp[j] * gp[j];
-      wp[j] -= lr_t * mp[j] / (sqrtf(vp[j]) + p.eps);
+      adam_elem(wp[j], gp[j], mp[j], vp[j], lr_t, p.b1, p.b2, p.eps);
     }
     reinterpret_cast<float4*>(p.p)[i] = w;
     reinterpret_cast<float4*>(p.m)[i] = m;
@@ -107,6 +117,106 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
       default: s = n * v.cout + k; break;                                       // pw dgrad: [N=c][K=f]
     }
     dst[e] = f2bf(src[s]);
+  }
+}
+
+// opt_step (launch.h): one block per OptItem. A thread that uses the step (lr_t) has its read completed before the
+// stores that depend on it, i.e. before the block's closing barrier and the ticket atomic (release, agent scope)
+// after it, so the last block advances the step only after every read of it.
+__global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
+  const OptItem it = p.items[blockIdx.x];
+  const int tid = threadIdx.x;
+  __shared__ float tl[64][65];
+  if (it.kind == OI_MOVING) {                           // bn_moving_kernel's update, replica sums in order
+    const int C = it.n;
+    const float mom = p.momentum;
+    for (int c = tid; c < C; c += NT) {
+      float va[STAT_REPLICAS], vb[STAT_REPLICAS];
+#pragma unroll
+      for (int r = 0; r < STAT_REPLICAS; ++r) {
+        va[r] = it.stats[r * 2 * C + c];
+        vb[r] = it.stats[r * 2 * C + C + c];
+      }
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < STAT_REPLICAS; ++r) {
+        s += va[r];
+        s2 += vb[r];
+      }
+      const float mean = s / it.count;
+      const float var = fmaxf(s2 / it.count - mean * mean, 0.f);
+      const float unbiased = var * (it.count / fmaxf(it.count - 1.f, 1.f));
+      it.mmean[c] = it.mmean[c] * mom + mean * (1.f - mom);
+      it.mvar[c] = it.mvar[c] * mom + unbiased * (1.f - mom);
+    }
+  } else if (it.kind == OI_FLAT) {
+    const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
+    float w[4], g[4], m[4], v[4];
+    bool on[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + u * NT;
+      const int64_t e = it.src + i;
+      on[u] = i < it.n && p.trainable[e];
+      w[u] = on[u] ? p.p[e] : 0.f;
+      g[u] = on[u] ? p.g[e] : 0.f;
+      m[u] = on[u] ? p.m[e] : 0.f;
+      v[u] = on[u] ? p.v[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!on[u]) continue;
+      const int64_t e = it.src + tid + u * NT;
+      adam_elem(w[u], g[u], m[u], v[u], lr_t, p.b1, p.b2, p.eps);
+      p.p[e] = w[u];
+      p.m[e] = m[u];
+      p.v[e] = v[u];
+    }
+  } else {
+    // 64x64 tile, thread (tx, ty) owns column c0 + tx of rows r0 + ty + 4j: coalesced 256-B rows of every fp32 array
+    const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
+    const int tx = tid & 63, ty = tid >> 6, c = it.c0 + tx;
+    const int64_t base = it.src;
+    float w[16], g[16], m[16], v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = it.r0 + ty + 4 * j;
+      const bool ok = r < it.rows && c < it.cols;
+      const int64_t e = base + (int64_t)r * it.cols + c;
+      w[j] = ok ? p.p[e] : 0.f;
+      g[j] = ok ? p.g[e] : 0.f;
+      m[j] = ok ? p.m[e] : 0.f;
+      v[j] = ok ? p.v[e] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = it.r0 + ty + 4 * j;
+      if (r < it.rows && c < it.cols) {
+        const int64_t e = base + (int64_t)r * it.cols + c;
+        adam_elem(w[j], g[j], m[j], v[j], lr_t, p.b1, p.b2, p.eps);
+        p.p[e] = w[j];
+        p.m[e] = m[j];
+        p.v[e] = v[j];
+        p.packed[it.dst_b + (int64_t)(r % it.q) * it.s1 + (int64_t)(r / it.q) * it.s2 + it.base2 + c] = f2bf(w[j]);
+      }
+      tl[ty + 4 * j][tx] = w[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int cc = it.c0 + ty + 4 * j, rr = it.r0 + tx;
+      if (cc < it.cols && rr < it.rows) p.packed[it.dst_t + (int64_t)cc * it.rows + rr] = f2bf(tl[tx][ty + 4 * j]);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(p.ticket, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (int)gridDim.x - 1) {                      // every block has read the step: advance it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      *p.ticket = 0;
+      *p.step += 1;
+      if (p.cursor != nullptr) *p.cursor += 1;
+    }
   }
 }
 
@@ -242,6 +352,12 @@ int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int
   int bx = (max_elems + NT - 1) / NT;
   if (bx > 256) bx = 256;
   hipLaunchKernelGGL(pack_kernel, dim3(bx, n_views), dim3(NT), 0, st, flat, packed, d_views, step, cursor);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int opt_step(const OptParams& p, hipStream_t st) {
+  if (p.n_items <= 0 || !p.ticket || !p.step) return 1;
+  hipLaunchKernelGGL(opt_step_kernel, dim3(p.n_items), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

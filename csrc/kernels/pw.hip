@@ -46,9 +46,37 @@ constexpr int pw_rows() { return K >= 128 ? 4096 / K : (S2 ? 32 : 64); }
 // S2: the input is the 2x2-block sum of p.sum2x2 (the decoder residual conv's upsample gradient): the four full-
 // resolution pixels of each B-fragment pixel are loaded and summed ((o00 + o01) + (o10 + o11), rounded once: node_bwd's
 // GM_SUM2X2), and the slice-0 blocks store the sums into x for the weight gradient.
-// bid / nblocks: this block's index among, and the number of, the launch's conv blocks (a multiple of 8)
-template <int NB, int K, int D, bool BWD, bool S2>
-CFL_DEVICE void pw_body(const ConvParams& p, int nslices, int bid, int nblocks) {
+// SIDE: the launch also carries an independent streaming pass (launch.h SideJob) whose blocks are interleaved with the
+// conv's in groups of 8, so a conv block keeps its dispatch-order XCD (block b -> XCD b % 8, which the slice mapping
+// below relies on) and both kinds are resident on every CU from the start: conv groups at even, side groups at odd
+// group positions while both last, then the remaining conv blocks, then the remaining side blocks. The conv code reads
+// the kernel argument p directly (a body function taking it by reference made the compiler copy it into registers at
+// entry: 182 -> 256 VGPRs and spills in the BN-backward form).
+template <int NB, int K, int D, bool BWD, bool S2 = false, int SIDE = SIDE_NONE>
+__global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices, int conv_blocks) {
+  int bid = blockIdx.x;
+  const int nblocks = conv_blocks;
+  if constexpr (SIDE != SIDE_NONE) {
+    const int side_blocks = gridDim.x - conv_blocks;
+    const int pairs = imin(conv_blocks >> 3, side_blocks >> 3);
+    const int b = blockIdx.x, grp = b >> 3;
+    bool conv;
+    int idx;
+    if (grp < 2 * pairs) {
+      conv = (grp & 1) == 0;
+      idx = (grp >> 1) * 8 + (b & 7);
+    } else {                                           // the rest: conv blocks first, then side blocks
+      const int rb = b - 16 * pairs, conv_rest = conv_blocks - 8 * pairs;
+      conv = rb < conv_rest;
+      idx = pairs * 8 + (conv ? rb : rb - conv_rest);
+    }
+    if (!conv) {
+      if constexpr (SIDE == SIDE_BBA) side::bba_body(p.side.bba, idx, side_blocks);
+      else side::node_pool_body<1>(p.side.pool, idx, side_blocks);
+      return;
+    }
+    bid = idx;
+  }
   constexpr int WR = pw_rows<K, S2>();
   constexpr int MF = WR / 16, NF = NB / 16, KS = K / 32;
   __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
@@ -249,34 +277,6 @@ CFL_DEVICE void pw_body(const ConvParams& p, int nslices, int bid, int nblocks) 
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
     atomicAdd(&rep[st * p.N + n0 + cc], v);
-  }
-}
-
-// The conv's blocks and (SIDE) the side job's blocks of one launch, interleaved in groups of 8 so a conv block keeps
-// its dispatch-order XCD (block b -> XCD b % 8, which pw_body's slice mapping relies on) and both kinds are resident
-// on every CU from the start: conv groups at even, side groups at odd group positions while both last, then the
-// remaining conv blocks, then the remaining side blocks.
-template <int NB, int K, int D, bool BWD, bool S2 = false, int SIDE = SIDE_NONE>
-__global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices, int conv_blocks) {
-  if constexpr (SIDE == SIDE_NONE) {
-    pw_body<NB, K, D, BWD, S2>(p, nslices, blockIdx.x, conv_blocks);
-  } else {
-    const int side_blocks = gridDim.x - conv_blocks;
-    const int pairs = imin(conv_blocks >> 3, side_blocks >> 3);
-    const int b = blockIdx.x, grp = b >> 3;
-    bool conv;
-    int idx;
-    if (grp < 2 * pairs) {
-      conv = (grp & 1) == 0;
-      idx = (grp >> 1) * 8 + (b & 7);
-    } else {                                           // the rest: conv blocks first, then side blocks
-      const int rb = b - 16 * pairs, conv_rest = conv_blocks - 8 * pairs;
-      conv = rb < conv_rest;
-      idx = pairs * 8 + (conv ? rb : rb - conv_rest);
-    }
-    if (conv) pw_body<NB, K, D, BWD, S2>(p, nslices, idx, conv_blocks);
-    else if constexpr (SIDE == SIDE_BBA) side::bba_body(p.side.bba, idx, side_blocks);
-    else side::node_pool_body<1>(p.side.pool, idx, side_blocks);
   }
 }
 
