@@ -226,7 +226,8 @@ class FLClient:
                     rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0), plane)
                 t2 = time.perf_counter()
                 phase = {"round": cr, "aggregate_s": t1 - t0, "upload_s": t2 - t1, "wait_s": 0.0,
-                         "payload_bytes": len(payload), "data_plane": plane or "grpc"}
+                         "payload_bytes": len(payload), "data_plane": plane or "grpc",
+                         "rank": self.aggregator.rank if self.aggregator is not None else -1}
                 st = rep.config["state"].scstring
                 print(f"### Received from state {st} ###")
                 if st == "RESP_ACY":

@@ -163,8 +163,11 @@ def test_rccl_device_path_sends_no_parameters(tmp_path):
     assert np.isclose(res["c0"][1], 8.0) and np.isclose(res["c1"][1], 8.0)       # (see the two-process test)
     assert np.isclose(srv.state.global_flat[table.entries[0].offset], 8.0)
     assert all(p["data_plane"] == "rccl" for ph in phases.values() for p in ph)
-    assert [p["payload_bytes"] for p in phases[1]] == [0, 0]                       # rank 1 uploads nothing
-    assert all(p["payload_bytes"] > 0 for p in phases[0])
+    # ranks follow registration order, not the client names: look the ranks up in the phase records
+    by_rank = {ph[0]["rank"]: ph for ph in phases.values()}
+    assert sorted(by_rank) == [0, 1] and all(len({p["rank"] for p in ph}) == 1 for ph in phases.values())
+    assert [p["payload_bytes"] for p in by_rank[1]] == [0, 0]                      # rank 1 uploads nothing
+    assert all(p["payload_bytes"] > 0 for p in by_rank[0])
     # round 1's reply (RESP_ARY or NOT_WAIT) carried no parameters to either client
     assert all(p.get("reply_bytes", 0) == 0 for ph in phases.values() for p in ph), phases
 
