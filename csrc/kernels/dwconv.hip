@@ -526,6 +526,12 @@ __global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) 
 // a block keeps TWO rings (dy raw, x with the producer's BN-apply + ReLU) and takes the wgrad's dy strip from the
 // centre row of the dy ring: dy and x are each read once per segment instead of dy twice + x twice (separate dgrad
 // with a BN-node epilogue reading x again, and wgrad), and one launch per layer instead of two.
+// The x ring holds the TRANSFORMED input (BN-apply + ReLU once per staged element; the wgrad reads each element 4.5
+// times, so transforming where read cost ~200 VALU ops per thread-step). NODE (the input is the BN node itself): the
+// node epilogue's raw y of this step's 4 output pixels is loaded at the top of the step, ahead of the ring prefetch,
+// so the epilogue's wait for it leaves the next step's rows in flight (they are rows the ring fetched a step ago:
+// L2 hits).
+template <bool NODE>
 __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int replicas, int seg_rows) {
   using namespace dws;
   __shared__ __attribute__((aligned(16))) bf16_t sG[NRING * HWp * LDP];   // dy rows
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     const int t = e / CT, c = e - t * CT;
     sW[e] = p.w[(8 - t) * p.C + cbase + c];
   }
-  const bool node = p.node.y != nullptr;
+  constexpr bool node = NODE;
   if (node && tid < 4 * CT) sNode[tid] = p.node.ab[(tid / CT) * p.C + cbase + tid % CT];
   {
     uint2 v[SR + 3], u[SR + 3];
@@ -566,23 +572,10 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     fetch<SR + 2>(g_b, p, x0, ybeg - 1, true, v, okv);
     fetch<SR + 2>(x_b, p, x0, ybeg - 1, true, u, oku);
     put<SR + 2>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
-    put<SR + 2>(sX, u, oku, ybeg - 1, false, a4, b4, 0);        // raw x: transformed where read (xt below)
+    put<SR + 2>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);   // transformed x (padding stays zero)
   }
   __syncthreads();
 
-  // the producer's BN-apply + ReLU of an x ring value at image position (iy, ix), rounded to bf16 exactly as the
-  // single-pass kernels' staging does (put / xform4); zero padding outside the image
-  auto xt = [&](float* f, bool inside) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float t = fmaf(a4[j], f[j], b4[j]);
-      if (relu) t = fmaxf(t, 0.f);
-      f[j] = t;
-    }
-    uint2 r = pack4(f);
-    if (!inside) r = make_uint2(0, 0);
-    unpack4(r, f);
-  };
   float accw[9][4], s0[4], s1[4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -608,6 +601,13 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
       const int hy = min(oy, p.H - 1) >> 1, hx = min(xx, p.W - 1) >> 1;
       hr[i] = *reinterpret_cast<const uint2*>(hsrc + (((size_t)b * Hh + hy) * Wh + hx) * p.C + c0);
+    }
+    uint2 yr[NODE ? SL : 1];                                 // the node's raw y at this step's output pixels
+    if constexpr (NODE) {
+      const int yy = min(oy, p.H - 1);
+#pragma unroll
+      for (int i = 0; i < SL; ++i)
+        yr[i] = *reinterpret_cast<const uint2*>(x_b + (yy * p.W + min(x0 + sc + i, p.W - 1)) * p.C);
     }
     fetch<SR>(g_b, p, x0, a + SR + 1, more, rg, okg);       // next step's rows, in flight during this step
     fetch<SR>(x_b, p, x0, a + SR + 1, more, rx, okx);
@@ -648,12 +648,10 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     for (int ky = 0; ky < 3; ++ky) {
       const int slot = (oy - 1 + ky + NRING) % NRING;
       const bf16_t* hrow = &sX[(slot * HWp + sc) * LDP + cg * CPT];
-      const bool rin = (unsigned)(oy - 1 + ky) < (unsigned)p.H;
 #pragma unroll
       for (int cx = 0; cx < SL + 2; ++cx) {
         float f[4];
         unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
-        xt(f, rin && (unsigned)(x0 + sc + cx - 1) < (unsigned)p.W);
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int o = cx - kx;
@@ -676,7 +674,6 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
             if (p.mask_x) {                                  // transformed x at this pixel: the x ring's centre row
               float xv[4];
               unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), xv);
-              xt(xv, true);
 #pragma unroll
               for (int j = 0; j < 4; ++j) o[j] = xv[j] > 0.f ? o[j] : 0.f;
             }
@@ -688,18 +685,17 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
             }
             v = pack4(o);
           }
-          if (node) {                                        // g = mask * o (o already bf16) + BN-backward sums
-            float o[4], y[4], na[4], nb[4], nmean[4], nrstd[4];
+          if constexpr (NODE) {                              // g = mask * o (o already bf16) + BN-backward sums
+            // (the node's BN is the input transform's: its scale / shift are a4 / b4, checked by dw_bwd)
+            float o[4], y[4], nmean[4], nrstd[4];
             const float* nc = &sNode[cg * CPT];
-            load_f4(nc, na);
-            load_f4(nc + CT, nb);
             load_f4(nc + 2 * CT, nmean);
             load_f4(nc + 3 * CT, nrstd);
             unpack4(v, o);
-            unpack4(*reinterpret_cast<const uint2*>(&sX[((oy % NRING) * HWp + sc + i + 1) * LDP + cg * CPT]), y);
+            unpack4(yr[i], y);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const float gg = (!p.node.relu || fmaf(na[j], y[j], nb[j]) > 0.f) ? o[j] : 0.f;
+              const float gg = (!relu || fmaf(a4[j], y[j], b4[j]) > 0.f) ? o[j] : 0.f;
               o[j] = gg;
               s0[j] += gg;
               s1[j] += gg * (y[j] - nmean[j]) * nrstd[j];
@@ -711,7 +707,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     }
     if (more) {
       put<SR>(sG, rg, okg, a + SR + 1, false, a4, b4, 0);
-      put<SR>(sX, rx, okx, a + SR + 1, false, a4, b4, 0);
+      put<SR>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
     }
     __syncthreads();
   }
@@ -820,13 +816,15 @@ int dw_bwd(const DwParams& p, hipStream_t st) {
     return rc ? rc : dw_wgrad(p, st);
   }
   // the fused pass takes the BN node's y from its raw x ring: the node must be the layer input itself
-  if (p.node.y != nullptr && p.node.y != p.x) return 1;
+  if (p.node.y != nullptr && (p.node.y != p.x || p.node.ab != p.xf.ab || p.node.relu != p.xf.relu)) return 1;
   // two rings (56 KB LDS): 2 blocks per CU, so one round of resident blocks is 512 (the single-pass kernels' 768
   // left a half-empty second round)
   int blocks, seg_rows;
   stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 512);
-  hipLaunchKernelGGL(dw_bwd_stream_kernel, dim3(blocks), dim3(NT), 0, st, p, p.replicas > 1 ? p.replicas : 1,
-                     seg_rows);
+  if (p.node.y) hipLaunchKernelGGL(dw_bwd_stream_kernel<true>, dim3(blocks), dim3(NT), 0, st, p,
+                                   p.replicas > 1 ? p.replicas : 1, seg_rows);
+  else hipLaunchKernelGGL(dw_bwd_stream_kernel<false>, dim3(blocks), dim3(NT), 0, st, p,
+                          p.replicas > 1 ? p.replicas : 1, seg_rows);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -1634,7 +1634,8 @@ def test_dw_wgrad_batch_grouped_equals_individual():
 def test_dw_bwd_fused_matches_dgrad_and_wgrad(B, H, W, C, node, relu):
     """dw_bwd (depthwise dgrad + BN-node epilogue + wgrad of one layer in one row-streaming pass with a dy ring and an
     x ring) equals dw_dgrad (bit for bit: same arithmetic) and dw_wgrad (up to float atomic order), on ragged maps
-    (segments / strips that end inside a step) and with / without the node epilogue."""
+    (segments / strips that end inside a step) and with / without the node epilogue. With the node, the layer input IS
+    the node (the engine's use: x = y, its transform = the node's BN + ReLU), which the fused kernel requires."""
     torch.manual_seed(47)
     C_ = hip()
     xb, _ = bf(torch.randn(B, H, W, C))
@@ -1646,15 +1647,16 @@ def test_dw_bwd_fused_matches_dgrad_and_wgrad(B, H, W, C, node, relu):
     nab = nab.to(DEV)
     reps = 32
     kw = lambda sums: dict(node_y=xb, node_ab=nab, node_sums=sums, node_reps=4, node_relu=relu) if node else {}
+    xab, xrelu = (nab, relu) if node else (ab, 1)
     dx_ref = torch.zeros_like(gb)
     sums_ref = torch.zeros(4 * 2 * C, device=DEV)
     C_.dw_dgrad(gb, w, dx_ref, B, H, W, C, 0, **kw(sums_ref))
     dw_ref = torch.zeros(reps * 9 * C, device=DEV)
-    C_.dw_wgrad(xb, gb, dw_ref, ab, 1, B, H, W, C, reps)
+    C_.dw_wgrad(xb, gb, dw_ref, xab, xrelu, B, H, W, C, reps)
     dx = torch.zeros_like(gb)
     sums = torch.zeros(4 * 2 * C, device=DEV)
     dw = torch.zeros(reps * 9 * C, device=DEV)
-    C_.dw_bwd(xb, ab, 1, gb, w, dx, dw, reps, B, H, W, C, **kw(sums))
+    C_.dw_bwd(xb, xab, xrelu, gb, w, dx, dw, reps, B, H, W, C, **kw(sums))
     torch.cuda.synchronize()
     assert torch.equal(dx, dx_ref), int((dx != dx_ref).sum())
     assert torch.allclose(dw.view(reps, -1).sum(0), dw_ref.view(reps, -1).sum(0), rtol=1e-4, atol=1e-3)
