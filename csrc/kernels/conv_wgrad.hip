@@ -78,32 +78,25 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
     doh[i] = r / p.Wo;
     dow[i] = r - doh[i] * p.Wo;
   }
+  // loaded RAW and branch-free (clamped addresses, validity bits); masked + transformed in store(), after the MFMAs
+  // that the prefetch should overlap (see wgrad3_body.h)
   uint4 rx[XPT], rg[GPT];
+  uint32_t xval = 0, gval = 0;
   auto load = [&](int m0) {
+    xval = 0;
+    gval = 0;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int ch = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
       const int m = m0 + ch / XW;
-      if (ch < XC && m < m_end) {
-        const int b = db[i], oh = doh[i], ow = dow[i];
-        const int ih = oh * p.stride - p.pad_t + ky, iw = ow * p.stride - p.pad_l + kx;
-        if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
-          v = *reinterpret_cast<const uint4*>(
-              p.x + (((size_t)b * p.Hin + (ih >> p.up_in)) * p.Win + (iw >> p.up_in)) * p.Cin + xc);
-          if (has_ab || p.xf.relu) {
-            float f[8];
-            unpack8(v, f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              f[j] = fmaf(ca[j], f[j], cb[j]);
-              if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
-            }
-            v = pack8(f);
-          }
-        }
-      }
-      rx[i] = v;
+      const int b = db[i], oh = doh[i], ow = dow[i];
+      const int ih = oh * p.stride - p.pad_t + ky, iw = ow * p.stride - p.pad_l + kx;
+      const bool ok = ch < XC && m < m_end && ih >= 0 && ih < Hl && iw >= 0 && iw < Wl;
+      // (rows past m_end decode past the last image: clamp the image too)
+      const int bc = imin(b, p.B - 1), ihc = imin(imax(ih, 0), Hl - 1), iwc = imin(imax(iw, 0), Wl - 1);
+      rx[i] = *reinterpret_cast<const uint4*>(
+          p.x + (((size_t)bc * p.Hin + (ihc >> p.up_in)) * p.Win + (iwc >> p.up_in)) * p.Cin + xc);
+      xval |= (uint32_t)ok << i;
       dow[i] += RM;                       // advance this chunk row to the next step's pixel
       while (dow[i] >= p.Wo) {
         dow[i] -= p.Wo;
@@ -117,20 +110,37 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
     for (int i = 0; i < GPT; ++i) {
       const int ch = tid + i * NT;
       const int m = m0 + ch / GW;
-      rg[i] = (ch < GC && m < m_end) ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.N + gn)
-                                     : make_uint4(0, 0, 0, 0);
+      const bool ok = ch < GC && m < m_end;
+      rg[i] = *reinterpret_cast<const uint4*>(p.dy + (size_t)imin(m, p.M - 1) * p.N + gn);
+      gval |= (uint32_t)ok << i;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int ch = tid + i * NT;
-      if (ch < XC) *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = rx[i];
+      if (ch < XC) {
+        uint4 v = rx[i];
+        if (!((xval >> i) & 1u)) {
+          v = make_uint4(0, 0, 0, 0);
+        } else if (has_ab || p.xf.relu) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            f[j] = fmaf(ca[j], f[j], cb[j]);
+            if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
+          }
+          v = pack8(f);
+        }
+        *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {
       const int ch = tid + i * NT;
-      if (ch < GC) *reinterpret_cast<uint4*>(&sG[buf][ch / GW][(ch % GW) * 8]) = rg[i];
+      if (ch < GC) *reinterpret_cast<uint4*>(&sG[buf][ch / GW][(ch % GW) * 8]) = ((gval >> i) & 1u) ? rg[i]
+                                                                                                  : make_uint4(0, 0, 0, 0);
     }
   };
 

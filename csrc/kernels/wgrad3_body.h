@@ -49,59 +49,70 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
   load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
   load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
 
+  // The next tile's halo / dy chunks are loaded RAW, branch-free (clamped in-image addresses, a validity bit per
+  // chunk) and only masked + transformed (producer BN-apply + ReLU) in store(), after the current tile's MFMAs:
+  // transformed right after the load, the prefetch was consumed at issue and every tile waited its full load
+  // latency (~2.4 us per 128-pixel tile against ~0.5 us of MFMAs).
   uint4 rh[H_PER_T], rd[D_PER_T];
+  uint32_t hval = 0, dval = 0;
   auto load = [&](int t) {
     const int b = t / (tiles_w * tiles_h);
     const int r = t - b * tiles_w * tiles_h;
     const int ty0 = (r / tiles_w) * TH, tx0 = (r % tiles_w) * TW;
+    hval = 0;
+    dval = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < HALO_CH) {
-        const int hp = e >> 2, q = e & 3;
-        const int hy = hp / HW, hx = hp - hy * HW;
-        const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
-        if (iy >= 0 && iy < Hl && ix >= 0 && ix < Wl) {
-          v = *reinterpret_cast<const uint4*>(
-              p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + cbase + q * 8);
-          if (has_ab || p.xf.relu) {
-            float f[8];
-            unpack8(v, f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              if (has_ab) f[j] = fmaf(a8[j], f[j], b8[j]);
-              if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
-            }
-            v = pack8(f);
-          }
-        }
-      }
-      rh[i] = v;
+      const int ec = e < HALO_CH ? e : HALO_CH - 1;
+      const int hp = ec >> 2, q = ec & 3;
+      const int hy = hp / HW, hx = hp - hy * HW;
+      const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
+      const bool ok = e < HALO_CH && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+      const int iyc = imin(imax(iy, 0), Hl - 1), ixc = imin(imax(ix, 0), Wl - 1);
+      rh[i] = *reinterpret_cast<const uint4*>(
+          p.x + (((size_t)b * p.Hin + (iyc >> p.up_in)) * p.Win + (ixc >> p.up_in)) * p.Cin + cbase + q * 8);
+      hval |= (uint32_t)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < D_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < D_CH) {
-        const int pp = e / (BNO / 8), q = e % (BNO / 8);
-        const int oy = ty0 + pp / TW, ox = tx0 + pp % TW;
-        if (oy < p.Ho && ox < p.Wo)
-          v = *reinterpret_cast<const uint4*>(p.dy + (((size_t)b * p.Ho + oy) * p.Wo + ox) * p.N + nBlock + q * 8);
-      }
-      rd[i] = v;
+      const int ec = e < D_CH ? e : D_CH - 1;
+      const int pp = ec / (BNO / 8), q = ec % (BNO / 8);
+      const int oy = ty0 + pp / TW, ox = tx0 + pp % TW;
+      const bool ok = e < D_CH && oy < p.Ho && ox < p.Wo;
+      rd[i] = *reinterpret_cast<const uint4*>(
+          p.dy + (((size_t)b * p.Ho + imin(oy, p.Ho - 1)) * p.Wo + imin(ox, p.Wo - 1)) * p.N + nBlock + q * 8);
+      dval |= (uint32_t)ok << i;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < HALO_CH) *reinterpret_cast<uint4*>(&sH[buf][e >> 2][(e & 3) * 8]) = rh[i];
+      if (e < HALO_CH) {
+        uint4 v = rh[i];
+        if (!((hval >> i) & 1u)) {
+          v = make_uint4(0, 0, 0, 0);                 // padding stays exactly 0 (TF SAME pads the transformed input)
+        } else if (has_ab || p.xf.relu) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (has_ab) f[j] = fmaf(a8[j], f[j], b8[j]);
+            if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
+          }
+          v = pack8(f);
+        }
+        *reinterpret_cast<uint4*>(&sH[buf][e >> 2][(e & 3) * 8]) = v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < D_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < D_CH) *reinterpret_cast<uint4*>(&sD[buf][e / (BNO / 8)][(e % (BNO / 8)) * 8]) = rd[i];
+      if (e < D_CH)
+        *reinterpret_cast<uint4*>(&sD[buf][e / (BNO / 8)][(e % (BNO / 8)) * 8]) =
+            ((dval >> i) & 1u) ? rd[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
