@@ -276,6 +276,17 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_group_kernel(const WgradGrou
 int wgrad_config(const WgradParams& p, int& bko, int& bno, int& rm) {
   const bool k128 = p.K % 128 == 0, n128 = p.N % 128 == 0;
   if (k128 && n128 && (int64_t)p.K * p.N >= 128 * 128 * 16) { bko = 128; bno = 128; rm = 32; return 0; }
+  // K, N % 128 == 0 at large M (the wide pointwise / residual layers at 512^2): 128x128 output tiles with 64-pixel
+  // stages - each operand is re-read N/128 resp. K/128 times instead of N/64, K/64 and a wave issues 16 MFMAs per
+  // 32-pixel k-step instead of 4. tools/kbench.py at 512^2 / batch 256: 64x64 / 128x128 (32-px stages) / 128x128
+  // (64-px stages) = 890.7 / 454.8 / 382.4 us (64^2, 256->256), 902.8 / 492.0 / 388.2 us (128^2, 128->128),
+  // 224.9 / 120.0 / 115.1 us (32^2, 256->256). TUNE_WGRAD1_BIG: 1 = 64x64 tiles, 2 = 32-pixel stages.
+  const int big = cfl_tune(TUNE_WGRAD1_BIG);
+  if (big != 1 && k128 && n128 && p.M >= 65536) {
+    bko = 128; bno = 128;
+    rm = big == 2 ? 32 : 64;
+    return big == 2 ? 0 : 6;
+  }
   rm = 128;
   if (p.K % 64 == 0 && p.N % 64 == 0) {
     bko = 64; bno = 64;
@@ -331,7 +342,8 @@ struct MixGroup {
   int xcd;                  // XCD-grouped block order (TUNE_WGRAD_MIX_XCD != 1)
 };
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int MIX_LDS = cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wgrad_lds_bytes<128, 128, 32>()),
+constexpr int MIX_LDS = cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wgrad_lds_bytes<128, 128, 32>()),
+                                  wgrad_lds_bytes<128, 128, 64>()),
                              cmax(cmax(wgrad_lds_bytes<64, 32, 128>(), wgrad_lds_bytes<32, 64, 128>()),
                                   cmax(wgrad_lds_bytes<32, 32, 128>(), wgrad_lds_bytes<64, 64, 64>())));
 static_assert(MIX_LDS <= 80 * 1024, "two mixed blocks per CU");
@@ -357,6 +369,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
     case 2: wg3::wgrad3_body<32, true>(P, a, b, bx, by, bz, smem); break;
     case 3: wg3::wgrad3_body<32, false>(P, a, b, bx, by, bz, smem); break;
     case 10: wgrad_body<128, 128, 32>(P, a, bx, by, bz, smem); break;
+    case 16: wgrad_body<128, 128, 64>(P, a, bx, by, bz, smem); break;
     case 12: wgrad_body<64, 32, 128>(P, a, bx, by, bz, smem); break;
     case 13: wgrad_body<32, 64, 128>(P, a, bx, by, bz, smem); break;
     case 14: wgrad_body<32, 32, 128>(P, a, bx, by, bz, smem); break;
@@ -439,8 +452,8 @@ static bool mix_ok(const WgradParams& p) {
 
 
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
-  static thread_local WgradParams by_cfg[4][16], gen_cfg[6][32];
-  int cnt[4] = {0, 0, 0, 0}, gcnt[6] = {0, 0, 0, 0, 0, 0};
+  static thread_local WgradParams by_cfg[4][16], gen_cfg[7][32];
+  int cnt[4] = {0, 0, 0, 0}, gcnt[7] = {0, 0, 0, 0, 0, 0, 0};
   const bool group = cfl_tune(TUNE_WGRAD_GROUP) != 1;
   const bool group1 = group && cfl_tune(TUNE_WGRAD_GROUP) != 2;
   if (group1 && cfl_tune(TUNE_WGRAD_MIX) != 1) {            // default: one mixed launch (plus any odd ones out)
@@ -474,11 +487,12 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
       if (rc) return rc;
     }
   }
-  for (int c = 0; c < 6; ++c) {
+  for (int c = 0; c < 7; ++c) {
     if (!gcnt[c]) continue;
     int rc;
     switch (c) {
       case 0: rc = launch_group<128, 128, 32>(gen_cfg[c], gcnt[c], st); break;
+      case 6: rc = launch_group<128, 128, 64>(gen_cfg[c], gcnt[c], st); break;
       case 1: rc = launch_group<64, 64, 128>(gen_cfg[c], gcnt[c], st); break;
       case 5: rc = launch_group<64, 64, 64>(gen_cfg[c], gcnt[c], st); break;
       case 2: rc = launch_group<64, 32, 128>(gen_cfg[c], gcnt[c], st); break;
@@ -502,6 +516,7 @@ int conv_wgrad(const WgradParams& p, hipStream_t st) {
   int bko, bno, rm;
   switch (wgrad_config(p, bko, bno, rm)) {
     case 0: launch<128, 128>(p, st); break;
+    case 6: launch<128, 128, 64>(p, st); break;
     case 1: launch<64, 64, 128>(p, st); break;
     case 5: launch<64, 64, 64>(p, st); break;
     case 2: launch<64, 32, 128>(p, st); break;

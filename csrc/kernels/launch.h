@@ -481,7 +481,9 @@ enum TuneKey {
   TUNE_SEP_BLOCKS = 34,        // fused SeparableConv forward: target grid size (default 512)
   TUNE_WGRAD_MIX_XCD = 35,     // mixed wgrad launch: 0 = XCD-grouped block order, 1 = dispatch order
   TUNE_SIDE = 36,              // streaming 1x1 dgrads: 0 = co-launch their side job (SideJob), 1 = run it alone first
-  TUNE_N = 37
+  TUNE_WGRAD1_BIG = 37,        // generic wgrad, K and N % 128 == 0 at M >= 64k: 0 = 128x128 tiles, 64-pixel stages;
+                               // 1 = 64x64 tiles; 2 = 128x128 tiles, 32-pixel stages
+  TUNE_N = 38
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -145,6 +145,35 @@ def test_conv_wgrad_1x1_and_up(stride, up):
     assert rel(dw.view(1, 1, Cin, N).cpu(), w.grad) < 2e-2
 
 
+@pytest.mark.parametrize("big", [0, 1, 2])
+@pytest.mark.parametrize("stride,Cin,N,use_ab", [(1, 128, 128, True), (2, 128, 256, False)])
+def test_conv_wgrad_wide_tiles_match_autograd(big, stride, Cin, N, use_ab):
+    """Generic 1x1 wgrad at M >= 64k pixels with K, N % 128 == 0 (the 512^2 wide layers): 128x128 tiles with 64-pixel
+    stages (default), 64x64 tiles (TUNE_WGRAD1_BIG = 1) and 128x128 with 32-pixel stages (2) against fp32 autograd,
+    BN-apply + ReLU on the input included; a ragged last pixel chunk (M not a multiple of the stage)."""
+    torch.manual_seed(23)
+    C_ = hip()
+    B, H = 5, 116 if stride == 1 else 232          # M = 67,280 output pixels
+    Ho = H // stride
+    xb, xf = bf(torch.randn(B, H, H, Cin))
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, N))
+    ab, a, b = ab_for(Cin, 29)
+    xin = xf.permute(0, 3, 1, 2)
+    if use_ab:
+        xin = torch.relu(xin * a.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)).to(torch.bfloat16).float()
+    w = torch.zeros(1, 1, Cin, N, requires_grad=True)
+    out = R.conv2d_same(xin, w, None, stride).permute(0, 2, 3, 1)
+    (out * dyf).sum().backward()
+    dw = torch.zeros(Cin * N, device=DEV)
+    C_.set_tune(C_.TUNE_WGRAD1_BIG, big)
+    try:
+        C_.conv_wgrad(xb, dyb, dw, ab.to(DEV) if use_ab else None, 1 if use_ab else 0, B, H, H, Cin, 0, Ho, Ho, N, 1,
+                      stride, 0, 0, 0, 0)
+    finally:
+        C_.set_tune(C_.TUNE_WGRAD1_BIG, 0)
+    assert rel(dw.view(1, 1, Cin, N).cpu(), w.grad) < 1e-2
+
+
 # algo 0 = row-streaming LDS ring (stream_blocks = grid target: 1 -> one segment per column strip, so a block walks
 # every row step of the image), 1 = generic row strips
 @pytest.mark.parametrize("B,H,C,algo,stream_blocks", [(2, 10, 64, 0, 0), (2, 10, 64, 1, 0), (3, 37, 32, 0, 0),
