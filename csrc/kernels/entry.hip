@@ -404,7 +404,11 @@ int entry_fwd(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
-  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS) : 512;   // A/B-measured
+  // grid cap: 512 at 256^2 / batch 16 (2,048 row steps; A/B-measured - fewer same-address statistics atomics); the
+  // many-step problems (512^2 planned batch: 561k steps) need more resident blocks to hide each block's one-step-ahead
+  // row prefetch: kbench 512^2 / b256 cap 512 / 1,024 / 2,048 = 583 / 432 / 424 us
+  const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS)
+                                                     : rows * ((p.Wo + ECH - 1) / ECH) >= 65536 ? 2048 : 512;
   if (use_mfma(p)) {
     const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
     hipLaunchKernelGGL(entry_fwd_mfma_kernel, dim3(steps < cap ? steps : cap), dim3(NT), 0, st, p, nch, steps);
@@ -443,7 +447,9 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
   }
   if (use_mfma(p)) {
     const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
-    const int mcap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) : 512;
+    // (as entry_fwd: 512 at 256^2 / b16; kbench 512^2 / b256 cap 512 / 1,024 / 2,048 = 521 / 487 / 420 us)
+    const int mcap = cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_WGRAD_BLOCKS)
+                                                           : steps >= 65536 ? 2048 : 512;
     const dim3 grid(steps < mcap ? steps : mcap);
     if (p.bwd.y) hipLaunchKernelGGL(entry_wgrad_mfma_kernel<true>, grid, dim3(NT), 0, st, p, nch, steps, reps);
     else hipLaunchKernelGGL(entry_wgrad_mfma_kernel<false>, grid, dim3(NT), 0, st, p, nch, steps, reps);
