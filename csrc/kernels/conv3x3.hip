@@ -752,9 +752,11 @@ int launch(const ConvParams& p, int splits, hipStream_t st) {
                          per, splits > 1 ? p.ws : nullptr);
       return splits;
     }
-    if (p.pj.v) {
-      hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
-      return 1;
+    if constexpr (TH * TW / 4 <= NT / (BN_ / 8)) {     // (the node join needs one half-res pixel per thread)
+      if (p.pj.v) {
+        hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, true, true>), grid, dim3(NT), 0, st, p, per, nullptr);
+        return 1;
+      }
     }
   }
   hipLaunchKernelGGL((conv3x3_kernel<TH, TW, BN_, WM, WN, WB>), grid, dim3(NT), 0, st, p, per,
@@ -794,9 +796,19 @@ static bool small_tiles(const ConvParams& p) {
   return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
 }
 
+// Large-M layers (the 64^2 / 128^2 decoder levels at the 512^2 planned batch: 4.5-18M pixels, Cin 64-256): 16x16-
+// pixel tiles. The whole-chunk weight tile (9 taps x 64 x 32, 36 KB) is re-read from L2 for every pixel tile, and at
+// this M the 8x16 tiles ran at ~28 % of the MFMA peak on that L2 stream; 256 pixels per tile halve the weight bytes
+// per MFMA. TUNE_CONV3_BIG: 1 = off, 2 = whenever the shape allows.
+static bool big_tiles(const ConvParams& p) {
+  const int v = cfl_tune(TUNE_CONV3_BIG);
+  if (v == 1 || p.pj.v || !use_wb(p) || wb_bn(p) != 64 || p.Ho % 16 || p.Wo % 16) return false;
+  return v == 2 || (int64_t)p.B * p.Ho * p.Wo >= (1 << 22);
+}
+
 bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_splits(const ConvParams& p) {
-  return small_tiles(p) || ws_eligible(p) || conv3x3_deep_eligible(p)
+  return small_tiles(p) || ws_eligible(p) || conv3x3_deep_eligible(p) || big_tiles(p)
              ? 1 : conv3x3_split_k(p);
 }
 
@@ -856,6 +868,8 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   const bool w16 = p.Wo >= 16;
   if (small_tiles(p)) {
     splits = launch<8, 8, 32, 2, 2, true>(p, 1, st);
+  } else if (big_tiles(p)) {
+    splits = launch<16, 16, 64, 2, 2, true>(p, 1, st);
   } else if (use_wb(p) && wb_bn(p) == 64) {
     if (w16) splits = launch<8, 16, 64, 2, 2, true>(p, splits, st);
     else splits = launch<16, 8, 64, 2, 2, true>(p, splits, st);

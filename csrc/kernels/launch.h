@@ -483,7 +483,8 @@ enum TuneKey {
   TUNE_SIDE = 36,              // streaming 1x1 dgrads: 0 = co-launch their side job (SideJob), 1 = run it alone first
   TUNE_WGRAD1_BIG = 37,        // generic wgrad, K and N % 128 == 0 at M >= 64k: 0 = 128x128 tiles, 64-pixel stages;
                                // 1 = 64x64 tiles; 2 = 128x128 tiles, 32-pixel stages
-  TUNE_N = 38
+  TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 4M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
+  TUNE_N = 39
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -939,6 +939,18 @@ def test_conv3x3_small_tiles_forced(B, Hs, Cin, N, up, use_ab):
         hip().set_tune(hip().TUNE_CONV3_SMALL, 0)
 
 
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [(2, 16, 64, 64, 0, True), (2, 16, 128, 128, 1, False),
+                                                  (1, 32, 256, 64, 0, True)])
+def test_conv3x3_big_tiles_forced(B, Hs, Cin, N, up, use_ab):
+    """TUNE_CONV3_BIG=2 forces the 16x16-pixel tiles of the large-M layers (several chunks, upsampled input) vs the
+    generic implicit GEMM and the fp32 reference."""
+    hip().set_tune(hip().TUNE_CONV3_BIG, 2)
+    try:
+        test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
+    finally:
+        hip().set_tune(hip().TUNE_CONV3_BIG, 0)
+
+
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,grid", [
     (2, 16, 64, 32, 0, True, 0),     # 128^2-level shape family: CH 2, 8x16 tiles
     (2, 8, 32, 64, 1, False, 0),     # upsampled input, CH 1, two column blocks
