@@ -966,6 +966,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_SIDE") = (int)TUNE_SIDE;
   m.attr("TUNE_WGRAD1_BIG") = (int)TUNE_WGRAD1_BIG;
   m.attr("TUNE_CONV3_BIG") = (int)TUNE_CONV3_BIG;
+  m.attr("TUNE_PW_NB") = (int)TUNE_PW_NB;
   m.attr("TUNE_CONV3_SPLIT_BLOCKS") = (int)TUNE_CONV3_SPLIT_BLOCKS;
   m.attr("TUNE_CONV3_SPLIT_TARGET") = (int)TUNE_CONV3_SPLIT_TARGET;
   m.def("bn_finalize", &bn_finalize_op);

@@ -484,7 +484,9 @@ enum TuneKey {
   TUNE_WGRAD1_BIG = 37,        // generic wgrad, K and N % 128 == 0 at M >= 64k: 0 = 128x128 tiles, 64-pixel stages;
                                // 1 = 64x64 tiles; 2 = 128x128 tiles, 32-pixel stages
   TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 4M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
-  TUNE_N = 39
+  TUNE_PW_NB = 39,             // streaming 1x1 kernel, N % 128 == 0 and K >= 128: 0 = 128-channel output slices at
+                               // M >= 1M pixels (else 64), 64 = always 64, 128 = always 128
+  TUNE_N = 40
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

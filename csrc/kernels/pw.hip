@@ -297,7 +297,7 @@ void launch_d(const ConvParams& p, hipStream_t st) {
   const int waves = (tiles + tpw - 1) / tpw;
   const int bps = ((waves + 3) / 4 + 7) / 8 * 8;
   const int cb = bps * nslices;
-  if constexpr (D == 1) {
+  if constexpr (D == 1 && NB <= 64) {     // (the 128-wide slices serve the plain and BN-backward forms only)
     if (p.side.kind == SIDE_BBA) {                 // the decoder residual dgrads + the BN_B backward apply
       const dim3 g(cb + bn_bwd_apply_grid(p.side.bba));
       if (p.sum2x2) hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true, SIDE_BBA>), g, dim3(NT), 0, st, p, nslices, cb);
@@ -313,6 +313,8 @@ void launch_d(const ConvParams& p, hipStream_t st) {
       hipLaunchKernelGGL((pw_kernel<NB, K, 1, false, true>), dim3(cb), dim3(NT), 0, st, p, nslices, cb);
       return;
     }
+  }
+  if constexpr (D == 1) {
     if (bwd) {
       hipLaunchKernelGGL((pw_kernel<NB, K, 1, true>), dim3(cb), dim3(NT), 0, st, p, nslices, cb);
       return;
@@ -351,6 +353,17 @@ bool pw_conv_supported(const ConvParams& p) {
 int pw_conv(const ConvParams& p, hipStream_t st) {
   if (!pw_conv_supported(p)) return 1;
   const bool n32 = p.N == 32;
+  // 128-channel output slices for the wide layers at large M (the 512^2 planned batch): each N slice re-reads (and in
+  // the BN-backward form re-transforms) the whole input, so half the slices halve that traffic; whole step 5,581 ->
+  // 5,753 img/s at 512^2 / b1,096. At 256^2 / b16 (M <= 65k for these layers) they measured slower (13,046 / 13,050 vs
+  // 12,907 / 12,937: fewer blocks). TUNE_PW_NB: 64 = never, 128 = wherever the shape allows.
+  const int nbt = cfl_tune(TUNE_PW_NB);
+  if (nbt != 64 && p.N % 128 == 0 && p.Cin >= 128 && !p.sum2x2 && !p.side.kind &&
+      (nbt == 128 || p.M >= (1 << 20))) {
+    if (p.Cin == 128) launch<128, 128>(p, st);
+    else launch<128, 256>(p, st);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   switch (p.Cin) {
     case 32: n32 ? launch<32, 32>(p, st) : launch<64, 32>(p, st); break;
     case 64: n32 ? launch<32, 64>(p, st) : launch<64, 64>(p, st); break;

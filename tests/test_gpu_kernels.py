@@ -1539,6 +1539,8 @@ def test_folder_dataset_device_resize_matches_host(tmp_path):
     (1, 128, 128, 128, 4, None, False, False),       # 1x1: streaming kernel, 2 output slices, long persistent loop
     (1, 256, 128, 10, 3, None, False, False),        # 1x1: streaming kernel, K = 256, ragged last tile (M = 300)
     (1, 32, 64, 33, 2, None, False, False),          # 1x1: streaming kernel, K = 32, ragged rows
+    (1, 128, 128, 128, 4, "pw128", False, False),    # 1x1: streaming kernel with 128-channel output slices
+    (1, 256, 256, 10, 3, "pw128", False, False),     # ... K = 256, 2 slices, ragged last tile
     (1, 64, 32, 16, 2, "pw_off", False, False),      # unfolded fallback from here on: 1x1 generic, 128x32 tiles
     (1, 128, 128, 128, 4, "pw_off", False, False),   # 1x1 generic, 128x128 tiles (M >= 65536)
     (1, 64, 64, 24, 2, "igemm_cfg", False, False),   # forced tile config
@@ -1555,7 +1557,7 @@ def test_conv_bwd_fold_matches_unfolded(ks, Cin, N, H, B, tune, split, node):
     torch.manual_seed(41)
     C_ = hip()
     keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "igemm_cfg": (C_.TUNE_IGEMM_CFG, 3),
-            "pw_off": (C_.TUNE_PW, 1)}
+            "pw_off": (C_.TUNE_PW, 1), "pw128": (C_.TUNE_PW_NB, 128)}
     if tune:
         C_.set_tune(*keys[tune])
     try:
@@ -1906,6 +1908,30 @@ def test_engine_device_batch_table_selects_and_advances():
         eng.bind_batches(tab[:2])
     with pytest.raises(ValueError):
         eng.bind_batches(torch.full((3, B), eng.n_data, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("B,H,Cin,N", [(2, 24, 128, 128), (3, 17, 256, 256), (1, 33, 128, 256)])
+def test_pw_wide_slices_equal_narrow(B, H, Cin, N):
+    """Streaming 1x1 conv with 128-channel output slices (TUNE_PW_NB = 128, the large-M default) equals the 64-channel
+    slices bit for bit (same per-channel K order), statistics to float-atomic order."""
+    C = hip()
+    torch.manual_seed(21)
+    xb, _ = bf(torch.randn(B, H, H, Cin))
+    wb = pack(PK_PW, torch.randn(1, 1, Cin, N) * 0.1, 1, Cin, N)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    outs = []
+    for nb in (64, 128):
+        C.set_tune(C.TUNE_PW_NB, nb)
+        try:
+            y = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            stats = torch.zeros(C.STAT_REPLICAS * 2 * N, device=DEV)
+            C.conv_igemm(xb, wb, bias, y, stats, None, 0, B, H, H, Cin, 0, H, H, N, 1, 1, 0, 0)
+            torch.cuda.synchronize()
+        finally:
+            C.set_tune(C.TUNE_PW_NB, 0)
+        outs.append((y.clone(), stats.view(-1, 2, N).sum(0).cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-2)
 
 
 @pytest.mark.parametrize("B,H,Cin,N,use_stats,use_bias,cap", [
