@@ -121,8 +121,10 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
 }
 
 // opt_step (launch.h): one block per OptItem. A thread that uses the step (lr_t) has its read completed before the
-// stores that depend on it, i.e. before the block's closing barrier and the ticket atomic (release, agent scope)
-// after it, so the last block advances the step only after every read of it.
+// stores that depend on it, i.e. before the block's closing barrier and the ticket atomic after it, so the last block
+// advances the step only after every read of it. The ticket is RELAXED: the ordering it needs is that of loads whose
+// values were already consumed, and nothing the blocks stored is read by the last block (an agent-scope release made
+// every block write back its XCD's L2 before retiring).
 __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
   const OptItem it = p.items[blockIdx.x];
   const int tid = threadIdx.x;
@@ -210,9 +212,8 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
   }
   __syncthreads();
   if (tid == 0) {
-    const int t = __hip_atomic_fetch_add(p.ticket, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = __hip_atomic_fetch_add(p.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {                      // every block has read the step: advance it
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       *p.ticket = 0;
       *p.step += 1;
       if (p.cursor != nullptr) *p.cursor += 1;
