@@ -43,6 +43,8 @@ def case(B, H, Cin, N, up=0):
                            ("per-tap-B", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_WB: 2}),
                            ("ws", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_WS: 2}),
                            ("small", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 2}),
+                           ("8x16x32", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 1, C.TUNE_CONV3_BN: 32}),
+                           ("8x16x64", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 1}),
                            ("generic", dict(stats=stats, ab=ab, relu=1, algo=1), {})]:
         for k, v in tune.items():
             C.set_tune(k, v)
@@ -58,6 +60,9 @@ def case(B, H, Cin, N, up=0):
     print(f"B{B} {H:3d}^2 {Cin:3d}->{N:3d} up{up}: " + "  ".join(f"{k} {v}" for k, v in out.items()), flush=True)
 
 
-for args in [(16, 64, 64, 64), (16, 64, 128, 64, 1), (16, 64, 64, 128), (16, 32, 128, 128), (16, 32, 256, 128, 1),
-             (16, 32, 128, 256), (16, 16, 256, 256), (16, 128, 32, 32), (16, 128, 64, 32, 1)]:
+SHAPES = [(16, 64, 64, 64), (16, 64, 128, 64, 1), (16, 64, 64, 128), (16, 32, 128, 128), (16, 32, 256, 128, 1),
+          (16, 32, 128, 256), (16, 16, 256, 256), (16, 128, 32, 32), (16, 128, 64, 32, 1)]
+if len(sys.argv) > 1:                       # e.g. "16" -> only the shapes at that output resolution
+    SHAPES = [s for s in SHAPES if s[1] in [int(a) for a in sys.argv[1:]]]
+for args in SHAPES:
     case(*args)
