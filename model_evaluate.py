@@ -35,21 +35,21 @@ class evaluate_LocalModel:
         """fl_server.py:31 expects {'loss','accuracy'} of the global model.
 
         With a visible GPU the global model is evaluated by the MI355X engine at the clients' resolution
-        (``cfg.img_size``) over the held-out split of a synthetic shard (inference-mode BN, the same validation
-        path the clients run); on a CPU-only server the fp32 oracle evaluates a small (<= 64^2) shard."""
+        (``cfg.img_size``) over the SAME held-out split the clients validate on (inference-mode BN, the same
+        validation path they run): the folder dataset's reference split, or - synthetic data - client rank 0's shard
+        (same seed, sample count and split), so the server's numbers are comparable to that client's ``val_*``;
+        ``max_batches`` bounds the pass. On a CPU-only server the fp32 oracle evaluates a small (<= 64^2) shard."""
         if self._eval is None:
             import dataclasses
             from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer, resolve_device
             dev = resolve_device(self.cfg)
             if dev == "cuda":
-                n_val = max(self.bs, min(self.cfg.val_samples, 8 * self.bs) // self.bs * self.bs)
-                cfg = dataclasses.replace(self.cfg, device="cuda", synthetic_samples=2 * n_val, val_samples=n_val,
-                                          batch_size=self.bs)
+                cfg = dataclasses.replace(self.cfg, device="cuda", batch_size=self.bs)
             else:
                 cfg = dataclasses.replace(self.cfg, device="cpu", synthetic_samples=max(2 * self.bs, 32),
                                           val_samples=self.bs, img_size=min(self.cfg.img_size, 64),
                                           batch_size=self.bs)
-            self._eval = make_trainer(cfg, "server-eval", table=self.table, device=dev)
+            self._eval = make_trainer(cfg, "server-eval", rank=0, table=self.table, device=dev)
         self._eval.backend.set_flat(model)
         from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
         vb = epoch_batches(self._eval.data.val_idx, self.bs, 0, 0)

@@ -148,3 +148,26 @@ def test_fl_rccl_product_path_two_clients_one_gpu(tmp_path):
     pay = sorted([p["payload_bytes"] for p in ph] for ph in phases)
     assert pay[0] == [0, 0] and all(b > 0 for b in pay[1]), pay                   # rank 1 uploads nothing
     assert all(p.get("reply_bytes", 0) == 0 for ph in phases for p in ph)         # no parameters shipped back
+
+
+def test_server_evaluator_uses_the_clients_held_out_split():
+    """model_evaluate.evaluate_LocalModel (the server's global-model hook, fl_server.py:31) evaluates on client rank
+    0's held-out split - the same images, split and inference path as that client's validation - so its loss /
+    accuracy equal the client trainer's eval of the same weights."""
+    sys.path.insert(0, ROOT)
+    import model_evaluate
+    from crack_detection_federatedlearning_grpc_amd import config as C
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer
+    from crack_detection_federatedlearning_grpc_amd.train.local import epoch_batches
+    cfg = C.from_args(None, preset="gpu1-256", img_size=64, batch_size=4, synthetic_samples=48, val_samples=32,
+                      data_seed=3, device="cuda")
+    table = ParamTable()
+    flat = table.init_flat(5)
+    ev = model_evaluate.evaluate_LocalModel(4, 64, cfg=cfg)
+    got = ev.train_model_tosave(flat)
+    client = make_trainer(cfg, "c0", 0, table=table, device="cuda")
+    client.backend.set_flat(flat)
+    want = client.backend.eval_batches(epoch_batches(client.data.val_idx, 4, 0, 0))
+    assert np.isclose(got["loss"], want["loss"], rtol=1e-6) and np.isclose(got["accuracy"], want["accuracy"])
+    assert 0 < got["loss"] < 10
