@@ -42,12 +42,16 @@ template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool PJ = false, boo
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
+  // LDS pitch of a halo line: TW + 2, except 16 for the 8-wide tiles - there a 16-row A fragment spans two pixel rows,
+  // and with 10-row lines every ds_read_b128 lane group hit 2-way bank conflicts under the row swizzle (measured
+  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 28 %, profiles/r3_final); 16-row lines make every group conflict-free
+  constexpr int HWL = TW == 8 ? 16 : HW, HPL = HH * HWL;
   constexpr int TM = BM / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
   constexpr int HALO_CHUNKS = HP * (BK / 8);                      // 16-byte pieces per halo tile
   constexpr int H_PER_T = (HALO_CHUNKS + NT - 1) / NT;
   constexpr int B_CHUNKS = BN_ * BK / 8, B_PER_T = (B_CHUNKS + NT - 1) / NT;
   constexpr int BW_CHUNKS = 9 * B_CHUNKS, BW_PER_T = WB ? (BW_CHUNKS + NT - 1) / NT : 1;
-  constexpr int SH = (WB ? 1 : 2) * HP * LDH, SB = (WB ? 9 : 2) * BN_ * LDB;
+  constexpr int SH = (WB ? 1 : 2) * HPL * LDH, SB = (WB ? 9 : 2) * BN_ * LDB;
   constexpr int LDC = BN_ + 8;
   static_assert(BM * LDC <= SH + SB, "C staging tile must fit");
   static_assert(WM * WN == 4 && TM % 16 == 0 && TN % 16 == 0, "wave tiling");
@@ -142,7 +146,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < HALO_CHUNKS) *reinterpret_cast<uint4*>(sH + buf * HP * LDH + swz_off(e >> 2, e & 3)) = rh[i];
+      if (e < HALO_CHUNKS) {
+        const int hp = e >> 2, hy = hp / HW, hx = hp - hy * HW;
+        *reinterpret_cast<uint4*>(sH + buf * HPL * LDH + swz_off(hy * HWL + hx, e & 3)) = rh[i];
+      }
     }
   };
   // ---- weight tile of K-step (chunk, tap): wt[n][tap*Cin + chunk*32 .. +32) ----
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int pp = wm * TM + i * 16 + (lane & 15);
-    fhp[i] = (pp / TW) * HW + pp % TW;
+    fhp[i] = (pp / TW) * HWL + pp % TW;
   }
   const int fq = lane >> 4;
   const int brow = wn * TN + (lane & 15);
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
         s8v af[FM], bfg[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          af[i] = *reinterpret_cast<const s8v*>(sH + swz_off(fhp[i] + ky * HW + kx, fq));
+          af[i] = *reinterpret_cast<const s8v*>(sH + swz_off(fhp[i] + ky * HWL + kx, fq));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           bfg[j] = *reinterpret_cast<const s8v*>(sB + swz_off(tap * BN_ + brow + j * 16, fq));
@@ -312,7 +319,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       s8v af[FM], bfg[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const s8v*>(sH + hbuf * HP * LDH + swz_off(fhp[i] + ky * HW + kx, fq));
+        af[i] = *reinterpret_cast<const s8v*>(sH + hbuf * HPL * LDH + swz_off(fhp[i] + ky * HWL + kx, fq));
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         bfg[j] = *reinterpret_cast<const s8v*>(sB + bbuf * BN_ * LDB + swz_off(brow + j * 16, fq));
