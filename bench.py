@@ -128,7 +128,12 @@ def main() -> int:
     eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
-    agg = FedAvgAllReduce(eng.flat, table, world) if world > 1 or args.fedavg_1rank else None
+    agg = None
+    if world > 1 or args.fedavg_1rank:
+        # first bucket = the encoder's parameters: the next round's first step replays its encoder graph after that
+        # bucket alone, the rest of the step after every bucket (UNetEngine.train_step)
+        agg = FedAvgAllReduce(eng.flat, table, world, first_bucket=eng.split_at)
+        agg.timing = True
     n_local = len(data.train_idx)
     batches = torch.as_tensor(epoch_batches(data.train_idx, args.batch, args.local_steps, seed=rank),
                               dtype=torch.int32, device=dev)
@@ -182,7 +187,8 @@ def main() -> int:
             torch.cuda.current_stream(dev).wait_stream(ev_stream)   # the round's last validation pass
         if agg is not None:
             # weighted FedAvg over RCCL/xGMI, bucketed in layer order on a side stream; each bucket's layers are
-            # repacked to bf16 there and the next round waits per bucket (engine.defer_until)
+            # repacked to bf16 there and the next round's first step waits per bucket (engine.defer_until: the
+            # encoder graph after bucket 0, the rest of the step after all)
             eng.defer_until(agg.average_async(float(n_local), on_bucket=eng.pack_bucket))
         else:
             eng.pack()
@@ -203,6 +209,9 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if agg is not None:            # FedAvg cost inside the timed region only (hipEvents, read after the run)
+        agg.timings.clear()
+        eng.stall_log = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         fl_round()
@@ -218,6 +227,25 @@ def main() -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    fedavg_stats = {}
+    if agg is not None:
+        fedavg_stats = agg.timing_summary()
+        # the compute stream's stalls on the FedAvg buckets (two waits per post-FedAvg step: before the encoder
+        # graph, before the rest); the timed region's last all-reduce is waited by the closing synchronize instead
+        stalls = [a.elapsed_time(b) for a, b in eng.stall_log]
+        per = [sum(stalls[i:i + 2]) for i in range(0, len(stalls) - 1, 2)]
+        if per and fedavg_stats:
+            exp = float(np.mean(per))
+            fedavg_stats["allreduce_exposed_ms"] = exp
+            tot = fedavg_stats["allreduce_repack_ms"]
+            fedavg_stats["overlap_fraction"] = max(0.0, min(1.0, 1.0 - exp / tot)) if tot > 0 else None
+        if world > 1:              # MAX over ranks (the slowest rank's collective bounds the round)
+            keys = [k for k in ("allreduce_ms", "allreduce_repack_ms", "allreduce_exposed_ms") if k in fedavg_stats]
+            t = torch.tensor([fedavg_stats[k] for k in keys], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            fedavg_stats.update({k: float(v) for k, v in zip(keys, t.tolist())})
+        fedavg_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in fedavg_stats.items()}
+        eng.stall_log = None
     fedavg_err = None
     if args.verify_fedavg and agg is not None:
         # one weighted FedAvg with unequal n_k against sum_k n_k w_k / sum n from all-gathered copies
@@ -254,6 +282,7 @@ def main() -> int:
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "dist_backend": (dist.get_backend() if world > 1 else None),
                **({"fedavg_max_abs_err": fedavg_err} if fedavg_err is not None else {}),
+               **fedavg_stats,
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",
                           "img_size": args.img, "global_batch": args.batch * world, "per_client_batch": args.batch,
                           "seq_len": None, "epochs_per_round": args.epochs,

@@ -52,6 +52,9 @@ class FLConfig:
                                          # communicator and falls back to the gRPC data plane
     dist_backend: str = "nccl"           # rccl data plane backend: nccl (= RCCL over xGMI) | gloo (CPU clients, or
                                          # a rehearsal of N clients sharing one GPU, which RCCL refuses)
+    async_upload: bool = True            # rccl data plane: after a successful collective the client starts the next
+                                         # round at once and reports TRAIN_DONE (rank 0: + the average) from a
+                                         # background thread; its reply is checked before the next report
     codec: str = "flat"                  # client upload / advertised reply format: flat (safe) | pickle (reference
                                          # wire format). The server answers each client in the format it
                                          # advertised, pickle for a reference client that advertises none

@@ -17,6 +17,7 @@ import json
 import os
 import random
 import sys
+import threading
 import time
 from typing import Callable, Dict, List, Optional, Protocol
 
@@ -59,6 +60,7 @@ class FLClient:
         self.info: Dict[str, object] = {}
         self.final_state = ""
         self.fallbacks = 0                      # RCCL -> gRPC data-plane fallbacks (peer loss)
+        self._pending = None                    # (thread, result box) of an async round report
 
     # -- transport helpers ---------------------------------------------------------------------------
     def _call(self, stub, req) -> "P.transportResponse":
@@ -146,6 +148,8 @@ class FLClient:
     # -- local work ------------------------------------------------------------------------------------
     def _train(self, cr: int) -> None:
         if self.cfg.fault_drop_round and cr >= self.cfg.fault_drop_round:
+            if self._pending is not None:      # the previous round's report went out (async upload) first
+                self._pending[0].join()
             print(f"[{self.name}] fault injection: dropping out at round {cr}")
             raise SystemExit(3)
         t0 = time.perf_counter()
@@ -156,10 +160,10 @@ class FLClient:
             codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
 
     def _payload(self) -> tuple:
-        """(TRAIN_DONE payload, data plane). RCCL mode: the weighted all-reduce runs here (in place on the GPU, or
-        over host arrays); rank 0 alone uploads the average for the server's copy, the other ranks send nothing.
-        A failed collective leaves the local model unchanged (fedavg_device rolls back) and the client continues
-        on the gRPC data plane."""
+        """(weights to upload or None, data plane). RCCL mode: the weighted all-reduce runs here (in place on the
+        GPU, or over host arrays); rank 0 alone uploads the average for the server's copy (its host copy is taken
+        here, before the next round can touch the weights), the other ranks send nothing. A failed collective
+        leaves the local model unchanged (fedavg_device rolls back) and the client continues on the gRPC plane."""
         n = getattr(self.trainer, "n_samples", 0)
         arrays = None
         plane = ""
@@ -181,12 +185,54 @@ class FLClient:
             else:
                 plane = "rccl"
                 if self.aggregator.rank != 0:
-                    return b"", plane                            # rank 0 alone uploads the server's copy
-        if self.cfg.fault_corrupt:
-            return b"\x80corrupt" + os.urandom(64), plane
+                    return None, plane                           # rank 0 alone uploads the server's copy
         if arrays is None:
             arrays = self.trainer.get_weights()
-        return codec.encode(arrays, self.cfg.codec, n_samples=n, wire_dtype=self.cfg.wire_dtype), plane
+        return arrays, plane
+
+    def _encode(self, arrays) -> bytes:
+        if arrays is None:
+            return b""
+        if self.cfg.fault_corrupt:
+            return b"\x80corrupt" + os.urandom(64)
+        return codec.encode(arrays, self.cfg.codec, n_samples=getattr(self.trainer, "n_samples", 0),
+                            wire_dtype=self.cfg.wire_dtype)
+
+    def _report(self, stub, cr: int, mv: int, arrays, plane: str) -> Dict:
+        """TRAIN_DONE of round ``cr`` and, on RESP_ACY, the VERSION long-poll until the server has aggregated the
+        round (NOT_WAIT) or finished (FIN): the reference's verb sequence (fl_client.py:121-166). Returns the
+        outcome and its phase timings; no local training happens here."""
+        t1 = time.perf_counter()
+        payload = self._encode(arrays)
+        with trace_phase("fl/upload"):
+            rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0), plane)
+        t2 = time.perf_counter()
+        st = rep.config["state"].scstring
+        print(f"### Received from state {st} ###")
+        out = {"state": st, "cr": cr, "mv": mv, "blob": b"",
+               "phase": {"round": cr, "upload_s": t2 - t1, "wait_s": 0.0, "payload_bytes": len(payload),
+                         "data_plane": plane or "grpc",
+                         "rank": self.aggregator.rank if self.aggregator is not None else -1}}
+        if st == "RESP_ACY":
+            while True:
+                vr = self._version(stub, mv, cr, self.cfg.long_poll_s)
+                if vr.state in (P.NOT_WAIT, P.FIN):
+                    out["phase"]["wait_s"] = time.perf_counter() - t2
+                    out["state"] = "NOT_WAIT" if vr.state == P.NOT_WAIT else "FIN"
+                    out["cr"] = vr.config["current_round"].scint32
+                    out["mv"] = vr.config["model_version"].scint32
+                    out["blob"] = vr.buffer_chunk
+                    out["phase"]["reply_bytes"] = len(vr.buffer_chunk)
+                    return out
+                time.sleep(min(self.cfg.poll_period_s, 1.0) if self.cfg.long_poll_s > 0
+                           else self.cfg.poll_period_s)
+        if st in ("RESP_ARY", "FIN"):
+            out["cr"] = rep.config["current_round"].scint32
+            out["mv"] = rep.config["model_version"].scint32
+            out["blob"] = rep.buffer_chunk
+            if st == "RESP_ARY":
+                out["phase"]["reply_bytes"] = len(rep.buffer_chunk)
+        return out
 
     def _apply(self, blob: bytes) -> None:
         if self.aggregator is not None or not blob:
@@ -215,57 +261,68 @@ class FLClient:
             self._training(stub)
             self._train(cr)
             while cr <= mtr:
+                join_s = 0.0
+                if self._pending is not None:     # the previous round's TRAIN_DONE / VERSION exchange
+                    tj = time.perf_counter()
+                    th, box = self._pending
+                    th.join()
+                    self._pending = None
+                    join_s = time.perf_counter() - tj
+                    if "error" in box:
+                        raise box["error"]
+                    res = box["res"]
+                    self._log_phase(dict(res["phase"], aggregate_s=box["aggregate_s"], join_wait_s=join_s,
+                                         exposed_s=box["aggregate_s"] + join_s, async_upload=True))
+                    if res["state"] == "FIN":     # the server finished the run (e.g. fewer rounds than advertised)
+                        cr, mv = res["cr"], res["mv"]
+                        self.final_state = "FIN"
+                        break
+                    if res["state"] not in ("NOT_WAIT", "RESP_ARY"):
+                        print(f"[{self.name}] unexpected state {res['state']!r}; exiting")
+                        self.final_state = res["state"]
+                        break
+                    if (res["cr"], res["mv"]) != (cr, mv):
+                        print(f"[{self.name}] server moved to round {res['cr']} / version {res['mv']} (expected "
+                              f"{cr} / {mv}); following it")
+                        cr, mv = res["cr"], res["mv"]
                 print(f"### Deliver model state: TRAIN DONE to server ### round {cr}")
                 if self.cfg.fault_delay_s:
                     time.sleep(self.cfg.fault_delay_s)
                 t0 = time.perf_counter()
                 with trace_phase("fl/aggregate"):
-                    payload, plane = self._payload()      # RCCL mode: the all-reduce runs here
-                t1 = time.perf_counter()
-                with trace_phase("fl/upload"):
-                    rep = self._train_done(stub, cr, payload, getattr(self.trainer, "n_samples", 0), plane)
-                t2 = time.perf_counter()
-                phase = {"round": cr, "aggregate_s": t1 - t0, "upload_s": t2 - t1, "wait_s": 0.0,
-                         "payload_bytes": len(payload), "data_plane": plane or "grpc",
-                         "rank": self.aggregator.rank if self.aggregator is not None else -1}
-                st = rep.config["state"].scstring
-                print(f"### Received from state {st} ###")
-                if st == "RESP_ACY":
-                    while True:
-                        vr = self._version(stub, mv, cr, self.cfg.long_poll_s)
-                        if vr.state == P.NOT_WAIT:
-                            phase["wait_s"] = time.perf_counter() - t2
-                            phase["reply_bytes"] = len(vr.buffer_chunk)
-                            self._log_phase(phase)
-                            cr = vr.config["current_round"].scint32
-                            mv = vr.config["model_version"].scint32
-                            self._apply(vr.buffer_chunk)
+                    arrays, plane = self._payload()        # RCCL mode: the all-reduce runs here
+                agg_s = time.perf_counter() - t0
+                if plane == "rccl" and self.cfg.async_upload and cr < mtr:
+                    # this client already holds the round's average: report it (rank 0: upload it) from a
+                    # background thread and start the next round now, off the server's aggregation path
+                    box: Dict = {"aggregate_s": agg_s}
+
+                    def report(cr=cr, mv=mv, arrays=arrays, plane=plane, box=box):
+                        try:
+                            box["res"] = self._report(stub, cr, mv, arrays, plane)
                             self._training(stub)
-                            self._train(cr)
-                            break
-                        if vr.state == P.FIN:
-                            phase["wait_s"] = time.perf_counter() - t2
-                            self._log_phase(phase)
-                            cr = vr.config["current_round"].scint32
-                            mv = vr.config["model_version"].scint32
-                            self.final_state = "FIN"
-                            break
-                        time.sleep(min(self.cfg.poll_period_s, 1.0) if self.cfg.long_poll_s > 0
-                                   else self.cfg.poll_period_s)
-                    if self.final_state == "FIN":
-                        break
-                elif st == "RESP_ARY":
-                    phase["reply_bytes"] = len(rep.buffer_chunk)
-                    self._log_phase(phase)
-                    self._training(stub)
-                    cr = rep.config["current_round"].scint32
-                    mv = rep.config["model_version"].scint32
-                    self._apply(rep.buffer_chunk)
+                        except BaseException as e:   # re-raised by the main thread at the join
+                            box["error"] = e
+                    th = threading.Thread(target=report, name=f"{self.name}-report", daemon=True)
+                    th.start()
+                    self._pending = (th, box)
+                    cr, mv = cr + 1, mv + 1              # what the server's aggregation of round cr yields
+                    self._train(cr)
+                    continue
+                res = self._report(stub, cr, mv, arrays, plane)
+                phase = dict(res["phase"], aggregate_s=agg_s)
+                st = res["state"]
+                self._log_phase(phase)
+                if st in ("NOT_WAIT", "RESP_ARY"):
+                    if st == "RESP_ARY":
+                        self._training(stub)
+                    cr, mv = res["cr"], res["mv"]
+                    self._apply(res["blob"])
+                    if st == "NOT_WAIT":
+                        self._training(stub)
                     self._train(cr)
                 elif st == "FIN":
-                    self._log_phase(phase)
-                    cr = rep.config["current_round"].scint32
-                    mv = rep.config["model_version"].scint32
+                    cr, mv = res["cr"], res["mv"]
                     self.final_state = "FIN"
                     break
                 else:

@@ -40,6 +40,63 @@ from .rpc import TransportServiceServicer, add_TransportServiceServicer_to_serve
 from .state import CTW, FIN, NOT_WAIT, RESP_ACY, RESP_ARY, SW, WAIT, RoundRecord, RoundState
 
 
+class LatestWorker:
+    """One worker thread that runs the NEWEST submitted job: a job submitted while another waits replaces it (a
+    round's snapshot / evaluation supersedes the previous round's if that one has not started yet), so slow disk
+    or a slow evaluator never queues one 8 MB model copy per round. ``flush`` waits until the worker is idle;
+    ``close(cancel)`` drops (or, cancel=False, runs) the pending job and joins the thread."""
+
+    def __init__(self, name: str):
+        self._cv = threading.Condition()
+        self._job: Optional[Callable[[], None]] = None
+        self._busy = False
+        self._closed = False
+        self._t = threading.Thread(target=self._loop, name=name, daemon=True)
+        self._t.start()
+
+    def submit(self, job: Callable[[], None]) -> None:
+        with self._cv:
+            if self._closed:
+                raise RuntimeError("worker closed")
+            self._job = job
+            self._cv.notify_all()
+
+    def _loop(self) -> None:
+        while True:
+            with self._cv:
+                while self._job is None and not self._closed:
+                    self._cv.wait()
+                if self._job is None:
+                    return
+                job, self._job, self._busy = self._job, None, True
+            try:
+                job()
+            except Exception as e:  # a failed write / evaluation must not kill the worker
+                print(f"[fl_server] background job failed: {e!r}")
+            finally:
+                with self._cv:
+                    self._busy = False
+                    self._cv.notify_all()
+
+    def flush(self, timeout: Optional[float] = None) -> bool:
+        end = None if timeout is None else time.monotonic() + timeout
+        with self._cv:
+            while self._job is not None or self._busy:
+                rem = None if end is None else end - time.monotonic()
+                if rem is not None and rem <= 0:
+                    return False
+                self._cv.wait(rem)
+            return True
+
+    def close(self, cancel: bool = False) -> None:
+        with self._cv:
+            if cancel:
+                self._job = None
+            self._closed = True
+            self._cv.notify_all()
+        self._t.join()
+
+
 def _scalar(v) -> "P.Scalar":
     if isinstance(v, bool):
         return P.Scalar(scint32=int(v))
@@ -80,7 +137,8 @@ class FLServer(TransportServiceServicer):
         self._blob_cache: Dict[tuple, bytes] = {}
         self._codec: Dict[str, tuple] = {}          # client name -> (codec, wire_dtype) it can decode
         self._rccl_round: Dict[str, int] = {}       # client -> round whose average it holds already (RCCL plane)
-        self._eval_pool: Optional[futures.ThreadPoolExecutor] = None
+        self._persist: Optional[LatestWorker] = None       # weight file + snapshot writes (off the lock)
+        self._eval_worker: Optional[LatestWorker] = None   # server-side evaluation of the newest global
         self.server: Optional[grpc.Server] = None
         self.port: Optional[int] = None
         self.dist_port = 0
@@ -126,21 +184,35 @@ class FLServer(TransportServiceServicer):
         print(f"[fl_server] round {rec.round} aggregated over {len(rec.clients)} client(s) "
               f"(n={[int(n) for n in rec.n_samples]}) in {dt:.2f}s -> version {st.model_version}"
               + (" (FIN)" if st.finished else ""))
-        if self.cfg.server_weight_file:   # reference: ./server_weights/weights.pickle (fl_server.py:104-105)
-            codec.save_weight_file(os.path.join(self.cfg.work_dir, self.cfg.server_weight_file)
-                                   if not os.path.isabs(self.cfg.server_weight_file) else self.cfg.server_weight_file,
-                                   self.table.to_list(st.global_flat))
-        if self.cfg.snapshot_dir:
-            save_snapshot(self.cfg.snapshot_dir, self.table, st.global_flat, st.current_round, st.model_version,
-                          st.finished)
+        # This hook runs under the RoundState lock: the file writes (8.2 MB pickle, .h5 snapshot) and the evaluation
+        # go to worker threads with a copy of the new global, so READY / VERSION long-polls / heartbeats - and the
+        # wake-up of the clients waiting for this round - never wait for the disk or the evaluator.
+        flat = st.global_flat.copy()
+        if self.cfg.server_weight_file or self.cfg.snapshot_dir:
+            if self._persist is None:
+                self._persist = LatestWorker("fl-persist")
+            args = (flat, st.current_round, st.model_version, st.finished)     # bound now, under the lock
+            self._persist.submit(lambda: self._write_round(*args))
         if self.evaluator is not None:   # fl_server.py:27-37 (dead code in the reference)
-            # off the RoundState lock (this hook runs under it): READY / VERSION / heartbeat RPCs keep flowing
-            # while the global model is evaluated on a worker thread
-            if self._eval_pool is None:
-                self._eval_pool = futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fl-eval")
-            self._eval_pool.submit(self._evaluate, rec.round, st.global_flat.copy())
+            if self._eval_worker is None:
+                self._eval_worker = LatestWorker("fl-eval")
+            self._eval_worker.submit(lambda r=rec.round: self._evaluate(r, flat))
         if st.finished:
             self.done.set()
+
+    def _write_round(self, flat: np.ndarray, current_round: int, version: int, finished: bool) -> None:
+        """The reference's ./server_weights/weights.pickle (fl_server.py:104-105) + the resume snapshot. Runs on
+        the persistence worker; only the newest pending round is written (each file is overwritten per round)."""
+        if self.cfg.server_weight_file:
+            codec.save_weight_file(os.path.join(self.cfg.work_dir, self.cfg.server_weight_file)
+                                   if not os.path.isabs(self.cfg.server_weight_file) else self.cfg.server_weight_file,
+                                   self.table.to_list(flat))
+        if self.cfg.snapshot_dir:
+            save_snapshot(self.cfg.snapshot_dir, self.table, flat, current_round, version, finished)
+
+    def flush_persistence(self, timeout: Optional[float] = None) -> bool:
+        """Wait until the latest round's weight file / snapshot is on disk."""
+        return self._persist.flush(timeout) if self._persist is not None else True
 
     def _evaluate(self, rnd: int, flat: np.ndarray) -> None:
         try:
@@ -265,8 +337,12 @@ class FLServer(TransportServiceServicer):
         self.state.stop()
         if self.server is not None:
             self.server.stop(grace)
-        if self._eval_pool is not None:
-            self._eval_pool.shutdown(wait=True)
+        if self._persist is not None:          # the last round's files are written before stop returns
+            self._persist.close(cancel=False)
+            self._persist = None
+        if self._eval_worker is not None:      # a pending (not yet started) evaluation is dropped
+            self._eval_worker.close(cancel=True)
+            self._eval_worker = None
 
     def serve_forever(self, exit_on_fin: bool = True) -> None:
         try:

@@ -84,16 +84,20 @@ class UNetEngine:
         self.batch_table: Optional[torch.Tensor] = None
         self.batch_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
-        # residual joins (max-pool + add / BN + add) fused into the residual conv's epilogue (CFL_FUSE_JOIN=0: off)
-        self.fuse_join = os.environ.get("CFL_FUSE_JOIN", "1") != "0"
         self._build_pack()
         self._alloc()
         # the optimizer tail (Adam + BN moving statistics + bf16 repack + step / cursor advance) as ONE opt_step
-        # launch (CFL_OPT_FUSE=0: adam_update, bn_moving_update and pack_weights launches)
-        self.fuse_opt = share is None and os.environ.get("CFL_OPT_FUSE", "1") != "0"
-        if self.fuse_opt:
+        # launch (training engines only)
+        if share is None:
             self._build_opt()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # the same step as TWO graphs split after the encoder forward (capture()): replayed right after a FedAvg,
+        # so the encoder - whose parameters form the first all-reduce bucket - runs while the later buckets reduce
+        self.graph_pre: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_post: Optional[torch.cuda.CUDAGraph] = None
+        self._mid_hook = None
+        self.split_at = self.table.entry(self.names[17], "kernel").offset   # flat end of the encoder parameters
+        self.stall_log: Optional[List[tuple]] = None   # (before, after) event pairs of post-FedAvg waits (bench)
         self.eval_graph: Optional[torch.cuda.CUDAGraph] = None
         self._retired: List[torch.Tensor] = []   # replaced workspaces a captured graph may still reference
         self._evaluators: Dict[int, "UNetEngine"] = {}
@@ -298,41 +302,18 @@ class UNetEngine:
         self._finish_dyn: List[tuple] = []
         self._wslabs: Dict[str, torch.Tensor] = {}
         self._build_finish()
-        # weight gradients (off the backward critical path: they read forward activations and incoming gradients
-        # that are never overwritten within a step) deferred to the end of backward and issued as ONE batch, the 3x3
-        # halo ones grouped per tile config into shared launches (conv_wgrad_batch) so their latency-bound grids
-        # co-run (CFL_WGRAD_DEFER=0: each issued where it is computed)
-        self.defer_wgrad = os.environ.get("CFL_WGRAD_DEFER", "1") != "0"
-        # BN-backward apply folded into the encoder's pointwise data gradients: the streaming 1x1 kernel (pw.hip) applies it
-        # to its B-fragment registers and stores dx from the first output slice's blocks - 6 bn_bwd_apply launches
-        # fewer, whole step 1.4421-1.4524 -> 1.4358-1.4361 ms/iteration (CFL_BNB_FOLD_PW=0: separate passes)
-        self.fold_pw = os.environ.get("CFL_BNB_FOLD_PW", "1") != "0"
-        # decoder residual-conv gradient dq = 2x2 sums of dxlo formed in its 1x1 dgrad's operand load (pw.hip) instead
-        # of a node_bwd pass: 3 launches fewer, whole step 1.4574-1.4693 -> 1.4463-1.4493 ms/iteration on the same box
-        # (CFL_SUM2X2_FOLD=0: the separate pass)
-        self.fold_sum2x2 = os.environ.get("CFL_SUM2X2_FOLD", "1") != "0"
-        # ... and into the entry conv's weight gradient, its only consumer (whole step 1.4412-1.4416 -> 1.4328-1.4346
-        # ms/iteration; CFL_BNB_FOLD_ENTRY=0: a separate pass)
-        self.fold_entry = os.environ.get("CFL_BNB_FOLD_ENTRY", "1") != "0"
-        # depthwise dgrad + wgrad of a layer in one fused pass reading dy and x once (dw_bwd; CFL_DW_BWD_FUSE=0: a
-        # dgrad launch plus a deferred, grouped wgrad)
-        self.fuse_dw_bwd = os.environ.get("CFL_DW_BWD_FUSE", "1") != "0"
-        # decoder node join (2x2 sum of the convT1 input gradient, ReLU mask, + residual gradient, BN_B(k-1) sums) in
-        # the convT1 dgrad's epilogue (CFL_POOL_JOIN=0: dxin stored + a node_bwd pass)
-        self.fuse_pool_join = os.environ.get("CFL_POOL_JOIN", "1") != "0"
-        # BN finalize done by the layer's first consumer from the replica sums (CFL_FIN_CONSUMER=0: a 1-block
-        # bn_finalize launch per BN layer)
-        self.fin_in_consumer = os.environ.get("CFL_FIN_CONSUMER", "1") != "0"
-        # training head: forward (logits, loss / accuracy sums) and backward in ONE pass over x_lo (head.hip FWD),
-        # possible whenever the loss has no whole-batch term (the Dice gradient needs the forward's sums first)
-        # (CFL_HEAD_FUSE=0: head_fwd at the end of forward + head_bwd)
-        self.fuse_head = self.dice == 0 and os.environ.get("CFL_HEAD_FUSE", "1") != "0"
-        # SeparableConv forward in one pass (sepconv.hip; CFL_SEP_FUSE=0: dw_fwd + pointwise conv)
-        self.fuse_sep = os.environ.get("CFL_SEP_FUSE", "1") != "0"
-        self.eager_after_fedavg = os.environ.get("CFL_EAGER_AFTER_FEDAVG", "0") == "1"
-        # independent streaming BN-backward passes co-launched with the residual convs' 1x1 dgrads that read the
-        # same incoming gradient (launch.h SideJob; CFL_SIDE_FUSE=0: separate launches)
-        self.side_fuse = os.environ.get("CFL_SIDE_FUSE", "1") != "0"
+        # The schedule's folds were each kept by a whole-bench A/B on the GPU (profiles/README.md; round 4 retired
+        # their env switches and off-branches):
+        # * weight gradients deferred to the end of backward and issued as ONE grouped batch (conv_wgrad_batch);
+        # * BN-backward apply folded into the encoder's pointwise dgrads (pw.hip) and the entry wgrad's dy load;
+        # * decoder residual-conv gradient dq = 2x2 sums of dxlo formed in its 1x1 dgrad's operand load;
+        # * depthwise dgrad + wgrad (+ the BN node) of a layer in one fused pass (dw_bwd);
+        # * decoder node join in the convT1 dgrad's epilogue; BN finalize in each BN layer's first consumer;
+        # * SeparableConv forward in one pass (sepconv.hip); streaming BN-backward passes co-launched with the
+        #   residual convs' 1x1 dgrads (launch.h SideJob); residual joins in the residual conv's epilogue.
+        # Training head: forward + backward in ONE pass over x_lo (head.hip FWD) whenever the loss has no
+        # whole-batch term (the Dice gradient needs the forward's sums first).
+        self.fuse_head = self.dice == 0
         self._wq: Optional[List[tuple]] = None
         self._dwq: Optional[List[tuple]] = None
         # per-step zeroing of gradients / statistics in one launch
@@ -420,7 +401,7 @@ class UNetEngine:
     def _xfin(self, name: str, train: bool) -> Dict[str, object]:
         """Consumer-side BN finalize kwargs: the consumer computes layer ``name``'s coefficients from its replica
         sums (and writes its ab rows) instead of a bn_finalize launch (empty: ab is final already)."""
-        if not train or not self.fin_in_consumer:
+        if not train:
             return {}
         return dict(xfin_stats=self.bn[name]["stats"], xfin_gamma=self.P(name, "gamma"),
                     xfin_beta=self.P(name, "beta"), xfin_count=float(self.bn_count(name)), xfin_eps=self.bn_eps)
@@ -429,15 +410,10 @@ class UNetEngine:
         """_xfin for a residual conv's join epilogue (the join BN's first consumer)."""
         return {"j" + k[1:]: v for k, v in self._xfin(name, train).items()}
 
-    def _bn_final(self, name: str, train: bool, consumer: bool = False) -> torch.Tensor:
-        """ab of BN layer ``name``; consumer=True: its next consumer finalizes it (_xfin), nothing is launched."""
-        b = self.bn[name]
-        if not train or (consumer and self.fin_in_consumer):
-            return b["ab"]          # inference: written by forward()'s bn_eval_coefs; train: by the next consumer
-        self.C.bn_finalize(b["stats"] if train else None, self.P(name, "gamma"), self.P(name, "beta"),
-                           self.P(name, "moving_mean"), self.P(name, "moving_variance"), b["ab"], b["C"],
-                           float(self.bn_count(name)), self.bn_eps, 1 if train else 0)
-        return b["ab"]
+    def _bn_final(self, name: str) -> torch.Tensor:
+        """ab of BN layer ``name``: in training its next consumer finalizes it from the batch statistics (_xfin),
+        in inference forward()'s bn_eval_coefs wrote it - nothing is launched here."""
+        return self.bn[name]["ab"]
 
     def _igemm(self, x, wt, bias, y, stats, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t,
                pad_l, node: Optional[Tuple[torch.Tensor, Dict[str, torch.Tensor], int]] = None,
@@ -490,7 +466,7 @@ class UNetEngine:
         st = self.bn[e_bn]["stats"] if train else None
         C.entry_fwd(self.images, self.idx, self.P(e_conv, "kernel"), self.P(e_conv, "bias"), A["y0"], st, B, self.S,
                     ENTRY_FILTERS)
-        ab0 = self._bn_final(e_bn, train, consumer=True)
+        ab0 = self._bn_final(e_bn)
         x = Lazy(A["y0"], ab0, 1, r[0], ENTRY_FILTERS)     # a0 = relu(BN0(y0))
         for k, F in enumerate(ENC_FILTERS):
             s1, b1, s2, b2, rc = (next(n) for _ in range(5))
@@ -498,19 +474,18 @@ class UNetEngine:
             # SeparableConv 1: the depthwise conv is the first consumer of BN0 (k = 0): it finalizes it
             self._sepconv(x.t, x.ab, s1, A[f"e{k}_d1"], A[f"e{k}_y1"], b1, H, x.C, F, train,
                           self._xfin(e_bn, train) if k == 0 else {})
-            ab1 = self._bn_final(b1, train, consumer=True)
+            ab1 = self._bn_final(b1)
             self._sepconv(A[f"e{k}_y1"], ab1, s2, A[f"e{k}_d2"], A[f"e{k}_y2"], b2, H, F, F, train,
                           self._xfin(b1, train))
-            ab2 = self._bn_final(b2, train, consumer=self.fuse_join)
-            if self.fuse_join:   # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
-                self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
-                           join=dict(join_mode=C.JOIN_POOL, join_y=A[f"e{k}_y2"], join_ab=ab2,
-                                     join_out=A[f"e{k}_x"], join_argmax=A[f"e{k}_am"], join_H=H, join_W=H,
-                                     **self._jfin(b2, train)))
-            else:
-                self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None)
-                C.pool_res_fwd(A[f"e{k}_y2"], ab2, A[f"e{k}_res"], A[f"e{k}_x"], A[f"e{k}_am"], B, H, H, F)
+            ab2 = self._bn_final(b2)
+            # residual 1x1/s2 conv whose epilogue does max-pool(BN(y2)) + add + argmax
+            self._conv(x, rc, PK_CONV, A[f"e{k}_res"], F, 1, 2, 0, H // 2, self.P(rc, "bias"), None,
+                       join=dict(join_mode=C.JOIN_POOL, join_y=A[f"e{k}_y2"], join_ab=ab2,
+                                 join_out=A[f"e{k}_x"], join_argmax=A[f"e{k}_am"], join_H=H, join_W=H,
+                                 **self._jfin(b2, train)))
             x = Lazy(A[f"e{k}_x"], None, 0, H // 2, F)
+        if self._mid_hook is not None:                       # split-graph capture: the encoder graph ends here
+            self._mid_hook()
         prev = x                                             # x3 at r[3]
         for k, F in enumerate(DEC_FILTERS):
             t1, b1, t2, b2, rc = (next(n) for _ in range(5))
@@ -518,19 +493,16 @@ class UNetEngine:
             up = 0 if k == 0 else 1
             self._convt(Lazy(prev.t, None, 1, prev.H, prev.C), t1, A[f"d{k}_c1"], F, up, Rk,
                         self.P(t1, "bias"), self.bn[b1]["stats"] if train else None)
-            abA = self._bn_final(b1, train, consumer=True)       # finalized by the convT2 forward below
+            abA = self._bn_final(b1)                             # finalized by the convT2 forward below
             self._convt(Lazy(A[f"d{k}_c1"], abA, 1, Rk, F), t2, A[f"d{k}_c2"], F, 0, Rk,
                         self.P(t2, "bias"), self.bn[b2]["stats"] if train else None,
                         **self._xfin(b1, train))
-            abB = self._bn_final(b2, train, consumer=self.fuse_join)
-            if self.fuse_join:   # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
-                self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None,
-                           join=dict(join_mode=C.JOIN_ADD_UP if up else C.JOIN_ADD, join_y=A[f"d{k}_c2"],
-                                     join_ab=abB, join_out=A[f"d{k}_xlo"], join_H=Rk, join_W=Rk,
-                                     **self._jfin(b2, train)))
-            else:
-                self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None)
-                C.bn_add_fwd(A[f"d{k}_c2"], abB, A[f"d{k}_q"], up, A[f"d{k}_xlo"], B, Rk, Rk, F)
+            abB = self._bn_final(b2)
+            # residual 1x1 conv whose epilogue adds BN_B(c2) (4 pixels per q pixel when up)
+            self._conv(prev, rc, PK_CONV, A[f"d{k}_q"], F, 1, 1, 0, prev.H, self.P(rc, "bias"), None,
+                       join=dict(join_mode=C.JOIN_ADD_UP if up else C.JOIN_ADD, join_y=A[f"d{k}_c2"],
+                                 join_ab=abB, join_out=A[f"d{k}_xlo"], join_H=Rk, join_W=Rk,
+                                 **self._jfin(b2, train)))
             prev = Lazy(A[f"d{k}_xlo"], None, 0, Rk, F)
         hl = next(n)
         if train and self.fuse_head:             # the training step's head forward runs inside head_bwd (backward)
@@ -546,7 +518,7 @@ class UNetEngine:
         else dw_fwd + the streaming pointwise conv."""
         C, B = self.C, self.B
         stats = self.bn[bn]["stats"] if train else None
-        if self.fuse_sep and C.sep_fwd_supported(B, H, H, K, N):
+        if C.sep_fwd_supported(B, H, H, K, N):
             C.sep_fwd(x, ab, 1, self.P(layer, "depthwise_kernel"), self.W(layer, PK_PW), self.P(layer, "bias"), d, y,
                       stats, B, H, H, K, N, **xfin)
             return
@@ -563,8 +535,8 @@ class UNetEngine:
             self.C.dw_wgrad(*args)
 
     def backward(self) -> None:
-        self._wq = [] if self.defer_wgrad else None
-        self._dwq = [] if self.defer_wgrad else None
+        self._wq = []
+        self._dwq = []
         try:
             self._backward()
         finally:
@@ -609,22 +581,13 @@ class UNetEngine:
             # residual conv's dgrad below, which reads the same dxlo: it runs as that launch's side job
             bba_B = (dxlo, A[f"d{k}_c2"], bnB["ab"], bnB["sums"], D[f"d{k}_dc"], self.G(b2, "gamma"),
                      self.G(b2, "beta"), B * Rk * Rk, F, self.RS)
-            if not self.side_fuse:
-                C.bn_bwd_apply(*bba_B)
-            # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo)
-            # (k > 0, default) the 2x2 sum is formed by the dgrad's operand load, which also stores dq for the
-            # weight gradient (issued after it)
-            s2 = k > 0 and self.fold_sum2x2
-            if k == 0:
-                dq = dxlo
-            else:
-                dq = D[f"d{k}_dq"]
-                if not s2:
-                    C.node_bwd(dxlo, GM_SUM2X2, 0, None, 0, 0, None, dq, None, 0, dq, None, B, prevres, prevres, F)
+            # residual 1x1 conv R_k on prev: q = R(prev) at prevres, dq = dxlo (k=0) or sum2x2(dxlo) (k > 0: the
+            # 2x2 sum is formed by the dgrad's operand load, which also stores dq for the weight gradient)
+            dq = dxlo if k == 0 else D[f"d{k}_dq"]
             # bias grad of R_k: sum(dq) == sum(g_B) == dbeta_B (the BN_B node has no ReLU) -> grad_finish copy
             self._igemm(dq, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"d{k}_dres"], None, None, 0, B, prevres,
-                        prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if s2 else {}),
-                        **({"side_bba": bba_B} if self.side_fuse else {}))
+                        prevres, F, 0, prevres, prevres, cprev, 1, 1, 0, 0, **({"sum2x2": dxlo} if k > 0 else {}),
+                        side_bba=bba_B)
             self._wgrad(prev_t, dq, rc, None, 0, B, prevres, prevres, cprev, 0, prevres, prevres,
                         F, 1, 1, 0, 0, 0)
             # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
@@ -639,7 +602,7 @@ class UNetEngine:
             # for k > 0 this gradient is also BN_B(k-1)'s node gradient (its BN-backward sums accumulate here) -
             # the join runs in the convT1 dgrad's epilogue at half resolution (dxin is never stored)
             pjkw = {}
-            if k > 0 and self.fuse_pool_join:
+            if k > 0:
                 bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
                 pjkw = dict(pj_v=prev_t, pj_add=D[f"d{k}_dres"], pj_out=D[f"d{k}_dprev"], pj_sy=A[f"d{k - 1}_c2"],
                             pj_sab=bprev["ab"], pj_sums=bprev["sums"], pj_reps=self.RS)
@@ -648,13 +611,8 @@ class UNetEngine:
             # convT1: input relu(up?(prev))
             self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
                         Rk, F, 3, 1, 1, 1, 1)
-            if not pjkw and k > 0:
-                bprev = self.bn[names[17 + 5 * (k - 1) + 3]]
-                C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
-                           prev_t, None, 0, D[f"d{k}_dprev"], bprev["sums"], B, prevres, prevres, cprev, self.RS,
-                           sy=A[f"d{k - 1}_c2"], sab=bprev["ab"])
-            elif not pjkw:
-                C.node_bwd(D[f"d{k}_dxin"], GM_SUM2X2 if up else GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
+            if k == 0:          # x3 = the encoder output: relu-masked main path + residual path
+                C.node_bwd(D[f"d{k}_dxin"], GM_SAME, 1, D[f"d{k}_dres"], GM_SAME, 0, None,
                            prev_t, None, 0, D[f"d{k}_dprev"], None, B, prevres, prevres, cprev)
             dxlo = D[f"d{k}_dprev"]
         # encoder
@@ -670,102 +628,60 @@ class UNetEngine:
             else:
                 xin = Lazy(A[f"e{k - 1}_x"], None, 0, H, cin)
             bnb, bna = self.bn[b2], self.bn[b1]
-            fold = self.fold_pw
             # BN_b node: routed through the max-pool (no ReLU); independent of the residual 1x1 stride-2 conv's
             # dgrad on x_in (dres = W^T dx_out, read only by the last depthwise backward of this level), which reads
             # the same dx_out: the routing pass runs as that launch's side job
             pool_b = (dx_out, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], D[f"e{k}_g"], bnb["sums"], B, H, H, F, self.RS)
             # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
-                        H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0,
-                        **({"side_pool": pool_b} if self.side_fuse else {}))
-            if not self.side_fuse:
-                C.node_bwd(dx_out, GM_MAXPOOL, 0, None, 0, 0, A[f"e{k}_am"], A[f"e{k}_y2"], bnb["ab"], 0,
-                           D[f"e{k}_g"], bnb["sums"], B, H, H, F, self.RS)
-            if not fold:
-                C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y2"], bnb["ab"], bnb["sums"], D[f"e{k}_dy"],
-                               self.G(b2, "gamma"), self.G(b2, "beta"), B * H * H, F, self.RS)
-            # pointwise 2 (folded: its dgrad applies BN_b's backward on load and stores dy)
-            self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None,
-                        None, 0, B, H, H, F, 0, H, H, F, 1, 1, 0, 0,
-                        bwd=(A[f"e{k}_y2"], b2, D[f"e{k}_dy"]) if fold else None)
+                        H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0, side_pool=pool_b)
+            # pointwise 2: its dgrad applies BN_b's backward on load and stores dy
+            self._igemm(D[f"e{k}_g"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None,
+                        None, 0, B, H, H, F, 0, H, H, F, 1, 1, 0, 0, bwd=(A[f"e{k}_y2"], b2, D[f"e{k}_dy"]))
             self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
                         F, 0, H, H, F, 1, 1, 0, 0, 0)
-            # depthwise 2 on relu(BN_a(y1))
-            # depthwise 2 on relu(BN_a(y1)): dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue,
-            # and (fused pass) the weight gradient from the same dy rows
-            if self.fuse_dw_bwd:
-                C.dw_bwd(A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"],
-                         self.gslab[(s2, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, F,
-                         node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
-                         node_relu=1)
-            else:
-                self._dw_wgrad(A[f"e{k}_y1"], D[f"e{k}_dd2"], self.gslab[(s2, "depthwise_kernel")], bna["ab"], 1, B,
-                               H, H, F, self.C.STAT_REPLICAS)
-                C.dw_dgrad(D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"], B, H, H, F, 0,
-                           node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
-                           node_relu=1)
-            if not fold:
-                C.bn_bwd_apply(D[f"e{k}_g"], A[f"e{k}_y1"], bna["ab"], bna["sums"], D[f"e{k}_dy2"],
-                               self.G(b1, "gamma"), self.G(b1, "beta"), B * H * H, F, self.RS)
-            # pointwise 1
-            self._igemm(D[f"e{k}_g"] if fold else D[f"e{k}_dy2"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"],
-                        None, None, 0, B, H, H, F, 0, H, H, cin, 1, 1, 0, 0,
-                        bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]) if fold else None)
+            # depthwise 2 on relu(BN_a(y1)): dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
+            # and the weight gradient from the same dy rows, one pass
+            C.dw_bwd(A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"],
+                     self.gslab[(s2, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, F,
+                     node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
+                     node_relu=1)
+            # pointwise 1 (BN_a's backward applied on load)
+            self._igemm(D[f"e{k}_g"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"],
+                        None, None, 0, B, H, H, F, 0, H, H, cin, 1, 1, 0, 0, bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]))
             self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
                         H, cin, 0, H, H, F, 1, 1, 0, 0, 0)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                         1, 2, 0, 0, 0)
             # depthwise 1 on relu(x_in), and the gradient of x_in itself: the depthwise branch (ReLU-masked) plus the
-            # stride-2 scatter of dres; for k = 0 x_in is relu(BN0(y0)), a BN node (mask + sums)
+            # stride-2 scatter of dres, in one pass (dgrad + wgrad + the node join in the dgrad's epilogue); for
+            # k = 0 x_in is relu(BN0(y0)), a BN node (mask + sums)
             bn0 = self.bn[names[1]]
             out = D[f"e{k}_dx"] if k > 0 else D["g0"]
-            if self.fuse_dw_bwd:                # one pass: dgrad + wgrad + the node join in the dgrad's epilogue
-                nkw = dict(node_y=A["y0"], node_ab=bn0["ab"], node_sums=bn0["sums"], node_reps=self.RS,
-                           node_relu=1) if k == 0 else dict(mask_x=1)
-                C.dw_bwd(xin.t, xin.ab, 1, D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), out,
-                         self.gslab[(s1, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, cin,
-                         add_half=D[f"e{k}_dres"], **nkw)
-            else:
-                self._dw_wgrad(xin.t, D[f"e{k}_dd1"], self.gslab[(s1, "depthwise_kernel")], xin.ab, 1, B, H, H,
-                               cin, self.C.STAT_REPLICAS)
-                C.dw_dgrad(D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), D[f"e{k}_dz0"], B, H, H, cin)
-                if k > 0:
-                    C.node_bwd(D[f"e{k}_dz0"], GM_SAME, 1, D[f"e{k}_dres"], GM_SCATTER2, 0, None, xin.t, None, 0,
-                               out, None, B, H, H, cin)
-                else:
-                    C.node_bwd(D["e0_dz0"], GM_SAME, 0, D["e0_dres"], GM_SCATTER2, 0, None, A["y0"], bn0["ab"], 1,
-                               out, bn0["sums"], B, H, H, cin, self.RS)
+            nkw = dict(node_y=A["y0"], node_ab=bn0["ab"], node_sums=bn0["sums"], node_reps=self.RS,
+                       node_relu=1) if k == 0 else dict(mask_x=1)
+            C.dw_bwd(xin.t, xin.ab, 1, D[f"e{k}_dd1"], self.P(s1, "depthwise_kernel"), out,
+                     self.gslab[(s1, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, cin,
+                     add_half=D[f"e{k}_dres"], **nkw)
             if k > 0:
                 dx_out = out
-            else:
-                if self.fold_entry:        # the entry BN's backward apply folded into the entry wgrad's dy load
-                    C.entry_wgrad(self.images, self.idx, D["g0"], self.gslab[(names[0], "kernel")], B, self.S,
-                                  ENTRY_FILTERS, self.C.STAT_REPLICAS, bwd_y=A["y0"], bwd_ab=bn0["ab"],
-                                  bwd_sums=bn0["sums"], bwd_reps=self.RS, bwd_dx=D["dy0"],
-                                  bwd_dgamma=self.G(names[1], "gamma"), bwd_dbeta=self.G(names[1], "beta"))
-                else:
-                    C.bn_bwd_apply(D["g0"], A["y0"], bn0["ab"], bn0["sums"], D["dy0"], self.G(names[1], "gamma"),
-                                   self.G(names[1], "beta"), B * H * H, cin, self.RS)
-                    C.entry_wgrad(self.images, self.idx, D["dy0"], self.gslab[(names[0], "kernel")], B, self.S,
-                                  ENTRY_FILTERS, self.C.STAT_REPLICAS)
+            else:          # the entry BN's backward apply folded into the entry wgrad's dy load
+                C.entry_wgrad(self.images, self.idx, D["g0"], self.gslab[(names[0], "kernel")], B, self.S,
+                              ENTRY_FILTERS, self.C.STAT_REPLICAS, bwd_y=A["y0"], bwd_ab=bn0["ab"],
+                              bwd_sums=bn0["sums"], bwd_reps=self.RS, bwd_dx=D["dy0"],
+                              bwd_dgamma=self.G(names[1], "gamma"), bwd_dbeta=self.G(names[1], "beta"))
 
     def optimizer_step(self) -> None:
         self._await_all()
-        C = self.C
-        if self.fuse_opt:
-            cursor = self.batch_cursor if self.batch_table is not None else None
-            C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
-                       self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
-            if self.fp8:
-                self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8,
-                                self.max_rows8, self.amax8, self.n_views8)
-            return
-        C.adam_update(self.flat, self.grad, self.m, self.v, self.trainable, self.lr, self.b1, self.b2, self.adam_eps,
-                      self.step_t)
-        C.bn_moving_update(self.moving_table, len(self.bn_names), self.momentum)
-        self.pack(step=True)                               # also advances the Adam step counter
+        if self._share is not None:
+            raise RuntimeError("optimizer_step on an inference-only engine")
+        cursor = self.batch_cursor if self.batch_table is not None else None
+        self.C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
+                        self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
+        if self.fp8:
+            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8,
+                            self.max_rows8, self.amax8, self.n_views8)
 
     def bind_batches(self, batches: torch.Tensor) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
@@ -782,6 +698,9 @@ class UNetEngine:
             if lo < 0 or hi >= self.n_data:
                 raise ValueError(f"bind_batches: indices [{lo}, {hi}] outside the bound dataset of {self.n_data}")
         nb = batches.shape[0]
+        if self.batch_table is None and self.graph is not None:
+            raise RuntimeError("bind_batches: the step graph was captured without a batch table (it reads idx); "
+                               "bind a batch table before the first graph capture")
         if self.batch_table is not None and nb == self.batch_table.shape[0]:
             self.batch_table.copy_(batches)
             return
@@ -879,21 +798,54 @@ class UNetEngine:
         with torch.cuda.graph(g):
             self.train_step_eager()
         self.graph = g
+        # the same launch sequence split after the encoder forward into two graphs sharing the step's buffers (the
+        # engine allocates nothing during capture): replayed only for the first step after a FedAvg
+        pre, post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.stream(s):
+            pre.capture_begin()
+
+            def split():
+                pre.capture_end()
+                post.capture_begin(pool=pre.pool())
+            self._mid_hook = split
+            try:
+                self.train_step_eager()
+            finally:
+                self._mid_hook = None
+            post.capture_end()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        self.graph_pre, self.graph_post = pre, post
+
+    def _stall_wait(self, end: Optional[int]) -> None:
+        """Make the stream wait for the FedAvg buckets up to flat offset ``end`` (None: all); with ``stall_log``
+        set, bracket the wait with timing events (their elapsed time = how long the compute stream stalled)."""
+        if self.stall_log is None:
+            self._await_all() if end is None else self._await_range(end)
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        self._await_all() if end is None else self._await_range(end)
+        e1.record(cur)
+        self.stall_log.append((e0, e1))
 
     def train_step(self, use_graph: bool = True) -> None:
         """One training iteration: a replay of the captured hipGraph. After an overlapped FedAvg (``defer_until``)
-        the stream first waits (device-side event waits, no host sync) for every bucket's reduce + repack, then
-        replays: the ~70 Python-issued launches of an eager step cost milliseconds, the wait at most the tail of an
-        8 MB all-reduce (CFL_EAGER_AFTER_FEDAVG=1: the eager first step that waits per layer instead)."""
-        if use_graph and self.graph is not None and self._pending and not self.eager_after_fedavg:
-            self._await_all()
-        if use_graph and self.graph is not None and not self._pending:
-            self.graph.replay()
-        elif use_graph and self.graph is None:
+        the step replays as its two split graphs: the encoder graph waits (device-side event waits, no host sync)
+        only for the buckets holding the encoder's parameters and their repack, the rest of the step for every
+        bucket - so the later buckets' all-reduce runs under the encoder forward."""
+        if use_graph and self.graph is None:
             self.capture()
-            self.graph.replay()
-        else:
+        if not use_graph:
             self.train_step_eager()
+        elif self._pending:
+            self._stall_wait(self.split_at)
+            self.graph_pre.replay()
+            self._stall_wait(None)
+            self.graph_post.replay()
+        else:
+            self.graph.replay()
 
     def eval_step(self, use_graph: bool = True) -> None:
         """Inference-mode forward (moving BN statistics) of the batch in ``idx``; loss / accuracy accumulate into

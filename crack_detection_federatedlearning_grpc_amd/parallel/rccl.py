@@ -18,6 +18,7 @@ On CPU-only hosts the same code runs over gloo (tests).
 """
 from __future__ import annotations
 
+import os
 import time
 from datetime import timedelta
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -27,18 +28,27 @@ import torch
 import torch.distributed as dist
 
 
-def _buckets(n: int, bucket_elems: int) -> List[slice]:
-    return [slice(s, min(n, s + bucket_elems)) for s in range(0, n, bucket_elems)]
+def _buckets(n: int, bucket_elems: int, first: int = 0) -> List[slice]:
+    """Layer-ordered buckets of ``bucket_elems``; ``first`` > 0: the first bucket ends exactly there (e.g. at the
+    encoder's last parameter, so the next round's encoder forward waits for that bucket alone)."""
+    out, s = [], 0
+    if 0 < first < n:
+        out.append(slice(0, first))
+        s = first
+    out += [slice(a, min(n, a + bucket_elems)) for a in range(s, n, bucket_elems)]
+    return out
 
 
 class FedAvgAllReduce:
     def __init__(self, flat: torch.Tensor, table=None, world: Optional[int] = None, bucket_mb: float = 2.0,
-                 group=None):
+                 group=None, first_bucket: int = 0):
         self.flat = flat
         self.group = group
         self.world = world or dist.get_world_size(group)
-        self.buckets = _buckets(flat.numel(), max(1024, int(bucket_mb * (1 << 20)) // 4))
+        self.buckets = _buckets(flat.numel(), max(1024, int(bucket_mb * (1 << 20)) // 4), first_bucket)
         self._side = None
+        self.timing = False               # record hipEvents around each call's collectives (bench.py)
+        self.timings: List[tuple] = []    # per call: (issue, last all-reduce done, last bucket repacked) events
 
     def _weight(self, n_local: float, weighted: bool):
         """This client's FedAvg weight n_k / sum n. The sample-count all-reduce runs on EVERY call (each rank
@@ -79,6 +89,10 @@ class FedAvgAllReduce:
                 for sl in self.buckets:
                     on_bucket(sl)
             return []
+        t_issue = None
+        if self.timing:
+            t_issue = torch.cuda.Event(enable_timing=True)
+            t_issue.record(torch.cuda.current_stream(self.flat.device))
         w = self._weight(n_local, weighted)
         if self._side is None:
             # high priority: HIP gives it its own hardware queue (a default-priority stream may be multiplexed onto
@@ -86,18 +100,37 @@ class FedAvgAllReduce:
             # tools/overlap_summary.py), and the per-bucket repack that gates the next round's layers goes first
             self._side = torch.cuda.Stream(device=self.flat.device, priority=-1)
         out = []
-        for sl in self.buckets:
+        t_ar = None
+        for i, sl in enumerate(self.buckets):
             b = self.flat[sl]
             b.mul_(w)
             work = dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             with torch.cuda.stream(self._side):
                 work.wait()                                   # side stream <- this bucket's collective
+                if self.timing and i == len(self.buckets) - 1:
+                    t_ar = torch.cuda.Event(enable_timing=True)
+                    t_ar.record(self._side)
                 if on_bucket is not None:
                     on_bucket(sl)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=self.timing)
                 ev.record(self._side)
             out.append((sl, ev))
+        if self.timing:
+            self.timings.append((t_issue, t_ar, out[-1][1]))
         return out
+
+    def timing_summary(self) -> Dict[str, float]:
+        """Mean over the recorded calls (events must be complete, e.g. after a synchronize): ``allreduce_ms`` =
+        issue of the first bucket's pre-scale on the compute stream -> last bucket's all-reduce done on the side
+        stream (weight all-reduce + bucketed SUM all-reduces); ``allreduce_repack_ms`` = ... -> last bucket's bf16
+        repack done."""
+        if not self.timings:
+            return {}
+        ar = [a.elapsed_time(b) for a, b, _ in self.timings]
+        rp = [a.elapsed_time(c) for a, _, c in self.timings]
+        return {"allreduce_ms": float(np.mean(ar)), "allreduce_repack_ms": float(np.mean(rp)),
+                "allreduce_calls": len(ar), "allreduce_buckets": len(self.buckets),
+                "allreduce_bytes": int(self.flat.numel() * self.flat.element_size())}
 
 
 class RcclAggregator:
@@ -140,10 +173,10 @@ class RcclAggregator:
                    int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)),
                    backend=getattr(cfg, "dist_backend", None) or None)
 
-    def _reducer(self, flat: torch.Tensor) -> FedAvgAllReduce:
-        key = (flat.data_ptr(), flat.numel())
+    def _reducer(self, flat: torch.Tensor, first_bucket: int = 0) -> FedAvgAllReduce:
+        key = (flat.data_ptr(), flat.numel(), first_bucket)
         if self._cached is None or self._cached[0] != key:
-            self._cached = (key, FedAvgAllReduce(flat, world=self.world))
+            self._cached = (key, FedAvgAllReduce(flat, world=self.world, first_bucket=first_bucket))
         return self._cached[1]
 
     def average(self, arrays: Sequence[np.ndarray], n_local: float) -> List[np.ndarray]:
@@ -160,10 +193,11 @@ class RcclAggregator:
         return out
 
     def average_device(self, flat: torch.Tensor, n_local: float,
-                       on_bucket: Optional[Callable[[slice], None]] = None) -> List[Tuple[slice, object]]:
+                       on_bucket: Optional[Callable[[slice], None]] = None,
+                       first_bucket: int = 0) -> List[Tuple[slice, object]]:
         """Device-resident FedAvg of a trainer's flat fp32 parameter buffer, in place: bucketed weighted
         all-reduce on a side stream (no host staging); returns the per-bucket events for ``defer_until``."""
-        return self._reducer(flat).average_async(float(max(n_local, 1)), on_bucket=on_bucket)
+        return self._reducer(flat, first_bucket).average_async(float(max(n_local, 1)), on_bucket=on_bucket)
 
     def wait_complete(self, events: Sequence[Tuple[slice, object]]) -> None:
         """Host-side completion check with a deadline: poll the last bucket's event (recorded after every earlier
@@ -179,23 +213,50 @@ class RcclAggregator:
             time.sleep(5e-5)
 
     def fedavg_device(self, flat: torch.Tensor, n_local: float,
-                      on_bucket: Optional[Callable[[slice], None]] = None) -> List[Tuple[slice, object]]:
+                      on_bucket: Optional[Callable[[slice], None]] = None,
+                      first_bucket: int = 0) -> List[Tuple[slice, object]]:
         """``average_device`` + ``wait_complete`` with rollback: the buckets are pre-scaled (w_k * n_k / sum n) and
         reduced in place, so a failure part-way would leave ``flat`` a mix of scaled, reduced and untouched
-        buckets. The buffer is copied first (8 MB device copy); on any failure the communicator is aborted (no
-        collective still writes ``flat``), the local model restored and the error re-raised - the caller then
-        uploads its unchanged local weights over gRPC."""
+        buckets. The buffer is copied first (8 MB device copy); on any failure the communicator is aborted, the
+        side stream drained (no queued bucket work lands after the restore), the local model restored and the
+        error re-raised - the caller then uploads its unchanged local weights over gRPC.
+
+        The host waits (with the deadline) for the last bucket here, so the rollback needs nothing later; in the
+        product path that wait is the collective itself plus the ranks' arrival skew - the control-plane chain
+        behind it (rank 0's upload, the server's aggregation, the VERSION long-poll) is taken off the round's
+        critical path by the client's asynchronous report (fl/client.py, ``async_upload``)."""
         if self._backup is None or self._backup.numel() != flat.numel() or self._backup.device != flat.device:
             self._backup = torch.empty_like(flat)
         self._backup.copy_(flat)
         try:
-            evs = self.average_device(flat, n_local, on_bucket=on_bucket)
+            evs = self.average_device(flat, n_local, on_bucket=on_bucket, first_bucket=first_bucket)
             self.wait_complete(evs)
             return evs
         except BaseException:
             self.abort()
+            self._drain_side(flat)
             flat.copy_(self._backup)
             raise
+
+    def _drain_side(self, flat: torch.Tensor, drain_s: float = 30.0) -> None:
+        """After an abort, work still queued on the aggregation side stream (the in-place all-reduce output of an
+        issued bucket, the per-bucket bf16 repacks) could land AFTER the rollback and overwrite the restored
+        weights with a partly reduced bucket. Wait (host deadline) for the side stream to drain and order the
+        current stream behind it; if it never drains the weights cannot be trusted: exit non-zero."""
+        red = self._cached[1] if self._cached is not None else None
+        side = red._side if red is not None else None
+        if side is None or flat.device.type != "cuda":
+            return
+        ev = torch.cuda.Event()
+        ev.record(side)
+        end = time.monotonic() + drain_s
+        while not ev.query():
+            if time.monotonic() > end:
+                print(f"[rccl] aggregation side stream did not drain {drain_s:.0f} s after the abort; the local "
+                      f"weights may be partly overwritten - exiting", flush=True)
+                os._exit(70)
+            time.sleep(1e-3)
+        torch.cuda.current_stream(flat.device).wait_stream(side)
 
     def abort(self) -> None:
         """A peer died or a collective timed out: tear the communicator down without a collective shutdown

@@ -129,15 +129,15 @@ class LocalFit:
 
     def fedavg_device(self, aggregator, n_local: float) -> bool:
         """Device-resident FedAvg (RCCL data plane): reduce the engine's flat fp32 parameter buffer in place,
-        bucketed on a side stream with each bucket's layers repacked to bf16 there, and wait (host deadline) for
-        the last bucket. On failure the aggregator has restored the local parameters; the bf16 copies, which the
+        bucketed on a side stream (first bucket = the encoder's parameters) with each bucket's layers repacked to
+        bf16 there, and wait (host deadline) for the last bucket. On failure the aggregator has restored the local parameters; the bf16 copies, which the
         side stream may have partly repacked, are rebuilt from them before the error propagates (the client
         then uploads its local model over gRPC). False when the backend holds no device buffer."""
         eng = getattr(self.backend, "eng", None)
         if eng is None or eng.flat.device.type != "cuda" or not hasattr(aggregator, "fedavg_device"):
             return False
         try:
-            evs = aggregator.fedavg_device(eng.flat, n_local, on_bucket=eng.pack_bucket)
+            evs = aggregator.fedavg_device(eng.flat, n_local, on_bucket=eng.pack_bucket, first_bucket=eng.split_at)
         except BaseException:
             eng.defer_until([])
             eng.pack()

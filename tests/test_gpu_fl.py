@@ -94,6 +94,11 @@ def test_bench_two_ranks_share_one_gpu():
     assert out["n_gpus"] == 2 and out["dist_backend"] == "gloo" and out["value"] > 0
     assert out["config"]["global_batch"] == 32
     assert out["fedavg_max_abs_err"] < 1e-5, out["fedavg_max_abs_err"]
+    # the N>1 line describes the data plane (BASELINE configs 3 / 5): all-reduce time, the compute stream's
+    # exposed share of it and the overlap fraction, measured with hipEvents inside the timed region
+    for k in ("allreduce_ms", "allreduce_repack_ms", "allreduce_exposed_ms", "overlap_fraction", "allreduce_buckets"):
+        assert k in out, (k, sorted(out))
+    assert out["allreduce_repack_ms"] >= out["allreduce_ms"] >= 0.0 and 0.0 <= out["overlap_fraction"] <= 1.0
     assert p.stdout.count("[bench] rank ") == 2                                 # each rank logged its view
 
 

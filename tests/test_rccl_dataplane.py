@@ -170,6 +170,12 @@ def test_rccl_device_path_sends_no_parameters(tmp_path):
     assert all(p["payload_bytes"] > 0 for p in by_rank[0])
     # round 1's reply (RESP_ARY or NOT_WAIT) carried no parameters to either client
     assert all(p.get("reply_bytes", 0) == 0 for ph in phases.values() for p in ph), phases
+    # async report (cfg.async_upload): round 1 was reported from a background thread while round 2 trained (its
+    # phase record carries the exposed part: the collective + the join), the last round synchronously (FIN)
+    for ph in phases.values():
+        assert [p["round"] for p in ph] == [1, 2]
+        assert [p.get("async_upload", False) for p in ph] == [True, False], ph
+        assert ph[0]["exposed_s"] >= ph[0]["aggregate_s"] and ph[0]["join_wait_s"] >= 0.0
 
 
 def test_rccl_failure_mid_bucket_uploads_local_model(tmp_path):
