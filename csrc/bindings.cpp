@@ -947,6 +947,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_CONV3_WS_GRID") = (int)TUNE_CONV3_WS_GRID;
   m.attr("TUNE_WGRAD_GROUP") = (int)TUNE_WGRAD_GROUP;
   m.attr("TUNE_CONV3_DEEP") = (int)TUNE_CONV3_DEEP;
+  m.attr("TUNE_CONV3_SK") = (int)TUNE_CONV3_SK;
+  m.attr("TUNE_CONV3_SK_CFG") = (int)TUNE_CONV3_SK_CFG;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;
   m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;

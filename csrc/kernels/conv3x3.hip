@@ -814,8 +814,10 @@ static bool big_tiles(const ConvParams& p) {
 }
 
 bool conv3x3_deep_eligible(const ConvParams& p);
+bool conv3x3_sk_eligible(const ConvParams& p);
+int conv3x3_sk(const ConvParams& p, hipStream_t st);
 int conv3x3_splits(const ConvParams& p) {
-  return small_tiles(p) || ws_eligible(p) || conv3x3_deep_eligible(p) || big_tiles(p)
+  return conv3x3_sk_eligible(p) || small_tiles(p) || ws_eligible(p) || conv3x3_deep_eligible(p) || big_tiles(p)
              ? 1 : conv3x3_split_k(p);
 }
 
@@ -846,6 +848,8 @@ int conv3x3_deep(const ConvParams& p, hipStream_t st);
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_supported(p)) return 1;
   if (p.bwd.y) return 6;                    // the BN-backward operand is applied by a separate pass (conv_igemm)
+  // low-resolution deep-K layers: K split over the block's waves, 32x32 MFMA register tiles (conv3x3_sk.hip)
+  if (conv3x3_sk_eligible(p)) return conv3x3_sk(p, st);
   if (p.xfin.stats && (p.pj.v || p.xf.C > 256 || !(ws_eligible(p) || use_wb(p)))) {
     // a kernel without the consumer-side finalize: finalize first, then the plain call
     const int rc = bn_finalize(p.xfin.stats, p.xfin.gamma, p.xfin.beta, nullptr, nullptr, const_cast<float*>(p.xf.ab),

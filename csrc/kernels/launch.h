@@ -486,7 +486,11 @@ enum TuneKey {
   TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 4M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
   TUNE_PW_NB = 39,             // streaming 1x1 kernel, N % 128 == 0 and K >= 128: 0 = 128-channel output slices at
                                // M >= 1M pixels (else 64), 64 = always 64, 128 = always 128
-  TUNE_N = 40
+  TUNE_CONV3_SK = 40,          // conv3x3 low-resolution deep-K layers: 0 = split-K-in-block 32x32 MFMA kernel
+                               //   (conv3x3_sk.hip) where eligible, 1 = off, 2 = force wherever the shape allows
+  TUNE_CONV3_SK_CFG = 41,      // ... tile config: 0 = heuristic, 1 = 8x8 px x 64 ch, 2 = 8x16 x 64, 3 = 16x16 x 32,
+                               //   4 = 8x16 x 32
+  TUNE_N = 42
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

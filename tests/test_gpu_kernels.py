@@ -1067,6 +1067,28 @@ def test_conv3x3_deep_dma_forced(B, Hs, Cin, N, up, use_ab):
         C_.set_tune(C_.TUNE_CONV3_WS, 0)
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [
+    (2, 16, 128, 64, 0, True),       # 4 chunks: the 3-stage weight ring wraps
+    (2, 8, 256, 128, 1, False),      # upsampled input (8 chunks), ReLU-only producer transform
+    (2, 16, 64, 64, 0, True),        # 2 chunks (shorter than the ring)
+    (3, 16, 32, 64, 0, False),       # 1 chunk
+])
+def test_conv3x3_sk_forced(B, Hs, Cin, N, up, use_ab, cfg):
+    """TUNE_CONV3_SK=2 forces the split-K-in-block kernel (conv3x3_sk.hip: 4 waves split each chunk's (tap, k-step)
+    units, 32x32x16 MFMA register tiles, LDS-DMA weight ring + register-staged transformed halo, partial tiles
+    summed through LDS) in each tile config; output and BN statistics vs the generic implicit GEMM and the fp32
+    reference."""
+    C_ = hip()
+    C_.set_tune(C_.TUNE_CONV3_SK, 2)
+    C_.set_tune(C_.TUNE_CONV3_SK_CFG, cfg)
+    try:
+        test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
+    finally:
+        C_.set_tune(C_.TUNE_CONV3_SK, 0)
+        C_.set_tune(C_.TUNE_CONV3_SK_CFG, 0)
+
+
 @pytest.mark.parametrize("deep", [False, True])
 def test_conv3x3_weight_stationary_node_epilogue(deep):
     if deep:
@@ -1787,7 +1809,8 @@ def test_dw_bwd_residual_join_matches_node_bwd(B, H, W, C, bn):
 
 
 @pytest.mark.parametrize("B,H,Cin,N,tune", [(2, 32, 64, 128, ""), (2, 16, 128, 256, ""), (2, 24, 32, 64, "ws"),
-                                            (2, 16, 64, 64, "small"), (2, 20, 64, 64, "")])
+                                            (2, 16, 64, 64, "small"), (2, 20, 64, 64, ""), (2, 32, 128, 64, "sk"),
+                                            (2, 32, 256, 256, "sk")])
 def test_conv3x3_pool_join_matches_node_bwd(B, H, Cin, N, tune):
     """Decoder node join in the 3x3 dgrad epilogue (conv_igemm pj_*: 2x2 sum of the conv output, ReLU mask from the
     half-resolution input, + residual gradient, BN-backward sums with xhat from another tensor) equals the conv into
@@ -1795,7 +1818,7 @@ def test_conv3x3_pool_join_matches_node_bwd(B, H, Cin, N, tune):
     per-tile (incl. ragged 20x20), weight-stationary and 8x8-tile kernels."""
     torch.manual_seed(57)
     C_ = hip()
-    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2)}
+    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "sk": (C_.TUNE_CONV3_SK, 2)}
     if tune:
         C_.set_tune(*keys[tune])
     try:
@@ -1855,14 +1878,15 @@ def test_dw_fwd_consumer_finalize_matches_bn_finalize(B, H, C):
 
 
 @pytest.mark.parametrize("B,Hs,Cin,N,tune", [(2, 16, 64, 64, ""), (2, 16, 32, 64, "ws"), (2, 16, 64, 32, "ws"),
-                                              (3, 8, 256, 128, "small"), (2, 12, 128, 64, "")])
+                                              (3, 8, 256, 128, "small"), (2, 12, 128, 64, ""), (2, 16, 256, 128, "sk"),
+                                              (2, 32, 128, 128, "sk")])
 def test_conv3x3_consumer_finalize_matches_bn_finalize(B, Hs, Cin, N, tune):
     """Consumer-side BN finalize of a 3x3 conv's input (conv_igemm xfin_*: per-tile, weight-stationary and 8x8-tile
     kernels compute the input BN's (a, b) from the replica sums in LDS and write the ab rows) equals bn_finalize +
     the conv bit for bit: same output, statistics and ab rows."""
     torch.manual_seed(61)
     C_ = hip()
-    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2)}
+    keys = {"ws": (C_.TUNE_CONV3_WS, 2), "small": (C_.TUNE_CONV3_SMALL, 2), "sk": (C_.TUNE_CONV3_SK, 2)}
     if tune:
         C_.set_tune(*keys[tune])
     try:

@@ -36,24 +36,28 @@ def case(B, H, Cin, N, up=0):
     ab = torch.rand(4 * Cin, device=dev) + 0.5
     bias = torch.zeros(N, device=dev)
     out = {}
-    for name, kw, tune in [("default", dict(stats=stats, ab=ab, relu=1), {}),
-                           ("no-stats", dict(stats=None, ab=ab, relu=1), {}),
-                           ("no-xform", dict(stats=stats, ab=None, relu=0), {}),
-                           ("BN32", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_BN: 32}),
-                           ("per-tap-B", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_WB: 2}),
-                           ("ws", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_WS: 2}),
-                           ("small", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 2}),
-                           ("8x16x32", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 1, C.TUNE_CONV3_BN: 32}),
-                           ("8x16x64", dict(stats=stats, ab=ab, relu=1), {C.TUNE_CONV3_SMALL: 1}),
-                           ("generic", dict(stats=stats, ab=ab, relu=1, algo=1), {})]:
+    std = dict(stats=stats, ab=ab, relu=1)
+    variants = [("default", std, {}), ("no-sk", std, {C.TUNE_CONV3_SK: 1})]
+    variants += [(f"sk{c}", std, {C.TUNE_CONV3_SK: 2, C.TUNE_CONV3_SK_CFG: c}) for c in (1, 2, 3, 4)]
+    variants += [("sk-plain", dict(stats=stats, ab=None, relu=0), {C.TUNE_CONV3_SK: 2})]
+    if not os.environ.get("PROBE_SK_ONLY"):
+        variants += [("no-stats", dict(stats=None, ab=ab, relu=1), {C.TUNE_CONV3_SK: 1}),
+                     ("no-xform", dict(stats=stats, ab=None, relu=0), {C.TUNE_CONV3_SK: 1}),
+                     ("BN32", std, {C.TUNE_CONV3_SK: 1, C.TUNE_CONV3_BN: 32}),
+                     ("ws", std, {C.TUNE_CONV3_WS: 2}),
+                     ("small", std, {C.TUNE_CONV3_SMALL: 2}),
+                     ("deep", std, {C.TUNE_CONV3_DEEP: 2}),
+                     ("8x16x64", std, {C.TUNE_CONV3_SK: 1, C.TUNE_CONV3_SMALL: 1}),
+                     ("generic", dict(std, algo=1), {})]
+    for name, kw, tune in variants:
         for k, v in tune.items():
             C.set_tune(k, v)
-        algo = kw.pop("algo", 0)
+        algo = kw.get("algo", 0)
         try:
             t = timeit(lambda: C.conv_igemm(x, wt, bias, y, kw["stats"], kw["ab"], kw["relu"], B, Hin, Hin, Cin, up,
                                             H, H, N, 3, 1, 1, 1, None, algo))
             out[name] = f"{t:6.1f}"
-        except RuntimeError as e:
+        except RuntimeError:
             out[name] = "  n/a"
         for k in tune:
             C.set_tune(k, 0)
