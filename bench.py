@@ -209,8 +209,9 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    n_ar0 = 0
     if agg is not None:            # FedAvg cost inside the timed region only (hipEvents, read after the run)
-        agg.timings.clear()
+        n_ar0 = len(agg.timings)
         eng.stall_log = []
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -229,11 +230,22 @@ def main() -> int:
         dt = float(t.item())
     fedavg_stats = {}
     if agg is not None:
+        # all-reduces issued inside the timed region (round r's FedAvg, consumed by round r+1's first step)
+        timed = agg.timings[n_ar0:]
+        agg.timings = timed
         fedavg_stats = agg.timing_summary()
-        # the compute stream's stalls on the FedAvg buckets (two waits per post-FedAvg step: before the encoder
-        # graph, before the rest); the timed region's last all-reduce is waited by the closing synchronize instead
-        stalls = [a.elapsed_time(b) for a, b in eng.stall_log]
-        per = [sum(stalls[i:i + 2]) for i in range(0, len(stalls) - 1, 2)]
+        # exposed FedAvg time per consumed all-reduce: from the compute stream's end of round r (the FedAvg issue
+        # event) to the first kernel of round r+1's encoder graph (the event after its bucket-0 wait) - pre-scale,
+        # host-side collective launches and any wait included - plus the stall before the rest of that step. The
+        # first timed step consumes the warm-up's all-reduce across the host barrier (not counted); the timed
+        # region's last all-reduce is waited by the closing synchronize.
+        st = eng.stall_log
+        per = []
+        for j in range(1, len(st) // 2):
+            if j - 1 < len(timed):
+                pre_after = st[2 * j][1]
+                post_before, post_after = st[2 * j + 1]
+                per.append(timed[j - 1][0].elapsed_time(pre_after) + post_before.elapsed_time(post_after))
         if per and fedavg_stats:
             exp = float(np.mean(per))
             fedavg_stats["allreduce_exposed_ms"] = exp

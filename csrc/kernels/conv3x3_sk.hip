@@ -48,6 +48,13 @@ CFL_DEVICE void sk_dma16(const void* src, bf16_t* lds_wave_base) {
 template <int N>
 CFL_DEVICE void sk_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// keep the issue order of the memory operations on either side (compiler and machine scheduler): the counted
+// vmcnt waits assume the halo loads of a step are issued before its weight DMAs
+CFL_DEVICE void sk_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // LDS store the compiler cannot see (hipcc would order a visible LDS store after ALL outstanding LDS-DMA loads,
 // draining the weight chunks in flight); it only touches the halo stage no DMA writes.
 CFL_DEVICE void sk_store16(bf16_t* p, uint4 v) {
@@ -76,7 +83,7 @@ struct SkCfg {
   static_assert(HWL >= HWR && HWL % 8 == 0, "halo pitch");
 };
 
-template <int TH, int TW, int BN, bool PJ, bool XFIN>
+template <int TH, int TW, int BN, int NCH, bool PJ, bool XFIN>
 __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
   using S = SkCfg<TH, TW, BN>;
   constexpr int BM = S::BM, HWL = S::HWL, HWR = S::HWR, FM = S::FM, FN = S::FN;
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
   constexpr int LDC = S::LDC;
 
   // ONE shared object (a second one can make hipcc drain the DMAs before every ds_read)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[S::SMEM + 2 * 4 * BN * 4 + (XFIN ? 2 * SK_MAX_CIN * 4 : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[S::SMEM + 2 * 4 * BN * 4 + 2 * SK_MAX_CIN * 4];
   bf16_t* wring = reinterpret_cast<bf16_t*>(smem);                    // [WSTAGES][9*BN rows][32]
   bf16_t* hring = wring + WSTAGES * S::WST;                           // [HSTAGES][HROWS][32]
   float (*sred)[4][BN] = reinterpret_cast<float (*)[4][BN]>(smem + S::SMEM);
@@ -98,13 +105,21 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
   const int b = tile / tiles_hw, tr = tile - b * tiles_hw;
   const int ty0 = (tr / tiles_w) * TH, tx0 = (tr % tiles_w) * TW;
   const int nBlock = bn_idx * BN;
-  const int chunks = p.Cin / BK;
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
   const bool has_ab = p.xf.ab != nullptr;
   const int relu = p.xf.relu;
   const bool xform = has_ab || relu;
 
-  if constexpr (XFIN) {          // consumer-side BN finalize of the input transform (first block writes the rows)
+  // producer BN coefficients of every input channel in LDS (a transform reads them per chunk; a global load there
+  // would be counted behind the weight DMAs in flight and drain them). XFIN: consumer-side BN finalize (computed
+  // from the producer's replica sums; the first block writes the layer's ab rows).
+  if constexpr (!XFIN) {
+    if (has_ab && tid < p.Cin) {
+      sxab[tid] = p.xf.ab[tid];
+      sxab[SK_MAX_CIN + tid] = p.xf.ab[p.xf.C + tid];
+    }
+    __syncthreads();
+  } else {
     if (tid < p.Cin) {
       float a, bb, mean, rstd;
       bn_coef_from_stats(p.xfin, p.Cin, tid, a, bb, mean, rstd);
@@ -152,43 +167,46 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
     hvalid |= (ok ? 1u : 0u) << i;
     hsrc[i] = ok ? p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + q * 8
                  : reinterpret_cast<const bf16_t*>(g_sk_zero);
-    hrow[i] = e < HPIECES ? hy * HWL + hx : -1;
+    hrow[i] = e < HPIECES ? hy * HWL + hx : HWR;              // past the halo: line 0's first pad row (never read)
   }
-  uint4 rh[H_PER_T];
+  // The halo loads are inline asm: hipcc's waitcnt pass does not count the LDS-DMAs issued after them, so for a
+  // compiler-visible load it drains vmcnt to 0 before the first use - and with it the weight DMAs of the chunk two
+  // steps ahead. Here the counted sk_wait_h below is the only wait, and it ties the registers (no use moves above it).
+  u4v rh[H_PER_T];
   auto load_h = [&](int ch) {                         // unconditional loads: a fixed vmcnt count per wave
 #pragma unroll
-    for (int i = 0; i < H_PER_T; ++i)
-      rh[i] = *reinterpret_cast<const uint4*>(hsrc[i] + (((hvalid >> i) & 1u) ? ch * BK : 0));
+    for (int i = 0; i < H_PER_T; ++i) {
+      const bf16_t* src = hsrc[i] + (((hvalid >> i) & 1u) ? ch * BK : 0);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rh[i]) : "v"(src) : "memory");
+    }
+  };
+  auto tie_h = [&]() {                                // after a counted wait: the halo registers are valid now
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) asm volatile("" : "+v"(rh[i]));
   };
   auto store_h = [&](int ch) {                        // producer transform on the way into LDS; padding stays 0
     float ha[8], hb[8];
     const int c8 = ch * BK + (tid & 3) * 8;           // every piece of this thread has channel quarter tid & 3
-    if constexpr (XFIN) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ha[j] = sxab[c8 + j];
-        hb[j] = sxab[SK_MAX_CIN + c8 + j];
-      }
-    } else {
-      load_f8_or(p.xf.ab + c8, has_ab, 1.f, ha);
-      load_f8_or(p.xf.ab + p.xf.C + c8, has_ab, 0.f, hb);
+    for (int j = 0; j < 8; ++j) {
+      ha[j] = has_ab ? sxab[c8 + j] : 1.f;
+      hb[j] = has_ab ? sxab[SK_MAX_CIN + c8 + j] : 0.f;
     }
     bf16_t* st = hring + (ch % HSTAGES) * S::HST;
+    // branch-free (divergent branches here made hipcc fall back to draining every DMA in flight): pieces past the
+    // halo go to an unused pad row, out-of-image pieces keep their zero
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
-      if (hrow[i] < 0) continue;
-      uint4 v = rh[i];
-      if (xform && ((hvalid >> i) & 1u)) {
-        float f[8];
-        unpack8(v, f);
+      const bool ok = (hvalid >> i) & 1u;
+      float f[8];
+      unpack8(make_uint4(rh[i][0], rh[i][1], rh[i][2], rh[i][3]), f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f[j] = fmaf(ha[j], f[j], hb[j]);
-          if (relu) f[j] = fmaxf(f[j], 0.f);
-        }
-        v = pack8(f);
+      for (int j = 0; j < 8; ++j) {
+        const float t = fmaf(ha[j], f[j], hb[j]);
+        const float r = relu ? fmaxf(t, 0.f) : t;
+        f[j] = ok ? r : 0.f;
       }
-      sk_store16(st + sk_off(hrow[i], (tid + i * NT) & 3), v);
+      sk_store16(st + sk_off(hrow[i], (tid + i * NT) & 3), pack8(f));
     }
   };
 
@@ -228,32 +246,40 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mf][nf][r] = 0.f;
 
-  // ---- prologue: weights of chunks 0 and 1 in flight, halo 0 stored, halo 1 in registers ----
-  issue_w(0);
-  if (chunks > 1) issue_w(1);
+  // ---- pipeline, fully unrolled over the NCH chunks (no loop-carried accumulator or load registers: a loop made
+  //      hipcc copy the accumulators AGPR <-> VGPR and drain every DMA in flight at the loop head) ----
+  // issue order per chunk step c: [halo loads of c + 1] [weight DMAs of c + 2]; waits count the younger ops only.
+  const int wcnt = wfull ? W_PER : W_PER - 1;                 // this wave's DMAs per chunk (wave-uniform)
+  (void)wcnt;
   load_h(0);
-  sk_wait_vm<0>();
+  sk_order();
+  issue_w(0);
+  if (NCH > 1) issue_w(1);
+  sk_order();
+  if (NCH > 1) { if (wfull) sk_wait_vm<2 * W_PER>(); else sk_wait_vm<2 * W_PER - 2>(); }
+  else { if (wfull) sk_wait_vm<W_PER>(); else sk_wait_vm<W_PER - 1>(); }
+  tie_h();
   store_h(0);
-  if (chunks > 1) load_h(1);
-
-  for (int ch = 0; ch < chunks; ++ch) {
-    // weights of chunk ch landed: at most the DMAs of chunk ch + 1 and the halo loads of chunk ch + 1 are younger
-    if (ch + 1 < chunks) {
-      if (wfull) sk_wait_vm<W_PER + H_PER_T>();
-      else sk_wait_vm<W_PER - 1 + H_PER_T>();
-    } else {
-      sk_wait_vm<0>();
-    }
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    // weights of chunk ch landed: only the DMAs of chunk ch + 1 may still be in flight
+    if (ch + 1 < NCH) { if (wfull) sk_wait_vm<W_PER>(); else sk_wait_vm<W_PER - 1>(); }
+    else sk_wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // this thread's halo stores of chunk ch
-    __builtin_amdgcn_s_barrier();                             // every wave's part landed; ring stage ch - 1 free
-    if (ch + 2 < chunks) issue_w(ch + 2);
+    __builtin_amdgcn_s_barrier();                             // every wave's part landed; stages of ch - 1 free
+    if (ch + 1 < NCH) load_h(ch + 1);                         // in flight during this chunk's MFMAs
+    sk_order();                                               // (the waits count the halo loads as the older ops)
+    if (ch + 2 < NCH) issue_w(ch + 2);
+    sk_order();
     const bf16_t* sw = wring + (ch % WSTAGES) * S::WST;
     const bf16_t* sh = hring + (ch % HSTAGES) * S::HST;
-    // this wave's units u = wid + 4 j of the chunk's 18 (tap, 16-channel k-step) units
+    // this wave's units u = wid + 4 j of the chunk's 18 (tap, 16-channel k-step) units; waves 2 and 3 run a
+    // 5th unit against a zero weight fragment (no branch: the chunk step takes the 5-unit waves' time anyway)
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      const int u = wid + 4 * j;
-      if (j == 4 && u >= 18) break;
+      const int u0 = wid + 4 * j;
+      const bool live = j < 4 || u0 < 18;
+      const int u = live ? u0 : 17;
       const int tap = u >> 1, s = u & 1;
       const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;     // tap / 3 for tap < 9
       const int q = 2 * s + kh;
@@ -261,23 +287,22 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
 #pragma unroll
       for (int mf = 0; mf < FM; ++mf) af[mf] = *reinterpret_cast<const s8v*>(sh + sk_off(fa[mf] + ky * HWL + kx, q));
 #pragma unroll
-      for (int nf = 0; nf < FN; ++nf)
-        bfg[nf] = *reinterpret_cast<const s8v*>(sw + sk_off(tap * BN + nf * 32 + (lane & 31), q));
+      for (int nf = 0; nf < FN; ++nf) {
+        const s8v w = *reinterpret_cast<const s8v*>(sw + sk_off(tap * BN + nf * 32 + (lane & 31), q));
+        bfg[nf] = live ? w : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+      }
 #pragma unroll
       for (int mf = 0; mf < FM; ++mf)
 #pragma unroll
         for (int nf = 0; nf < FN; ++nf)
           acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mf], bfg[nf], acc[mf][nf], 0, 0, 0);
     }
-    if (ch + 1 < chunks) {                                    // halo of chunk ch + 1 -> the other halo stage
-      if (ch + 2 < chunks) {
-        if (wfull) sk_wait_vm<W_PER>();
-        else sk_wait_vm<W_PER - 1>();
-      } else {
-        sk_wait_vm<0>();
-      }
+    if (ch + 1 < NCH) {                                       // halo of chunk ch + 1 -> the other halo stage
+      __builtin_amdgcn_sched_barrier(0);                      // (the wait stays behind this chunk's MFMAs)
+      if (ch + 2 < NCH) { if (wfull) sk_wait_vm<W_PER>(); else sk_wait_vm<W_PER - 1>(); }
+      else sk_wait_vm<0>();
+      tie_h();
       store_h(ch + 1);
-      if (ch + 2 < chunks) load_h(ch + 2);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -382,50 +407,56 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
   }
 }
 
-template <int TH, int TW, int BN>
-int launch_sk(const ConvParams& p, hipStream_t st) {
+template <int TH, int TW, int BN, int NCH>
+int launch_sk_n(const ConvParams& p, hipStream_t st) {
   const int blocks = (p.Ho / TH) * (p.Wo / TW) * p.B * (p.N / BN);
-  if (p.xfin.stats) {
-    if (p.Cin > SK_MAX_CIN || p.pj.v) return 1;
-    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, false, true>), dim3(blocks), dim3(NT), 0, st, p);
-  } else if (p.pj.v) {
-    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, true, false>), dim3(blocks), dim3(NT), 0, st, p);
-  } else {
-    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, false, false>), dim3(blocks), dim3(NT), 0, st, p);
-  }
+  if (p.xfin.stats)
+    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, NCH, false, true>), dim3(blocks), dim3(NT), 0, st, p);
+  else if (p.pj.v)
+    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, NCH, true, false>), dim3(blocks), dim3(NT), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv3x3_sk_kernel<TH, TW, BN, NCH, false, false>), dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// tile configs: 1 = 8x8 px x 64 ch, 2 = 8x16 x 64, 3 = 16x16 x 32, 4 = 8x16 x 32
+template <int TH, int TW, int BN>
+int launch_sk(const ConvParams& p, hipStream_t st) {
+  switch (p.Cin / BK) {
+    case 2: return launch_sk_n<TH, TW, BN, 2>(p, st);
+    case 4: return launch_sk_n<TH, TW, BN, 4>(p, st);
+    case 8: return launch_sk_n<TH, TW, BN, 8>(p, st);
+  }
+  return 1;
+}
+
+// tile configs: 1 = 8x8 px x 64 ch, 2 = 8x16 x 64, 4 = 8x16 x 32 (a 16x16 x 32 config measured slowest everywhere)
 bool sk_cfg_fits(const ConvParams& p, int cfg) {
   switch (cfg) {
     case 1: return p.Ho % 8 == 0 && p.Wo % 8 == 0 && p.N % 64 == 0;
     case 2: return p.Ho % 8 == 0 && p.Wo % 16 == 0 && p.N % 64 == 0;
-    case 3: return p.Ho % 16 == 0 && p.Wo % 16 == 0 && p.N % 32 == 0;
     case 4: return p.Ho % 8 == 0 && p.Wo % 16 == 0 && p.N % 32 == 0;
   }
   return false;
 }
 
 int sk_blocks(const ConvParams& p, int cfg) {
-  const int th = cfg == 3 ? 16 : 8, tw = cfg == 1 ? 8 : 16, bn = cfg <= 2 ? 64 : 32;
-  return (p.Ho / th) * (p.Wo / tw) * p.B * (p.N / bn);
+  const int tw = cfg == 1 ? 8 : 16, bn = cfg <= 2 ? 64 : 32;
+  return (p.Ho / 8) * (p.Wo / tw) * p.B * (p.N / bn);
 }
 
 // default tile: the largest whole tile that still gives every CU a block (fewer weight re-reads per output)
 int sk_pick(const ConvParams& p) {
   const int forced = cfl_tune(TUNE_CONV3_SK_CFG);
   if (forced > 0) return sk_cfg_fits(p, forced) ? forced : 0;
-  for (int cfg : {2, 3, 4, 1})
+  for (int cfg : {2, 4, 1})
     if (sk_cfg_fits(p, cfg) && sk_blocks(p, cfg) >= 240) return cfg;
   return sk_cfg_fits(p, 1) ? 1 : 0;
 }
 
 }  // namespace
 
-// Eligible shapes: Cin >= 128 (>= 4 chunks: the K split over 4 waves and the 3-stage ring need depth) on maps with at
-// most 32^2 pixels per image (the per-tile / weight-stationary kernels keep the wide high-resolution levels).
-// TUNE_CONV3_SK: 0 = default (eligible shapes), 1 = never, 2 = whenever the shape allows it.
+// Shapes: Cin = 64 / 128 / 256 (2, 4 or 8 chunks, compiled), maps tiled exactly by the config.
+// TUNE_CONV3_SK: 0 = default, 1 = never, 2 = whenever the shape allows it.
 bool conv3x3_sk_eligible(const ConvParams& p) {
   const int v = cfl_tune(TUNE_CONV3_SK);
   if (v == 1) return false;
@@ -434,10 +465,13 @@ bool conv3x3_sk_eligible(const ConvParams& p) {
                  cfl_tune(TUNE_CONV3_WS) == 2))
     return false;
   if (p.ks != 3 || p.stride != 1 || p.pad_t != 1 || p.pad_l != 1 || p.Cin % BK || p.K != 9 * p.Cin) return false;
+  const int nch = p.Cin / BK;
+  if (nch != 2 && nch != 4 && nch != 8) return false;        // compiled chunk counts
+  if (p.Cin > SK_MAX_CIN) return false;                       // coefficient staging
   if (p.bwd.y || sk_pick(p) == 0) return false;
-  if (p.xfin.stats && (p.Cin > SK_MAX_CIN || p.pj.v)) return false;
+  if (p.xfin.stats && p.pj.v) return false;
   if (p.pj.v && (p.Ho % 2 || p.Wo % 2)) return false;
-  return v == 2 || (p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32);
+  return v == 2;                                                // opt-in until it measures faster
 }
 
 int conv3x3_sk(const ConvParams& p, hipStream_t st) {
@@ -445,7 +479,6 @@ int conv3x3_sk(const ConvParams& p, hipStream_t st) {
   switch (sk_pick(p)) {
     case 1: return launch_sk<8, 8, 64>(p, st);
     case 2: return launch_sk<8, 16, 64>(p, st);
-    case 3: return launch_sk<16, 16, 32>(p, st);
     case 4: return launch_sk<8, 16, 32>(p, st);
   }
   return 1;

@@ -288,21 +288,18 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
   __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sG[2][ECH][ELD];
   __shared__ float red[4][32 * 32];
-  __shared__ float sco[BWD ? 5 * 32 + NT : 1];
+  __shared__ __attribute__((aligned(16))) float sco[BWD ? 5 * 32 + NT : 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // this thread's dy channels (tid & 3) * 8 .. +7 (e & 3 below with e = tid + NT * k)
   float ca[8], cm[8], cr[8], k1[8], k2[8];
   if constexpr (BWD) {
     bnb_prologue<NT>(p.bwd, 32, sco, sco + 5 * 32, blockIdx.x == 0);
     const int c0 = (tid & 3) * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ca[j] = sco[c0 + j];
-      cm[j] = sco[32 + c0 + j];
-      cr[j] = sco[64 + c0 + j];
-      k1[j] = sco[96 + c0 + j];
-      k2[j] = sco[128 + c0 + j];
-    }
+    load_f8(sco + c0, ca);              // 16-byte LDS reads (scalar reads at an 8-float stride conflicted)
+    load_f8(sco + 32 + c0, cm);
+    load_f8(sco + 64 + c0, cr);
+    load_f8(sco + 96 + c0, k1);
+    load_f8(sco + 128 + c0, k2);
   }
   const int g = lane >> 4, r16 = lane & 15;
   // A operand (X^T): lane holds tap row 16i + r16 at pixels 32*wid + 8g + 0..7 (column stride 2 pixels = 6 bytes)

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
   __shared__ __attribute__((aligned(16))) bf16_t sW[KS * NB * 32];
   __shared__ __attribute__((aligned(16))) float sBias[NB];
   __shared__ float sred[2][NT / 64][NB];
-  __shared__ float sco[BWD ? 5 * K + NT : 1];            // BN-backward coefficients (bnb_prologue)
+  __shared__ __attribute__((aligned(16))) float sco[BWD ? 5 * K + NT : 1];   // BN-backward coefficients (bnb_prologue)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, q = lane >> 4;

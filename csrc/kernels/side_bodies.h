@@ -109,7 +109,7 @@ CFL_DEVICE void node_pool_body(const NodeBwdParams& p, int bid, int nblocks) {
 constexpr int BBA_IPT = 4;
 
 CFL_DEVICE void bba_body(const BnBwdApplyParams& p, int bid, int nblocks) {
-  __shared__ float co[5 * BNB_MAX_C];
+  __shared__ __attribute__((aligned(16))) float co[5 * BNB_MAX_C];
   __shared__ float part[NT];
   const int G = p.C >> 3, lg = ilog2(G);
   const int total = p.M << lg;
@@ -133,15 +133,14 @@ CFL_DEVICE void bba_body(const BnBwdApplyParams& p, int bid, int nblocks) {
   // the same prologue and element arithmetic as the conv operands that fold this pass (common.h BnBwdIn)
   const BnBwdIn q{p.y, p.ab, p.sums, p.sum_reps, 1.f / (float)p.M, p.dy, p.dgamma, p.dbeta};
   bnb_prologue<NT>(q, p.C, co, part, bid == 0);
-  float a[8], mean[8], rstd[8], k1[8], k2[8];        // this thread's channel group: constant over its items
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    a[j] = co[c0 + j];
-    mean[j] = co[p.C + c0 + j];
-    rstd[j] = co[2 * p.C + c0 + j];
-    k1[j] = co[3 * p.C + c0 + j];
-    k2[j] = co[4 * p.C + c0 + j];
-  }
+  // this thread's channel group: constant over its items. 16-byte reads: 8-float rows at an 8-float stride read as
+  // scalars were 8-way LDS bank conflicts per read (SQ_LDS_BANK_CONFLICT 43 %, profiles/r3_final/pmc_summary.txt)
+  float a[8], mean[8], rstd[8], k1[8], k2[8];
+  load_f8(co + c0, a);
+  load_f8(co + p.C + c0, mean);
+  load_f8(co + 2 * p.C + c0, rstd);
+  load_f8(co + 3 * p.C + c0, k1);
+  load_f8(co + 4 * p.C + c0, k2);
   // BBA_IPT items per thread per iteration, all loads issued before any math (memory-level parallelism: the small
   // layers launch few blocks, so one item in flight per thread would leave HBM latency-bound)
   for (; t0 < total; t0 += BBA_IPT * S) {

@@ -82,7 +82,7 @@ def test_bench_two_ranks_share_one_gpu():
     port = _free_port()
     args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
             "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-            "--gpus", "2", "--steps", "1", "--warmup", "1", "--epochs", "1", "--local-steps", "6", "--val-steps", "2",
+            "--gpus", "2", "--steps", "2", "--warmup", "1", "--epochs", "1", "--local-steps", "6", "--val-steps", "2",
             "--samples", "256", "--dist-backend", "gloo", "--verify-fedavg"]
     p = subprocess.run(args, cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                        timeout=240)

@@ -424,7 +424,9 @@ def test_opt_step_adam_magnitude_matches_keras_adam():
         d_e = (eng.flat.cpu() - f0)[m]
         d_r = (ref.flat - f0)[m]
         err = (d_e - d_r).abs()
-        tol = 1e-3 * d_r.abs() + 1e-7
+        # rtol 1e-3 on the update; the absolute term is 2 fp32 ulps of a weight near 1 (BN gammas start at 1.0, and
+        # w_t - w_0 of such a weight carries the rounding of w_t itself)
+        tol = 1e-3 * d_r.abs() + 2.4e-7
         bad = int((err > tol).sum())
         assert bad == 0, (t, bad, float(err.max()), float(d_r.abs().max()))
         assert float(d_r.abs().max()) > 0.5e-3 * (t + 1)          # the steps are real (~lr per step)
@@ -552,13 +554,15 @@ def test_conv_igemm_big_m_tiles(N):
 
 
 def test_conv_igemm_split_k_with_stats():
-    """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue (the LDS-DMA deep-K kernel, which
-    takes such shapes by default, is switched off here)."""
+    """Deep ConvT layer (M=256, K=2304): split-K partials + reduction epilogue (the split-K-in-block and LDS-DMA
+    deep-K kernels, which take such shapes by default, are switched off here)."""
     hip().set_tune(hip().TUNE_CONV3_DEEP, 1)
+    hip().set_tune(hip().TUNE_CONV3_SK, 1)
     try:
         _split_k_with_stats()
     finally:
         hip().set_tune(hip().TUNE_CONV3_DEEP, 0)
+        hip().set_tune(hip().TUNE_CONV3_SK, 0)
 
 
 def _split_k_with_stats():
@@ -1067,12 +1071,12 @@ def test_conv3x3_deep_dma_forced(B, Hs, Cin, N, up, use_ab):
         C_.set_tune(C_.TUNE_CONV3_WS, 0)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [1, 2, 4])
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [
     (2, 16, 128, 64, 0, True),       # 4 chunks: the 3-stage weight ring wraps
     (2, 8, 256, 128, 1, False),      # upsampled input (8 chunks), ReLU-only producer transform
     (2, 16, 64, 64, 0, True),        # 2 chunks (shorter than the ring)
-    (3, 16, 32, 64, 0, False),       # 1 chunk
+    (1, 32, 128, 128, 0, True),      # a 32^2 map: several pixel tiles per image
 ])
 def test_conv3x3_sk_forced(B, Hs, Cin, N, up, use_ab, cfg):
     """TUNE_CONV3_SK=2 forces the split-K-in-block kernel (conv3x3_sk.hip: 4 waves split each chunk's (tap, k-step)
