@@ -1,9 +1,10 @@
 """Overlap of the FedAvg side stream with the compute stream, from a rocprofv3 kernel trace of
 ``bench.py --fedavg-1rank`` (or any N-rank bench run).
 
-FedAvgAllReduce.average_async issues each bucket's all-reduce (RCCL kernels on RCCL's stream) and then, on the
-aggregation side stream, that bucket's bf16 repack (pack_kernel); the next round's first training step runs eagerly
-and waits per layer (UNetEngine.defer_until). Per FL-round boundary this reports the side-queue busy time
+FedAvgAllReduce.average_async issues each bucket's all-reduce (RCCL kernels on RCCL's stream; bucket 0 = the
+encoder's parameters) and then, on the aggregation side stream, that bucket's bf16 repack (pack_kernel); the next
+round's first training step replays its two split graphs (UNetEngine.train_step): the encoder graph after bucket 0,
+the rest of the step after every bucket. Per FL-round boundary this reports the side-queue busy time
 (RCCL + side-stream pack kernels), how much of it ran while a compute-queue kernel was running (overlap fraction), and
 the compute-queue idle time inside that window.
 
