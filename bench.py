@@ -46,7 +46,6 @@ def main() -> int:
                     help="validation batches per epoch (-1: the whole held-out split, as Keras fit(validation_data))")
     ap.add_argument("--samples", type=int, default=8000, help="synthetic images per client")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--fp8", action="store_true", help="decoder Conv2DTranspose forward in fp8 e4m3 (config 5)")
     ap.add_argument("--profile-steps", type=int, default=0, help="if >0: run this many single steps and exit")
     ap.add_argument("--profile-eval-steps", type=int, default=0,
                     help="if >0: run this many validation (inference) steps at the bench's eval batch and exit")
@@ -125,7 +124,7 @@ def main() -> int:
               flush=True)
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank,
                                  split=min(6213, max(args.batch, int(args.samples * 0.7766))))
-    eng = UNetEngine(table, args.batch, args.img, dev, fp8=args.fp8)
+    eng = UNetEngine(table, args.batch, args.img, dev)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
     agg = None
@@ -285,7 +284,7 @@ def main() -> int:
         out = {"metric": "images/sec/node per FL round", "value": round(value, 2), "unit": "images/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(round_s * 1000.0, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "bf16+fp8-convT-fwd" if args.fp8 else "bf16", "data": "synthetic (device-rendered crack masks, random init)",
+               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-rendered crack masks, random init)",
                "wall_clock_per_round_s": round(round_s, 4),
                "ms_per_iteration": round(round_s * 1000.0 / (args.epochs * args.local_steps), 4),
                "val_images_per_round": world * args.epochs * val_steps * args.batch,
@@ -336,7 +335,7 @@ def run_fl_bench(args, world: int, rank: int, engine_round_s: float) -> dict:
                       steps_per_epoch=args.local_steps, synthetic_samples=args.samples, val_samples=split,
                       max_rounds=rounds, num_clients=world, register_window_s=120.0, codec="flat",
                       data_plane="rccl" if world > 1 else "grpc", client_weight_file="", server_weight_file="",
-                      predict_round=0, use_graph=not args.no_graph, conv_dtype="fp8" if args.fp8 else "bf16",
+                      predict_round=0, use_graph=not args.no_graph,
                       work_dir="/tmp", data_seed=7)
     port = torch.zeros(1, dtype=torch.int64, device="cuda")
     srv = None

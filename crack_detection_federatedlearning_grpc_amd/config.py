@@ -79,7 +79,6 @@ class FLConfig:
     predict_round: int = 5               # client_fit_model.py:235 (cr == 5)
     device: str = "auto"                 # auto | cpu | cuda
     dtype: str = "bf16"                  # activation dtype on the GPU path (fp32 master weights)
-    conv_dtype: str = "bf16"             # bf16 | fp8: decoder Conv2DTranspose forward in fp8 e4m3 MFMA (config 5)
     use_graph: bool = True               # capture the train step in a hipGraph
 
     # --- data ------------------------------------------------------------------------------------
@@ -126,14 +125,6 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # config 3: 8 clients, RCCL weighted all-reduce.
     "gpu8-256": dict(device="cuda", img_size=256, batch_size=16, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, long_poll_s=20.0),
-    # config 5: fp8 (e4m3) Conv2DTranspose forward MFMA path + overlapped RCCL aggregation, 8 clients. MEASURED SLOWER
-    # than bf16 on one MI355X at both sizes it was tried at: 256^2 / batch 16 10,373 vs 11,317 img/s (the ConvTs are
-    # latency-bound there) and 512^2 / HBM-planned batch 1,096 4,680 vs 4,780 img/s (profiles/r3_512/bench.jsonl) - the
-    # per-tensor activation scaling pass and the e4m3 conversions cost more than the halved operand bytes save. Kept
-    # as the config-5 numerics path (tests/test_gpu_kernels.py covers it against fp32), not as a speed-up.
-    "gpu8-fp8": dict(device="cuda", img_size=256, batch_size=16, ready_stall_s=0.0, num_clients=8,
-                     register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, long_poll_s=20.0,
-                     conv_dtype="fp8"),
     # config 4: 512x512 large batch, activation memory sized for 288 GB HBM.
     "gpu8-512": dict(device="cuda", img_size=512, batch_size=0, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5),

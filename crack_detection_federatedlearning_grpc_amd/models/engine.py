@@ -47,12 +47,9 @@ class Lazy:
 class UNetEngine:
     def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
                  lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
-                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, fp8: bool = False,
-                 share: Optional["UNetEngine"] = None):
+                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, share: Optional["UNetEngine"] = None):
         """``share``: an inference-only engine (see ``evaluator``) reading another engine's parameters and packed
         weights in place (no copy, no repack)."""
-        self.fp8 = fp8                     # decoder Conv2DTranspose forward in fp8 e4m3 (conv3x3_fp8.hip)
-        self._fp8_calibrated = False
         if img % 16:
             raise ValueError("image size must be a multiple of 16")
         self.C = hip()
@@ -139,9 +136,6 @@ class UNetEngine:
         t = self._bucket_packs[key]
         if t is not None:
             self.C.pack_weights(self.flat, self.packed, t[0], t[1], t[2])
-        if self.fp8 and sl.stop >= self.table.total:     # last bucket: the fp8 ConvT copies of the new average
-            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
-                            None, self.n_views8)
 
     def G(self, layer: str, w: str) -> torch.Tensor:
         e = self.table.entry(layer, w)
@@ -173,24 +167,6 @@ class UNetEngine:
         self.packed = self._share.packed if self._share is not None else torch.zeros(off, dtype=torch.int16,
                                                                                      device=self.dev)
         self.pack_table = self.C.make_pack_table(views, self.flat)
-        if self.fp8:   # fp8 copies of the forward ConvT weights + per-output-channel scales + delayed amax slots
-            v8, off8, soff, self.p8_at = [], 0, 0, {}
-            for kind, src, _dst, ks, cin, cout in views:
-                if kind != PK_CONVT:
-                    continue
-                layer = next(ly for (ly, kd) in self.packed_at if kd == kind and
-                             self.table.entry(ly, "kernel").offset == src)
-                n = 9 * cin * cout
-                v8.append((kind, src, off8, ks, cin, cout, soff))
-                self.p8_at[layer] = (off8, n, soff, cout, len(v8) - 1)
-                off8 += (n + 15) // 16 * 16
-                soff += cout
-            self.packed8 = torch.zeros(off8, dtype=torch.uint8, device=self.dev)
-            self.scales8 = torch.ones(soff, dtype=torch.float32, device=self.dev)
-            self.amax8 = torch.zeros(len(v8), 2, dtype=torch.float32, device=self.dev)
-            self.amax8[:, 0] = 1.0                            # seed; replaced by the calibration forward
-            self.pack8_table = self.C.make_pack8_table(v8, self.flat)
-            self.n_views8, self.max_rows8 = len(v8), max(v[5] for v in v8)
         self._views = views
         self._view_src = {(v[0], ly): v for ly, v in zip([k[0] for k in self.packed_at], views)}
         self._bucket_packs: Dict[Tuple[int, int], object] = {}
@@ -679,9 +655,6 @@ class UNetEngine:
         cursor = self.batch_cursor if self.batch_table is not None else None
         self.C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
                         self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
-        if self.fp8:
-            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8,
-                            self.max_rows8, self.amax8, self.n_views8)
 
     def bind_batches(self, batches: torch.Tensor) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
@@ -719,51 +692,14 @@ class UNetEngine:
         cursor = self.batch_cursor if step and self.batch_table is not None else None
         self.C.pack_weights(self.flat, self.packed, self.pack_table, self.n_views, self.max_pack,
                             self.step_t if step else None, cursor)
-        if self.fp8:   # after an optimizer step also fold the recorded activation amax (delayed scaling)
-            self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
-                            self.amax8 if step else None, self.n_views8)
 
     def _convt(self, x: "Lazy", layer: str, y: torch.Tensor, N: int, up_in: int, Ho: int,
-               bias: torch.Tensor, stats: Optional[torch.Tensor],
-               **extra) -> None:
-        """Decoder Conv2DTranspose forward: fp8 MFMA kernel when enabled (maps of at least 8x8; smaller ones - only
-        at tiny test resolutions - stay on the bf16 path), else the bf16 halo kernel. ``extra``: consumer-side
-        finalize kwargs of the input's BN (bf16 path only)."""
-        if not self.fp8 or Ho < 8:
-            self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra)
-            return
-        if extra:                              # the fp8 kernel reads a final ab
-            xs = extra
-            self.C.bn_finalize(xs["xfin_stats"], xs["xfin_gamma"], xs["xfin_beta"], xs["xfin_gamma"],
-                               xs["xfin_beta"], x.ab, x.C, xs["xfin_count"], xs["xfin_eps"], 1)
-        B = self.B
-        need = self.C.conv_splits_fp8(B, Ho, Ho, N, x.C)
-        if need > 1 and need * B * Ho * Ho * N > self.ws.numel():
-            if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("split-K workspace must be sized before graph capture")
-            self._retired.append(self.ws)
-            self.ws = torch.empty(need * B * Ho * Ho * N, dtype=torch.float32, device=self.dev)
-        off8, n8, soff, cout, i = self.p8_at[layer]
-        if self._pending:
-            self._await_all()                # the fp8 copies are repacked after the LAST FedAvg bucket
-        self.C.conv3x3_fp8(x.t, self.packed8[off8:off8 + n8], self.scales8[soff:soff + cout], self.amax8[i],
-                           bias, y, stats, x.ab, x.relu, B, x.H, x.H, x.C, up_in, Ho, Ho, N,
-                           self.ws if need > 1 else None)
-
-    def _fp8_calibrate(self) -> None:
-        """Seed the delayed activation scales: one training-mode forward records every fp8 conv input's amax,
-        which the fold then installs (weights, BN state and metrics untouched)."""
-        if not self.fp8 or self._fp8_calibrated:
-            return
-        self._fp8_calibrated = True
-        saved = self.metrics.clone()
-        self._zero_step()
-        self.amax8[:, 0] = 1e30                               # no saturation while measuring
-        self.forward(True)
-        self.C.pack_fp8(self.flat, self.packed8, self.scales8, self.pack8_table, self.n_views8, self.max_rows8,
-                        self.amax8, self.n_views8)
-        self._zero_step()
-        self.metrics.copy_(saved)
+               bias: torch.Tensor, stats: Optional[torch.Tensor], **extra) -> None:
+        """Decoder Conv2DTranspose forward (client_fit_model.py:129,133) on the bf16 3x3 kernels. ``extra``:
+        consumer-side finalize kwargs of the input's BN. (Round 4 removed the fp8 e4m3 forward path: on the
+        non-scaled fp8 MFMA, which issues at the bf16 rate on gfx950, it measured slower at 256^2 and 512^2 -
+        profiles/README.md.)"""
+        self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra)
 
     def _zero_step(self) -> None:
         if self.batch_table is not None:
@@ -773,7 +709,6 @@ class UNetEngine:
             self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
 
     def train_step_eager(self) -> None:
-        self._fp8_calibrate()
         self._zero_step()
         self.forward(True)
         self.backward()
@@ -850,7 +785,6 @@ class UNetEngine:
     def eval_step(self, use_graph: bool = True) -> None:
         """Inference-mode forward (moving BN statistics) of the batch in ``idx``; loss / accuracy accumulate into
         ``eval_metrics``. Replayed from its own hipGraph (captured after an eager warm-up)."""
-        self._fp8_calibrate()
         if self._share is not None:
             self._share._await_all()                   # the parameters are the parent's (FedAvg buckets in flight)
         if not use_graph:
@@ -905,13 +839,12 @@ class UNetEngine:
         """An inference-only engine of batch ``batch`` over THIS engine's parameters, packed weights and dataset.
         Validation loss / accuracy are per-pixel means over the whole held-out split (head.hip sums, normalised by
         the pixel count), so evaluating the same images in larger batches gives the same numbers - and larger
-        batches fill the GPU (the 16-image eval forward is launch/latency-bound). Not used for the fp8 path (its
-        activation scales are calibrated per engine) or with the per-batch Dice term.
+        batches fill the GPU (the 16-image eval forward is launch/latency-bound). Not used with the per-batch Dice term.
 
         ``snapshot``: the evaluator reads its OWN copy of the fp32 parameters and packed weights (``ParamSnapshot``,
         refreshed from this engine by ``snap.refresh()``), so a validation pass can run on another stream while the
         next epoch trains (``overlapped_validation``)."""
-        if (batch == self.B and not snapshot) or self.fp8 or self.dice:
+        if (batch == self.B and not snapshot) or self.dice:
             return self
         key = (batch, snapshot)
         ev = self._evaluators.get(key)
@@ -993,7 +926,7 @@ class HipBackend:
         self.cfg = cfg
         self.table = table
         self.eng = UNetEngine(table, cfg.batch_size, data.img_size, "cuda", cfg.loss, cfg.lr, cfg.beta1, cfg.beta2,
-                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps, fp8=getattr(cfg, "conv_dtype", "") == "fp8")
+                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps)
         images = data.images if isinstance(data.images, torch.Tensor) else torch.as_tensor(data.images)
         masks = data.masks if isinstance(data.masks, torch.Tensor) else torch.as_tensor(data.masks)
         self.eng.bind_data(images.to(self.eng.dev), masks.to(self.eng.dev))

@@ -221,14 +221,6 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
-int conv_splits_fp8_op(int B, int Ho, int Wo, int N, int Cin) {
-  ConvParams p{};
-  p.B = B; p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = 3; p.stride = 1; p.pad_t = 1; p.pad_l = 1; p.Cin = Cin;
-  p.M = B * Ho * Wo;
-  p.K = 9 * Cin;
-  return conv3x3_split_k(p);
-}
-
 int conv_splits_op(int B, int Ho, int Wo, int N, int ks, int stride, int pad, int Cin) {
   ConvParams p{};
   p.B = B; p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = ks; p.stride = stride; p.pad_t = pad; p.pad_l = pad; p.Cin = Cin;
@@ -777,31 +769,6 @@ void zero_spans_op(at::Tensor table, int n, int64_t max_bytes, OptT batches, Opt
   ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream(), bs), "zero_spans");
 }
 
-// views: list of (kind, src, dst_bytes, ks, cin, cout, dst_scale) -> device table (fp8 pack)
-at::Tensor make_pack8_table(std::vector<std::tuple<int, int64_t, int64_t, int, int, int, int64_t>> views,
-                            at::Tensor like) {
-  std::vector<PackView> h;
-  for (auto& v : views) {
-    PackView p{};
-    p.kind = std::get<0>(v); p.src = std::get<1>(v); p.dst = std::get<2>(v);
-    p.ks = std::get<3>(v); p.cin = std::get<4>(v); p.cout = std::get<5>(v); p.dst_scale = std::get<6>(v);
-    TORCH_CHECK(p.kind == PK_CONVT && p.ks == 3 && (9 * p.cin) % 4 == 0, "fp8 pack: PK_CONVT 3x3 views only");
-    h.push_back(p);
-  }
-  auto cpu = torch::empty({(int64_t)(h.size() * sizeof(PackView))}, torch::kUInt8);
-  std::memcpy(cpu.data_ptr(), h.data(), h.size() * sizeof(PackView));
-  return cpu.to(like.device());
-}
-
-void pack_fp8_op(at::Tensor flat, at::Tensor packed8, at::Tensor scales, at::Tensor table, int n_views, int max_rows,
-                 OptT amax, int n_amax) {
-  TORCH_CHECK(table.numel() == (int64_t)n_views * (int64_t)sizeof(PackView), "pack_fp8: table size");
-  TORCH_CHECK(packed8.scalar_type() == at::kByte, "pack_fp8: packed8 must be uint8");
-  ok(pack_fp8(ptr<const float>(flat, "flat"), ptr<uint8_t>(packed8, "packed8"), ptr<float>(scales, "scales"),
-              ptr<const PackView>(table, "table"), n_views, max_rows, stream(), optr<float>(amax, "amax"), n_amax),
-     "pack_fp8");
-}
-
 // src: uint8 device bytes of n decoded images back to back; offs: int64 [n] byte offsets; dims: int32 [n, 2] (h, w);
 // dst: uint8 [n, dh, dw, c] or [n, dh, dw] (c = 1)
 void resize_batch_op(at::Tensor src, at::Tensor offs, at::Tensor dims, at::Tensor dst, int binarize) {
@@ -812,34 +779,6 @@ void resize_batch_op(at::Tensor src, at::Tensor offs, at::Tensor dims, at::Tenso
   const int dh = (int)dst.size(1), dw = (int)dst.size(2), c = dst.dim() == 4 ? (int)dst.size(3) : 1;
   ok(resize_batch(ptr<const uint8_t>(src, "src"), ptr<const int64_t>(offs, "offs"), ptr<const int>(dims, "dims"),
                   ptr<uint8_t>(dst, "dst"), n, dh, dw, c, binarize, stream()), "resize_batch");
-}
-
-void conv3x3_fp8_op(at::Tensor x, at::Tensor wt8, at::Tensor wscale, at::Tensor amax, OptT bias, at::Tensor y,
-                    OptT stats, OptT ab, int relu, int B, int Hin, int Win, int Cin, int up_in, int Ho, int Wo, int N,
-                    OptT ws) {
-  Conv8Params q{};
-  ConvParams& p = q.c;
-  p.x = ptr<const bf16_t>(x, "x");
-  p.bias = optr<const float>(bias, "bias");
-  p.y = ptr<bf16_t>(y, "y");
-  p.stats = optr<float>(stats, "stats");
-  p.xf = xf(ab, Cin, relu);
-  p.B = B; p.Hin = Hin; p.Win = Win; p.Cin = Cin; p.up_in = up_in;
-  p.Ho = Ho; p.Wo = Wo; p.N = N; p.ks = 3; p.stride = 1; p.pad_t = 1; p.pad_l = 1;
-  p.M = B * Ho * Wo;
-  p.K = 9 * Cin;
-  p.ws = optr<float>(ws, "ws");
-  p.ws_elems = p.ws ? ws->numel() : 0;
-  q.wt8 = ptr<const uint8_t>(wt8, "wt8");
-  q.wscale = ptr<const float>(wscale, "wscale");
-  q.amax = ptr<float>(amax, "amax");
-  TORCH_CHECK(x.numel() == (int64_t)B * Hin * Win * Cin, "conv3x3_fp8: x size");
-  TORCH_CHECK(wt8.numel() >= (int64_t)N * p.K && wscale.numel() >= N && amax.numel() >= 2, "conv3x3_fp8: w sizes");
-  TORCH_CHECK(y.numel() == (int64_t)p.M * N, "conv3x3_fp8: y size");
-  TORCH_CHECK(!p.stats || stats->numel() >= (int64_t)STAT_REPLICAS * 2 * N, "conv3x3_fp8: stats size");
-  const int rc = conv3x3_fp8(q, stream());
-  TORCH_CHECK(rc <= 0, "conv3x3_fp8 failed (code ", rc, ")");
-  if (rc < 0) ok(splitk_epilogue(p, -rc, stream()), "conv3x3_fp8 split-K epilogue");
 }
 
 void render_cracks_op(at::Tensor segs, at::Tensor params, at::Tensor images, at::Tensor masks, int n, int img,
@@ -884,7 +823,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;
   m.def("conv_splits", &conv_splits_op);
-  m.def("conv_splits_fp8", &conv_splits_fp8_op);
   m.def("conv_wgrad", &conv_wgrad_op, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("ab"), py::arg("relu"),
         py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"),
         py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("dst_mode"),
@@ -993,13 +931,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_update", &adam_update_op);
   m.def("adam_step_done", &adam_step_done_op);
   m.def("make_pack_table", &make_pack_table);
-  m.def("make_pack8_table", &make_pack8_table);
-  m.def("pack_fp8", &pack_fp8_op, py::arg("flat"), py::arg("packed8"), py::arg("scales"), py::arg("table"),
-        py::arg("n_views"), py::arg("max_rows"), py::arg("amax") = py::none(), py::arg("n_amax") = 0);
-  m.def("conv3x3_fp8", &conv3x3_fp8_op, py::arg("x"), py::arg("wt8"), py::arg("wscale"), py::arg("amax"),
-        py::arg("bias"), py::arg("y"), py::arg("stats"), py::arg("ab"), py::arg("relu"), py::arg("B"), py::arg("Hin"),
-        py::arg("Win"), py::arg("Cin"), py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"),
-        py::arg("ws") = py::none());
   m.def("pack_weights", &pack_weights_op, py::arg("flat"), py::arg("packed"), py::arg("table"), py::arg("n_views"),
         py::arg("max_elems"), py::arg("step") = py::none(), py::arg("cursor") = py::none());
   m.def("make_opt_table", &make_opt_table);

@@ -274,16 +274,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
     const bf16_t* sw = wring + (ch % WSTAGES) * S::WST;
     const bf16_t* sh = hring + (ch % HSTAGES) * S::HST;
     // this wave's units u = wid + 4 j of the chunk's 18 (tap, 16-channel k-step) units; waves 2 and 3 run a
-    // 5th unit against a zero weight fragment (no branch: the chunk step takes the 5-unit waves' time anyway)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    // 5th unit against a zero weight fragment (no branch: the chunk step takes the 5-unit waves' time anyway).
+    // Fragments are double-buffered in registers: unit j + 1's LDS reads are issued before unit j's MFMAs, so each
+    // read has FM * FN MFMAs (>= 128 cycles) of cover instead of waiting in front of its own MFMAs.
+    auto frag = [&](int j, s8v (&af)[FM], s8v (&bfg)[FN]) {
       const int u0 = wid + 4 * j;
       const bool live = j < 4 || u0 < 18;
       const int u = live ? u0 : 17;
       const int tap = u >> 1, s = u & 1;
       const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;     // tap / 3 for tap < 9
       const int q = 2 * s + kh;
-      s8v af[FM], bfg[FN];
 #pragma unroll
       for (int mf = 0; mf < FM; ++mf) af[mf] = *reinterpret_cast<const s8v*>(sh + sk_off(fa[mf] + ky * HWL + kx, q));
 #pragma unroll
@@ -291,12 +291,33 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
         const s8v w = *reinterpret_cast<const s8v*>(sw + sk_off(tap * BN + nf * 32 + (lane & 31), q));
         bfg[nf] = live ? w : s8v{0, 0, 0, 0, 0, 0, 0, 0};
       }
+    };
+    auto mma = [&](const s8v (&af)[FM], const s8v (&bfg)[FN]) {
 #pragma unroll
       for (int mf = 0; mf < FM; ++mf)
 #pragma unroll
         for (int nf = 0; nf < FN; ++nf)
           acc[mf][nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mf], bfg[nf], acc[mf][nf], 0, 0, 0);
-    }
+    };
+    s8v a0[FM], b0[FN], a1[FM], b1[FN];
+    frag(0, a0, b0);
+    frag(1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    frag(2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    frag(3, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    frag(4, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
     if (ch + 1 < NCH) {                                       // halo of chunk ch + 1 -> the other halo stage
       __builtin_amdgcn_sched_barrier(0);                      // (the wait stays behind this chunk's MFMAs)
       if (ch + 2 < NCH) { if (wfull) sk_wait_vm<W_PER>(); else sk_wait_vm<W_PER - 1>(); }
@@ -456,7 +477,7 @@ int sk_pick(const ConvParams& p) {
 }  // namespace
 
 // Shapes: Cin = 64 / 128 / 256 (2, 4 or 8 chunks, compiled), maps tiled exactly by the config.
-// TUNE_CONV3_SK: 0 = default, 1 = never, 2 = whenever the shape allows it.
+// TUNE_CONV3_SK: 0 = default, 1 = never, 2 = whenever the shape allows it, 3 = the low-resolution levels only.
 bool conv3x3_sk_eligible(const ConvParams& p) {
   const int v = cfl_tune(TUNE_CONV3_SK);
   if (v == 1) return false;
@@ -471,7 +492,8 @@ bool conv3x3_sk_eligible(const ConvParams& p) {
   if (p.bwd.y || sk_pick(p) == 0) return false;
   if (p.xfin.stats && p.pj.v) return false;
   if (p.pj.v && (p.Ho % 2 || p.Wo % 2)) return false;
-  return v == 2;                                                // opt-in until it measures faster
+  // default off until it measures faster; 3 = the low-resolution candidate (maps <= 32^2, Cin >= 128) for A/B runs
+  return v == 2 || (v == 3 && p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32);
 }
 
 int conv3x3_sk(const ConvParams& p, hipStream_t st) {

@@ -165,19 +165,9 @@ bool pw_conv_supported(const ConvParams& p);
 int pw_conv(const ConvParams& p, hipStream_t st);
 int conv_igemm_splits(const ConvParams& p);   // K splits the launcher would use (workspace = splits*M*N floats)
 int conv3x3_splits(const ConvParams& p);
-int conv3x3_split_k(const ConvParams& p);     // K splits of the standard tiles (fp8 path)
+int conv3x3_split_k(const ConvParams& p);     // K splits of the standard 8x16 / 16x8 tiles
 int splitk_epilogue(const ConvParams& p, int splits, hipStream_t st);   // sum partials + bias/stats/node epilogue
 
-// fp8 (e4m3) forward 3x3 conv (conv3x3_fp8.hip): c.wt unused; per-output-channel weight scales, delayed
-// per-tensor activation scaling through amax[2] (scale from amax[0], this call's amax max-ed into amax[1])
-struct Conv8Params {
-  ConvParams c;
-  const uint8_t* wt8;      // [N][K] fp8 weights (pack_fp8)
-  const float* wscale;     // [N]
-  float* amax;             // [2]
-};
-int conv3x3_fp8(const Conv8Params& p, hipStream_t st);
-bool conv3x3_fp8_supported(const ConvParams& c);
 
 
 // ---------------------------------------------------------------- weight gradient (conv_wgrad.hip)
@@ -362,14 +352,10 @@ enum PackKind { PK_CONV = 0, PK_CONV_DGRAD1x1 = 1, PK_CONVT = 2, PK_CONVT_DGRAD 
 struct PackView {
   int kind;
   int64_t src;             // offset in the flat fp32 buffer
-  int64_t dst;             // offset in the bf16 pack buffer (fp8 pack: byte offset)
+  int64_t dst;             // offset in the bf16 pack buffer
   int ks, cin, cout;       // layer geometry (Keras meaning)
-  int64_t dst_scale;       // fp8 pack: offset of the per-output-channel scales
+  int64_t dst_scale;       // (unused; kept for the table's layout)
 };
-// fp8 weight pack of PK_CONVT views (dst = byte offset into packed8, dst_scale = offset into scales); if amax is
-// given, also folds every conv's recorded amax[i][1] into its scale slot amax[i][0] (delayed scaling)
-int pack_fp8(const float* flat, uint8_t* packed8, float* scales, const PackView* d_views, int n_views, int max_rows,
-             hipStream_t st, float* amax = nullptr, int n_amax = 0);
 // step != nullptr: also increments the Adam step counter (adam_step_done folded into this launch)
 int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int n_views, int max_elems,
                  hipStream_t st, int* step = nullptr, int* cursor = nullptr);   // cursor: BatchSelect's, += 1
@@ -486,8 +472,8 @@ enum TuneKey {
   TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 4M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
   TUNE_PW_NB = 39,             // streaming 1x1 kernel, N % 128 == 0 and K >= 128: 0 = 128-channel output slices at
                                // M >= 1M pixels (else 64), 64 = always 64, 128 = always 128
-  TUNE_CONV3_SK = 40,          // conv3x3 low-resolution deep-K layers: 0 = split-K-in-block 32x32 MFMA kernel
-                               //   (conv3x3_sk.hip) where eligible, 1 = off, 2 = force wherever the shape allows
+  TUNE_CONV3_SK = 40,          // split-K-in-block 32x32 MFMA 3x3 kernel (conv3x3_sk.hip): 0 = default, 1 = off,
+                               //   2 = force wherever the shape allows, 3 = the low-resolution levels (<= 32^2, Cin >= 128)
   TUNE_CONV3_SK_CFG = 41,      // ... tile config: 0 = heuristic, 1 = 8x8 px x 64 ch, 2 = 8x16 x 64, 3 = 16x16 x 32,
                                //   4 = 8x16 x 32
   TUNE_N = 42

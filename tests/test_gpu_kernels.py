@@ -849,60 +849,6 @@ def test_rccl_rollback_waits_for_queued_side_stream_work():
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("Hs,Cin,N,up,B", [(16, 64, 64, 0, 2), (8, 64, 32, 1, 2), (8, 256, 64, 0, 4)])
-def test_conv3x3_fp8_matches_bf16(Hs, Cin, N, up, B):
-    """fp8 e4m3 ConvT forward (per-channel weight scales, delayed per-tensor activation scale) vs the bf16 kernel;
-    the last case exercises split-K."""
-    torch.manual_seed(31)
-    C_ = hip()
-    Ho = Hs * (2 if up else 1)
-    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
-    wk = torch.randn(3, 3, N, Cin) * 0.05                       # Keras Conv2DTranspose layout (kh, kw, out, in)
-    ab, a, b = ab_for(Cin, 21)
-    flat = wk.reshape(-1).to(DEV)
-    table8 = C_.make_pack8_table([(PK_CONVT, 0, 0, 3, Cin, N, 0)], flat)
-    w8 = torch.zeros(9 * Cin * N, dtype=torch.uint8, device=DEV)
-    sc = torch.zeros(N, device=DEV)
-    C_.pack_fp8(flat, w8, sc, table8, 1, N)
-    t = (xf * a + b).relu()
-    amax = torch.tensor([float(t.abs().max()), 0.0], device=DEV)
-    bias = (torch.randn(N) * 0.1).to(DEV)
-    ws = torch.zeros(16 * B * Ho * Ho * N, device=DEV)
-    y8 = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
-    s8 = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
-    C_.conv3x3_fp8(xb, w8, sc, amax, bias, y8, s8, ab.to(DEV), 1, B, Hs, Hs, Cin, up, Ho, Ho, N, ws)
-    yb = torch.zeros_like(y8)
-    sb = torch.zeros_like(s8)
-    wb = pack(PK_CONVT, wk, 3, Cin, N)
-    C_.conv_igemm(xb, wb, bias, yb, sb, ab.to(DEV), 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, ws)
-    assert rel(from_bits(y8), from_bits(yb)) < 0.06
-    assert abs(float(amax[1]) - float(t.abs().max())) <= 1e-2 * float(t.abs().max())   # recorded for next step
-    st8, stb = s8.view(-1, 2, N).sum(0).cpu(), sb.view(-1, 2, N).sum(0).cpu()
-    assert rel(st8, stb) < 0.06
-
-
-def test_engine_fp8_trains_close_to_bf16():
-    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
-    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
-    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
-    table = ParamTable()
-    data = make_synthetic_device(16, 64, seed=3)
-    losses = {}
-    for fp8 in (False, True):
-        eng = UNetEngine(table, 4, 64, fp8=fp8)
-        eng.bind_data(data.images, data.masks)
-        eng.set_flat(table.init_flat(3))
-        ls = []
-        for i in range(30):
-            eng.idx.copy_(torch.arange(4 * (i % 4), 4 * (i % 4) + 4, dtype=torch.int32, device=eng.dev))
-            eng.train_step(use_graph=True)
-            if i % 10 == 9:
-                ls.append(eng.read_metrics("train")["loss"])
-        losses[fp8] = ls
-        assert ls[-1] < ls[0] and all(np.isfinite(ls))
-    assert abs(losses[True][0] - losses[False][0]) < 0.1 * losses[False][0]
-
-
 def test_ops_autograd_layers_match_torch():
     """ops/: Conv2D 3x3 / 1x1, Conv2DTranspose 3x3 and depthwise 3x3 as autograd functions vs fp32 torch."""
     from crack_detection_federatedlearning_grpc_amd import ops

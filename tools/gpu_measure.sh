@@ -1,5 +1,5 @@
 #!/bin/bash
-# Full measurement pass at HEAD -> gpurun_out/$OUT: bench (bf16 x2, fp8 x2), steady-state kernel trace (bf16, fp8),
+# Full measurement pass at HEAD -> gpurun_out/$OUT: bench (bf16 x2), steady-state kernel trace,
 # PMC counter passes, per-call roofline (kbench). Copy the summaries you keep into profiles/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -7,8 +7,8 @@ OUT=${OUT:-measure}
 O=$R/gpurun_out/$OUT
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p $O
-for v in bf16 fp8; do
-  A=""; [ $v = fp8 ] && A="--fp8"
+for v in bf16; do
+  A=""
   for i in 1 2; do
     timeout -k 10 300 python bench.py --steps 2 --warmup 1 $A > $O/bench_${v}_$i.log 2>&1 || { tail -20 $O/bench_${v}_$i.log; exit 1; }
     grep '^{' $O/bench_${v}_$i.log >> $O/bench.jsonl
@@ -16,8 +16,8 @@ for v in bf16 fp8; do
   done
 done
 cd /tmp
-for v in bf16 fp8; do
-  A=""; [ $v = fp8 ] && A="--fp8"
+for v in bf16; do
+  A=""
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run --output-format csv -- \
       python $R/bench.py --profile-steps 21 $A > $O/prof_$v.log 2>&1 || { tail -5 $O/prof_$v.log; exit 1; }
   python $R/tools/prof_summary.py $O/prof_$v 40 > $O/summary_$v.txt || exit 1

@@ -172,10 +172,10 @@ def min_bytes(eng, name, a, k):
 
 def conv_flops(name, a):
     """2*M*N*K of the conv_igemm / conv_wgrad calls (positional ints: B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, ...)."""
-    if name not in ("conv_igemm", "conv_wgrad", "conv3x3_fp8"):
+    if name not in ("conv_igemm", "conv_wgrad"):
         return 0.0
     ints = [x for x in a if isinstance(x, int) and not isinstance(x, bool)]
-    i0 = 1 if name == "conv_igemm" or name == "conv3x3_fp8" else 1    # relu flag precedes B
+    i0 = 1    # relu flag precedes B
     try:
         B, Hin, Win, Cin, up, Ho, Wo, N, ks = ints[i0:i0 + 9]
     except ValueError:
