@@ -492,8 +492,10 @@ bool conv3x3_sk_eligible(const ConvParams& p) {
   if (p.bwd.y || sk_pick(p) == 0) return false;
   if (p.xfin.stats && p.pj.v) return false;
   if (p.pj.v && (p.Ho % 2 || p.Wo % 2)) return false;
-  // default off until it measures faster; 3 = the low-resolution candidate (maps <= 32^2, Cin >= 128) for A/B runs
-  return v == 2 || (v == 3 && p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32);
+  // default off until it measures faster; 3 = the low-resolution candidate (maps <= 32^2, Cin >= 128) for A/B runs;
+  // 4 = only the shapes the isolated probe measured faster (16^2 maps; 32^2 maps with N <= 128)
+  const bool low = p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32;
+  return v == 2 || (v == 3 && low) || (v == 4 && low && (p.Ho * p.Wo <= 16 * 16 || p.N <= 128));
 }
 
 int conv3x3_sk(const ConvParams& p, hipStream_t st) {
