@@ -492,9 +492,12 @@ bool conv3x3_sk_eligible(const ConvParams& p) {
   if (p.bwd.y || sk_pick(p) == 0) return false;
   if (p.xfin.stats && p.pj.v) return false;
   if (p.pj.v && (p.Ho % 2 || p.Wo % 2)) return false;
-  // default off until it measures faster; 3 = the low-resolution candidate (maps <= 32^2, Cin >= 128) for A/B runs;
-  // 4 = only the shapes the isolated probe measured faster (16^2 maps; 32^2 maps with N <= 128)
+  // default: the 8-chunk (Cin = 256) convs of the <= 32^2 levels without the decoder node join. In-step per-position
+  // trace A/B (tools/gpu_trace_ab.sh, 256^2 / b16): those five calls 1.5-1.9 / 0.3-0.4 us faster each; the Cin = 128
+  // calls -0.1 .. +2.4 us and the node-join form +9.7 us (its join loads wait in front of the K loop), so not those.
+  // 3 = every low-resolution candidate (maps <= 32^2, Cin >= 128), 4 = 16^2 maps and 32^2 maps with N <= 128 (A/B).
   const bool low = p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32;
+  if (v == 0) return p.Cin == 256 && p.Ho * p.Wo <= 32 * 32 && !p.pj.v;
   return v == 2 || (v == 3 && low) || (v == 4 && low && (p.Ho * p.Wo <= 16 * 16 || p.N <= 128));
 }
 

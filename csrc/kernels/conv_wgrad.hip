@@ -11,6 +11,8 @@
 // pixels, register-staged double buffer. The M range is split over gridDim.z so the grid holds ~512 long-running
 // blocks; partial tiles are combined with fp32 atomics into the layer's slot of the flat gradient buffer (or into
 // WGRAD_REPLICAS replica rows summed by grad_finish), writing Keras layouts (HWIO for Conv2D / pointwise; (kh,kw,out,in) with the spatial flip for Conv2DTranspose).
+#include <cstdio>
+
 #include "common.h"
 #include "launch.h"
 #include "wgrad3_body.h"
@@ -410,11 +412,17 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
     blocks = 0;
     return hipGetLastError() == hipSuccess ? 0 : 3;
   };
+  const int only = cfl_tune(TUNE_WGRAD_MIX_ONLY), skip = cfl_tune(TUNE_WGRAD_MIX_SKIP);
+  static bool listed = false;
+  const bool list = cfl_tune(TUNE_WGRAD_MIX_LIST) == 1 && !listed;
+  int idx = -1;
   for (int pass = 0; pass < 2; ++pass)
     for (int i = 0; i < n; ++i) {
       const WgradParams& p = ps[i];
       const bool halo = p.algo != 1 && conv3x3_wgrad_supported(p);
       if (halo != (pass == 0)) continue;
+      ++idx;
+      if ((only > 0 && idx != only - 1) || (idx < 31 && ((skip >> idx) & 1))) continue;   // timing experiments
       if (g.n == MIX_MAX) {
         const int rc = flush();
         if (rc) return rc;
@@ -440,7 +448,11 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
       }
       it.block0 = blocks;
       blocks += it.gx * it.gy * zs;
+      if (list)
+        fprintf(stderr, "[wgrad_mix] item %2d kind %2d B%d %dx%d Cin %d up %d -> %dx%d N %d ks %d s %d: %d blocks\n", idx,
+                it.kind, p.B, p.Hin, p.Win, p.Cin, p.up_in, p.Ho, p.Wo, p.N, p.ks, p.stride, it.gx * it.gy * zs);
     }
+  if (list) listed = true;
   return flush();
 }
 

@@ -472,11 +472,14 @@ enum TuneKey {
   TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 4M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
   TUNE_PW_NB = 39,             // streaming 1x1 kernel, N % 128 == 0 and K >= 128: 0 = 128-channel output slices at
                                // M >= 1M pixels (else 64), 64 = always 64, 128 = always 128
-  TUNE_CONV3_SK = 40,          // split-K-in-block 32x32 MFMA 3x3 kernel (conv3x3_sk.hip): 0 = default, 1 = off,
+  TUNE_CONV3_SK = 40,          // split-K-in-block 32x32 MFMA 3x3 kernel (conv3x3_sk.hip): 0 = default (Cin 256 at <= 32^2), 1 = off,
                                //   2 = force wherever the shape allows, 3 = the low-resolution levels (<= 32^2, Cin >= 128)
   TUNE_CONV3_SK_CFG = 41,      // ... tile config: 0 = heuristic, 1 = 8x8 px x 64 ch, 2 = 8x16 x 64, 3 = 16x16 x 32,
                                //   4 = 8x16 x 32
-  TUNE_N = 42
+  TUNE_WGRAD_MIX_ONLY = 42,    // TIMING ONLY (wrong gradients): mixed wgrad launch keeps only item k - 1 (mix order)
+  TUNE_WGRAD_MIX_SKIP = 43,    // TIMING ONLY: mixed wgrad launch drops the items of this bit mask (bit k = item k)
+  TUNE_WGRAD_MIX_LIST = 44,    // 1: print the mixed launch's items (index, kind, shape, blocks) to stderr once
+  TUNE_N = 45
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

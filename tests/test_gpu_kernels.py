@@ -981,6 +981,8 @@ def test_conv3x3_big_tiles_forced(B, Hs, Cin, N, up, use_ab):
     (2, 8, 32, 64, 1, False, 0),     # upsampled input, CH 1, two column blocks
     (3, 16, 32, 128, 0, True, 6),    # 4 column blocks, grid 6 -> 4: several tiles per block
     (2, 8, 64, 32, 1, True, 2),      # upsampled, CH 2: a 2-block grid walks all 4 tiles
+    (3, 16, 32, 32, 0, True, 2),     # 2 blocks walk 3 tiles each: odd tail of the two-tile loop
+    (2, 16, 32, 32, 0, True, 3),     # 3 blocks over 4 tiles: blocks with 1 and 2 tiles
 ])
 def test_conv3x3_weight_stationary_forced(B, Hs, Cin, N, up, use_ab, grid):
     """TUNE_CONV3_WS=2 forces the weight-stationary persistent kernel (every K of a 32-column block resident in
@@ -1039,14 +1041,16 @@ def test_conv3x3_sk_forced(B, Hs, Cin, N, up, use_ab, cfg):
         C_.set_tune(C_.TUNE_CONV3_SK_CFG, 0)
 
 
-@pytest.mark.parametrize("deep", [False, True])
-def test_conv3x3_weight_stationary_node_epilogue(deep):
+@pytest.mark.parametrize("deep,grid", [(False, 0), (True, 0), (False, 3)])
+def test_conv3x3_weight_stationary_node_epilogue(deep, grid):
     if deep:
         hip().set_tune(hip().TUNE_CONV3_DEEP, 2)
+    hip().set_tune(hip().TUNE_CONV3_WS_GRID, grid)
     try:
         _node_epilogue_ws_vs_tile()
     finally:
         hip().set_tune(hip().TUNE_CONV3_DEEP, 0)
+        hip().set_tune(hip().TUNE_CONV3_WS_GRID, 0)
 
 
 def _node_epilogue_ws_vs_tile():

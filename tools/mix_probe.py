@@ -1,0 +1,74 @@
+"""Time the mixed weight-gradient launch (conv_wgrad.hip wgrad_mix_kernel) of the bench step and each of its items:
+the deferred wgrad list of one eager training step (256^2, batch 16) is captured and replayed between HIP events
+as a whole, with only item k (TUNE_WGRAD_MIX_ONLY) and without item k (TUNE_WGRAD_MIX_SKIP). Timing only: the
+restricted launches leave the other items' slabs stale.
+
+    python tools/mix_probe.py [img] [batch]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device  # noqa: E402
+from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine  # noqa: E402
+from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+dev = torch.device("cuda")
+table = ParamTable()
+data = make_synthetic_device(64, S, seed=0)
+eng = UNetEngine(table, B, S, dev)
+eng.bind_data(data.images, data.masks)
+eng.set_flat(table.init_flat(0))
+eng.idx.copy_(torch.arange(B, dtype=torch.int32, device=dev))
+C = eng.C
+eng.train_step(use_graph=False)                     # allocates the slabs
+captured = []
+real = C.conv_wgrad_batch
+
+
+class Shim:
+    def __getattr__(self, k):
+        return getattr(C, k)
+
+    def conv_wgrad_batch(self, wq):
+        captured.append(list(wq))
+        real(wq)
+
+
+eng.C = Shim()
+eng.train_step(use_graph=False)
+eng.C = C
+torch.cuda.synchronize()
+wq = captured[-1]
+
+
+def timeit(reps=30):
+    for _ in range(3):
+        real(wq)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        real(wq)
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+C.set_tune(C.TUNE_WGRAD_MIX_LIST, 1)
+full = timeit()
+C.set_tune(C.TUNE_WGRAD_MIX_LIST, 0)
+print(f"whole mixed launch: {full:.1f} us ({len(wq)} deferred wgrads)", flush=True)
+n = len(wq)
+for k in range(n):
+    C.set_tune(C.TUNE_WGRAD_MIX_ONLY, k + 1)
+    alone = timeit()
+    C.set_tune(C.TUNE_WGRAD_MIX_ONLY, 0)
+    C.set_tune(C.TUNE_WGRAD_MIX_SKIP, 1 << k)
+    without = timeit()
+    C.set_tune(C.TUNE_WGRAD_MIX_SKIP, 0)
+    print(f"item {k:2d}: alone {alone:6.1f} us   mix without it {without:6.1f} us ({without - full:+.1f})", flush=True)
