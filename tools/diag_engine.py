@@ -25,7 +25,7 @@ def rel(a, b):
 
 def main(S=64, B=2):
     table = ParamTable()
-    data = make_synthetic_device(8, S, seed=0)
+    data = make_synthetic_device(max(8, B), S, seed=0)   # idx 0..B-1 must be bound images
     eng = UNetEngine(table, B, S)
     eng.bind_data(data.images, data.masks)
     flat = table.init_flat(0)

@@ -18,7 +18,7 @@ from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  #
 
 def one(S, B, seed):
     table = ParamTable()
-    data = make_synthetic_device(8, S, seed=seed)
+    data = make_synthetic_device(max(8, B), S, seed=seed)   # idx 0..B-1 must be bound images
     eng = UNetEngine(table, B, S)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(seed))

@@ -19,10 +19,11 @@ S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 dev = torch.device("cuda")
 table = ParamTable()
-data = make_synthetic_device(64, S, seed=0)
+data = make_synthetic_device(max(64, B), S, seed=0)   # every index of the probe batch must be a bound image
 eng = UNetEngine(table, B, S, dev)
 eng.bind_data(data.images, data.masks)
 eng.set_flat(table.init_flat(0))
+assert data.images.shape[0] >= B, "the batch indexes images 0..B-1"
 eng.idx.copy_(torch.arange(B, dtype=torch.int32, device=dev))
 C = eng.C
 eng.train_step(use_graph=False)                     # allocates the slabs
