@@ -708,6 +708,16 @@ class UNetEngine:
         else:
             self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
 
+    def _check_idx(self) -> None:
+        """Host-side range check of a directly written ``idx`` (eager steps / before capture; bound batch tables are
+        checked in bind_batches): the kernels gather images and masks through it, so an index past the bound
+        dataset is an out-of-range device read (a GPU memory fault), not an error."""
+        if self.images is None or self.batch_table is not None:
+            return
+        lo, hi = int(self.idx.min()), int(self.idx.max())
+        if lo < 0 or hi >= self.n_data:
+            raise ValueError(f"idx holds [{lo}, {hi}] but the bound dataset has {self.n_data} images")
+
     def train_step_eager(self) -> None:
         self._zero_step()
         self.forward(True)
@@ -771,8 +781,10 @@ class UNetEngine:
         only for the buckets holding the encoder's parameters and their repack, the rest of the step for every
         bucket - so the later buckets' all-reduce runs under the encoder forward."""
         if use_graph and self.graph is None:
+            self._check_idx()
             self.capture()
         if not use_graph:
+            self._check_idx()
             self.train_step_eager()
         elif self._pending:
             self._stall_wait(self.split_at)
@@ -788,10 +800,12 @@ class UNetEngine:
         if self._share is not None:
             self._share._await_all()                   # the parameters are the parent's (FedAvg buckets in flight)
         if not use_graph:
+            self._check_idx()
             self.forward(False)
             return
         self._await_all()
         if self.eval_graph is None:
+            self._check_idx()
             s = torch.cuda.Stream(device=self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             with torch.cuda.stream(s):

@@ -320,6 +320,20 @@ def _engine_and_ref(S=64, B=2, seed=0):
     return table, eng, flat, x, y
 
 
+def test_engine_refuses_out_of_range_indices():
+    """A directly written idx past the bound dataset is refused on the host (eager step, eval step, capture) - the
+    kernels gather images / masks through it, so it would be an out-of-range device read, not an error."""
+    table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=0)
+    eng.idx.copy_(torch.tensor([0, 8], dtype=torch.int32, device=DEV))     # 8 images are bound: index 8 is past
+    for step in (lambda: eng.train_step(use_graph=False), lambda: eng.train_step(use_graph=True),
+                 lambda: eng.eval_step(use_graph=False)):
+        with pytest.raises(ValueError):
+            step()
+    eng.idx.copy_(torch.tensor([0, 7], dtype=torch.int32, device=DEV))
+    eng.train_step(use_graph=False)
+    torch.cuda.synchronize()
+
+
 def test_memplan_matches_engine_allocation():
     """models/memplan.py prices the engine: measured HBM after an eager 512^2 train step (activations, backward
     buffers, slabs, split-K workspace) stays under the plan, and the per-batch growth matches the planned planes."""
