@@ -895,11 +895,13 @@ class UNetEngine:
 
     def eval_batch_for(self, n_images: int, cap: int = 0) -> int:
         """Largest eval batch <= cap that is a multiple of B and divides ``n_images`` (a whole number of the
-        reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 1024
-        images - the inference engine holds forward activations only (21.7 MB per 256^2 image), and batches of
-        several hundred images fill the chip where the 16-48-image forward is launch / latency-bound."""
+        reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 2048
+        images up to 256^2, 1024 above - the inference engine holds forward activations only (21.7 MB per 256^2
+        image: 38.5 GB for the bench's 1,776-image split in ONE launch, vs three 592-image launches under a 1024 cap:
+        13,069 vs 13,037 img/s), and batches of several hundred images fill the chip where the 16-48-image forward is
+        launch / latency-bound."""
         if cap <= 0:
-            cap = int(os.environ.get("CFL_EVAL_CAP", "1024"))
+            cap = int(os.environ.get("CFL_EVAL_CAP", "2048" if self.S <= 256 else "1024"))
         nb = n_images // self.B
         best = 1
         for k in range(1, nb + 1):
