@@ -62,6 +62,9 @@ def main() -> int:
                          "per layer) - for kernel traces of the overlap (tools/overlap_summary.py)")
     ap.add_argument("--verify-fedavg", action="store_true",
                     help="after the timed rounds, check one weighted FedAvg against an all-gathered reference")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="deterministic reduction mode (int64 fixed-point cross-block sums: bitwise-reproducible "
+                         "steps; models/engine.py UNetEngine(deterministic=True), env CFL_DETERMINISTIC=1)")
     ap.add_argument("--tune", default="",
                     help="launch-shape knobs for A/B sweeps, 'KEY=V,...' (csrc/kernels/launch.h TuneKey names without "
                          "the TUNE_ prefix, e.g. WGRAD3_BLOCKS=256); default: the built-in heuristics")
@@ -124,7 +127,8 @@ def main() -> int:
               flush=True)
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank,
                                  split=min(6213, max(args.batch, int(args.samples * 0.7766))))
-    eng = UNetEngine(table, args.batch, args.img, dev)
+    det = args.deterministic or os.environ.get("CFL_DETERMINISTIC", "0") == "1"
+    eng = UNetEngine(table, args.batch, args.img, dev, deterministic=det)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
     agg = None
@@ -292,6 +296,7 @@ def main() -> int:
                "peak_hbm_gb_per_client": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "dist_backend": (dist.get_backend() if world > 1 else None),
+               "deterministic": det,
                **({"fedavg_max_abs_err": fedavg_err} if fedavg_err is not None else {}),
                **fedavg_stats,
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",

@@ -47,12 +47,24 @@ class Lazy:
 class UNetEngine:
     def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
                  lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
-                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, share: Optional["UNetEngine"] = None):
+                 bn_momentum: float = 0.99, bn_eps: float = 1e-3, share: Optional["UNetEngine"] = None,
+                 deterministic: Optional[bool] = None):
         """``share``: an inference-only engine (see ``evaluator``) reading another engine's parameters and packed
-        weights in place (no copy, no repack)."""
+        weights in place (no copy, no repack).
+
+        ``deterministic`` (default: env CFL_DETERMINISTIC=1): every cross-block reduction of the step (BN batch
+        statistics, BN-backward sums, weight-gradient replica rows, the head's dW / db) accumulates 64-bit
+        fixed-point integers instead of float atomics (csrc/kernels/common.h), so replays of the same step are
+        bitwise equal. The mode is per PROCESS (each kernel module's constant flag): an engine refuses to step when
+        the process mode differs from its own (its reduction buffers are laid out for one of the two)."""
         if img % 16:
             raise ValueError("image size must be a multiple of 16")
         self.C = hip()
+        if deterministic is None:
+            deterministic = share.det if share is not None else os.environ.get("CFL_DETERMINISTIC", "0") == "1"
+        self.det = bool(deterministic)
+        self.C.set_det(1 if self.det else 0)
+        self._w = 2 if self.det else 1       # float slots per reduction-buffer element (int64 in the mode)
         self._pending: List[tuple] = []
         self.table = table
         self.B, self.S = batch, img
@@ -229,15 +241,16 @@ class UNetEngine:
         self.bn_names = [ly.name for ly in bn_layers]
         tot_c = sum(ly.cout for ly in bn_layers)
         RS = self.RS = int(os.environ.get("CFL_SUM_REPLICAS", self.C.SUM_REPLICAS))
-        self.stats_all = torch.zeros(R * 2 * tot_c, dtype=torch.float32, device=self.dev)
-        self.sums_all = torch.zeros(RS * 2 * tot_c, dtype=torch.float32, device=self.dev)
+        w = self._w                          # deterministic mode: int64 elements at the same indices
+        self.stats_all = torch.zeros(w * R * 2 * tot_c, dtype=torch.float32, device=self.dev)
+        self.sums_all = torch.zeros(w * RS * 2 * tot_c, dtype=torch.float32, device=self.dev)
         self.ab_all = torch.zeros(4 * tot_c, dtype=torch.float32, device=self.dev)
         self.bn: Dict[str, Dict[str, torch.Tensor]] = {}
         so = 0
         for ly in bn_layers:
             c = ly.cout
-            self.bn[ly.name] = dict(C=c, stats=self.stats_all[R * 2 * so:R * 2 * (so + c)],
-                                    sums=self.sums_all[RS * 2 * so:RS * 2 * (so + c)],
+            self.bn[ly.name] = dict(C=c, stats=self.stats_all[w * R * 2 * so:w * R * 2 * (so + c)],
+                                    sums=self.sums_all[w * RS * 2 * so:w * RS * 2 * (so + c)],
                                     ab=self.ab_all[4 * so:4 * (so + c)])
             so += c
         # forward activations (raw bf16) and backward buffers: shapes from models/memplan.py (the HBM planner
@@ -259,13 +272,13 @@ class UNetEngine:
             slabs += [(s1, "depthwise_kernel", 9 * cin), (s2, "depthwise_kernel", 9 * F)]
             cin = F
         tot = sum((n + 63) // 64 * 64 for _, _, n in slabs)
-        self.gws = torch.zeros(R * tot, dtype=torch.float32, device=self.dev)
+        self.gws = torch.zeros(self._w * R * tot, dtype=torch.float32, device=self.dev)
         self.gslab: Dict[Tuple[str, str], torch.Tensor] = {}
         entries, off = [], 0
-        for ly, w, n in slabs:
-            sl = self.gws[off:off + R * n]
-            self.gslab[(ly, w)] = sl
-            entries.append((sl, self.G(ly, w), n, R, self.C.GF_REDUCE))
+        for ly, wn, n in slabs:
+            sl = self.gws[self._w * off:self._w * (off + R * n)]
+            self.gslab[(ly, wn)] = sl
+            entries.append((sl, self.G(ly, wn), n, R, self.C.GF_REDUCE))
             off += R * ((n + 63) // 64 * 64)
         for k in range(len(ENC_FILTERS)):
             entries.append((self.G(names[2 + 5 * k + 3], "beta"), self.G(names[2 + 5 * k + 4], "bias"),
@@ -274,6 +287,14 @@ class UNetEngine:
             base = 17 + 5 * k
             entries.append((self.G(names[base + 3], "beta"), self.G(names[base + 4], "bias"), DEC_FILTERS[k], 1,
                             self.C.GF_COPY))
+        # deterministic mode: the head's dW / db accumulate as int64 fixed point here (head_bwd), converted into the
+        # flat gradient by two GF_FIXED entries
+        cin = DEC_FILTERS[-1]
+        self.head_fx = torch.zeros(2 * (cin + 1) + 62, dtype=torch.float32, device=self.dev) if self.det else None
+        if self.det:
+            hl = names[-1]
+            entries.append((self.head_fx, self.G(hl, "kernel"), cin, 1, self.C.GF_FIXED))
+            entries.append((self.head_fx[2 * cin:], self.G(hl, "bias"), 1, 1, self.C.GF_FIXED))
         self._finish_static = entries
         self._finish_dyn: List[tuple] = []
         self._wslabs: Dict[str, torch.Tensor] = {}
@@ -331,8 +352,8 @@ class UNetEngine:
             if rows == 1 and plain:
                 # one plainly-stored row (the 16^2 decoder layers) IS the gradient: stored in place, no finish pass
                 slab = dst
-            else:
-                slab = torch.zeros(rows * n, dtype=torch.float32, device=self.dev)
+            else:       # atomic replica rows hold int64 fixed point in the deterministic mode (plain rows: floats)
+                slab = torch.zeros(rows * n * (1 if plain else self._w), dtype=torch.float32, device=self.dev)
                 self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
             self._wslabs[key] = slab
             self._finish_dirty = True
@@ -538,7 +559,7 @@ class UNetEngine:
         C.head_bwd(A["d3_xlo"], self.P(hl, "kernel"), self.P(hl, "bias"), self.masks, self.idx, self.h,
                    self.metrics, D["dxlo3"], self.G(hl, "kernel"), self.G(hl, "bias"), B, r[0], DEC_FILTERS[-1],
                    self.dice, node_y=A["d3_c2"], node_ab=bn_last["ab"], node_sums=bn_last["sums"], node_reps=self.RS,
-                   fused=1 if self.fuse_head else 0)
+                   fused=1 if self.fuse_head else 0, dwfx=self.head_fx)
         dxlo = D["dxlo3"]
         for k in range(3, -1, -1):
             F = DEC_FILTERS[k]
@@ -718,7 +739,13 @@ class UNetEngine:
         if lo < 0 or hi >= self.n_data:
             raise ValueError(f"idx holds [{lo}, {hi}] but the bound dataset has {self.n_data} images")
 
+    def _check_det(self) -> None:
+        if self.C.det() != int(self.det):
+            raise RuntimeError(f"engine built for deterministic={self.det} but the process mode is "
+                               f"{bool(self.C.det())} (another engine switched it; the mode is per process)")
+
     def train_step_eager(self) -> None:
+        self._check_det()
         self._zero_step()
         self.forward(True)
         self.backward()
@@ -780,6 +807,8 @@ class UNetEngine:
         the step replays as its two split graphs: the encoder graph waits (device-side event waits, no host sync)
         only for the buckets holding the encoder's parameters and their repack, the rest of the step for every
         bucket - so the later buckets' all-reduce runs under the encoder forward."""
+        if use_graph:
+            self._check_det()
         if use_graph and self.graph is None:
             self._check_idx()
             self.capture()
@@ -865,7 +894,7 @@ class UNetEngine:
         if ev is None:
             share = ParamSnapshot(self) if snapshot else self
             ev = UNetEngine(self.table, batch, self.S, self.dev, "bce", self.lr, self.b1, self.b2, self.adam_eps,
-                            self.momentum, self.bn_eps, share=share)
+                            self.momentum, self.bn_eps, share=share, deterministic=self.det)
             ev.snap = share if snapshot else None
             if self.images is not None:
                 ev.bind_data(self.images, self.masks)

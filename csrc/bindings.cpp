@@ -603,12 +603,16 @@ void head_fwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, 
 
 void head_bwd_op(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor masks, at::Tensor idx, at::Tensor h,
                  at::Tensor metrics, at::Tensor dx, at::Tensor dw, at::Tensor db, int B, int R, int Cin, int dice,
-                 OptT node_y, OptT node_ab, OptT node_sums, int node_reps, int fused) {
+                 OptT node_y, OptT node_ab, OptT node_sums, int node_reps, int fused, OptT dwfx) {
   HeadParams p = headp(x, w, bias, masks, idx, h, metrics, B, R, Cin, dice);
   p.fused = fused;
   p.dx = ptr<bf16_t>(dx, "dx");
   p.dw = ptr<float>(dw, "dw");
   p.db = ptr<float>(db, "db");
+  if (cfl_det_host()) {               // deterministic mode: dW / db accumulate as int64 fixed point (GF_FIXED)
+    TORCH_CHECK(dwfx.has_value() && dwfx->numel() >= 2 * (Cin + 1), "head_bwd: the deterministic mode needs dwfx");
+    p.dwfx = ptr<float>(*dwfx, "dwfx");
+  }
   TORCH_CHECK(dx.numel() == x.numel(), "head_bwd: dx size");
   p.node = node_epi_args(node_y, node_ab, node_sums, node_reps, 0, dx.numel(), Cin);
   ok(head_bwd(p, stream()), "head_bwd");
@@ -720,10 +724,15 @@ std::tuple<at::Tensor, int> make_grad_finish_table(std::vector<std::tuple<at::Te
     g.src = ptr<float>(std::get<0>(e), "src");
     g.dst = ptr<float>(std::get<1>(e), "dst");
     g.n = std::get<2>(e); g.replicas = std::get<3>(e); g.mode = std::get<4>(e);
-    TORCH_CHECK(g.n % 4 == 0 && (reinterpret_cast<uintptr_t>(g.src) & 15) == 0 &&
-                (reinterpret_cast<uintptr_t>(g.dst) & 15) == 0, "grad_finish: n % 4 and 16-byte alignment");
+    TORCH_CHECK(g.mode >= GF_REDUCE && g.mode <= GF_FIXED, "grad_finish: mode");
+    TORCH_CHECK(g.mode != GF_FIXED || cfl_det_host(), "grad_finish: GF_FIXED entries need the deterministic mode");
+    TORCH_CHECK(g.mode == GF_FIXED || (g.n % 4 == 0 && (reinterpret_cast<uintptr_t>(g.src) & 15) == 0 &&
+                (reinterpret_cast<uintptr_t>(g.dst) & 15) == 0), "grad_finish: n % 4 and 16-byte alignment");
     TORCH_CHECK(std::get<1>(e).numel() >= g.n, "grad_finish: dst size");
-    TORCH_CHECK(std::get<0>(e).numel() >= (int64_t)g.n * (g.mode == GF_COPY ? 1 : g.replicas), "grad_finish: src size");
+    // deterministic mode: REDUCE / FIXED sources are int64 fixed-point elements (two floats each)
+    const int64_t w = cfl_det_host() && (g.mode == GF_REDUCE || g.mode == GF_FIXED) ? 2 : 1;
+    TORCH_CHECK(std::get<0>(e).numel() >= w * g.n * (g.mode == GF_COPY || g.mode == GF_FIXED ? 1 : g.replicas),
+                "grad_finish: src size");
     h.push_back(g);
   }
   TORCH_CHECK(h.size() <= 256, "grad_finish: at most 256 entries");
@@ -865,6 +874,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(), py::arg("bwd_reps") = 1,
         py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(), py::arg("bwd_dbeta") = py::none());
   m.def("make_grad_finish_table", &make_grad_finish_table);
+  m.def("set_det", [](int v) { ok(cfl_det_set(v), "set_det"); },
+        "deterministic reduction mode (int64 fixed-point cross-block sums) on / off; before any graph capture");
+  m.def("det", []() { return cfl_det_host(); });
+  m.attr("GF_FIXED") = (int)GF_FIXED;
   m.def("grad_finish", &grad_finish_op);
   m.def("make_zero_table", &make_zero_table);
   m.def("zero_spans", &zero_spans_op, py::arg("table"), py::arg("n"), py::arg("max_bytes"),
@@ -930,7 +943,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_bwd", &head_bwd_op, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("masks"), py::arg("idx"),
         py::arg("h"), py::arg("metrics"), py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("B"), py::arg("R"),
         py::arg("Cin"), py::arg("dice"), py::arg("node_y") = py::none(), py::arg("node_ab") = py::none(),
-        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("fused") = 0);
+        py::arg("node_sums") = py::none(), py::arg("node_reps") = 1, py::arg("fused") = 0,
+        py::arg("dwfx") = py::none());
   m.def("adam_update", &adam_update_op);
   m.def("adam_step_done", &adam_step_done_op);
   m.def("make_pack_table", &make_pack_table);

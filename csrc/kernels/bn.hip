@@ -22,6 +22,11 @@ constexpr int FT = 1024;
 
 // sums of channel threadIdx.x (valid for threadIdx.x < C after the call) into (s, s2)
 __device__ __forceinline__ void replica_sums(const float* stats, int C, float (*part)[FT], float& s, float& s2) {
+  if (cfl_det()) {                                   // int64 fixed-point rows (common.h): exact in any order
+    s = s2 = 0.f;
+    if (threadIdx.x < C) stat_sums_det(stats, C, threadIdx.x, s, s2);
+    return;
+  }
   const int per = FT / C, c = threadIdx.x % C, j = threadIdx.x / C;
   float a = 0.f, b = 0.f;
   // fully unrolled with a guard: a thread's (up to STAT_REPLICAS / 4 for C = 256) loads all issue before the adds
@@ -221,12 +226,12 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
   if (!p.sums) return;
   // replica row of this block: every block adding into ONE row of sums serialises at the memory-side atomic units
   const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
-  if (sab) block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * 2 * p.C, red);
+  if (sab) block_channel_atomics<2>(s, G, p.C, p.sums, (size_t)(blockIdx.x % reps) * 2 * p.C, false, red);
   else {
     float s1[1][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[0][j] = s[0][j];
-    block_channel_atomics<1>(s1, G, p.C, p.sums + (size_t)(blockIdx.x % reps) * p.C, red);
+    block_channel_atomics<1>(s1, G, p.C, p.sums, (size_t)(blockIdx.x % reps) * p.C, false, red);
   }
 }
 
@@ -332,3 +337,6 @@ int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_bwd_apply_grid(p)), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_bn(int v) { return cfl_det_upload(v); }

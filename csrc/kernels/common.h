@@ -117,6 +117,43 @@ CFL_DEVICE float block_sum(float v, float* red /* >= NT/64 floats of LDS */) {
 CFL_DEVICE int imin(int a, int b) { return a < b ? a : b; }
 CFL_DEVICE int imax(int a, int b) { return a > b ? a : b; }
 
+// ---------------------------------------------------------------- deterministic reduction mode
+// Every cross-block reduction of a training step - BN batch statistics, BN-backward node sums, weight-gradient
+// replica rows, the head's dW / db - is a float atomicAdd by default: the total depends on the order in which the
+// blocks' atomics arrive, so two replays of one step differ in the last bits. In deterministic mode
+// (CFL_DETERMINISTIC=1, models/engine.py) each of these atomics adds a 64-bit fixed-point integer instead,
+// llrint(v * 2^s): integer addition is associative, so the totals and everything computed from them are bitwise
+// reproducible. The reduction buffers then hold int64 elements at the SAME element indices (twice the bytes: the
+// engine allocates them so), and their consumers sum replica rows as integers and convert once. Scales (|total|
+// bound per element; resolution):
+//   CFL_FX_S0 = 2^24  BN sums of the (bf16-rounded) layer outputs       (< 5.5e11; 6e-8)
+//   CFL_FX_S1 = 2^16  BN sums of their squares                           (< 1.4e14; 1.5e-5)
+//   CFL_FX_G  = 2^40  BN-backward node sums, weight gradients, head dW   (< 8.4e6;  9.1e-13)
+// The flag is each translation unit's constant g_cfl_det (set through cfl_det_set() in every TU, launch.h, before
+// any graph capture). The host copy (cfl_det_host) sizes grad_finish's work split.
+namespace {
+__constant__ int g_cfl_det;
+}
+#define CFL_FX_S0 16777216.0
+#define CFL_FX_S1 65536.0
+#define CFL_FX_G 1099511627776.0
+CFL_DEVICE bool cfl_det() { return g_cfl_det != 0; }
+// element i of a reduction buffer += v: a float atomic, or (deterministic) an int64 fixed-point atomic at `scale`
+CFL_DEVICE void red_add(float* buf, size_t i, float v, double scale) {
+  if (cfl_det())
+    atomicAdd(reinterpret_cast<unsigned long long*>(buf) + i, (unsigned long long)__double2ll_rn((double)v * scale));
+  else
+    atomicAdd(buf + i, v);
+}
+// raw int64 element i of a deterministic-mode reduction buffer
+CFL_DEVICE long long red_raw(const float* buf, size_t i) { return reinterpret_cast<const long long*>(buf)[i]; }
+CFL_DEVICE float red_fx(long long q, double scale) { return (float)((double)q / scale); }
+// scale of the epilogue sums of a BN layer's statistics (st 0: sums, 1: sums of squares) or of node sums
+CFL_DEVICE double red_scale(bool stats, int st) { return stats ? (st ? CFL_FX_S1 : CFL_FX_S0) : CFL_FX_G; }
+static inline int cfl_det_upload(int v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_det), &v, sizeof(int)) == hipSuccess ? 0 : 3;
+}
+
 // log2 of a power of two (host or device)
 __host__ __device__ inline int ilog2(int x) {
   int l = 0;
@@ -126,9 +163,11 @@ __host__ __device__ inline int ilog2(int x) {
 
 // Per-channel sums of 8-channel vectors held by a 256-thread block where thread t owns channel group t % G:
 // reduce the wave's lanes that share the group (stride G), then the 4 waves through LDS, then one atomic per
-// channel into dst[0..C) and (if NS == 2) dst[C..2C).
+// channel into buf[off + 0..C) and (if NS == 2) buf[off + C..2C) (red_add: float, or int64 fixed point in the
+// deterministic mode at the BN-statistics scales when `stats`, else the node-sum scale).
 template <int NS>
-CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* dst, float (*red)[4][256]) {
+CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* buf, size_t off, bool stats,
+                                      float (*red)[4][256]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c0 = (threadIdx.x % G) * 8;
 #pragma unroll
   for (int k = 0; k < NS; ++k)
@@ -145,7 +184,7 @@ CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* ds
   for (int e = threadIdx.x; e < NS * C; e += 256) {
     const int k = e / C, c = e - k * C;
     const float v = red[k][0][c] + red[k][1][c] + red[k][2][c] + red[k][3][c];
-    atomicAdd(&dst[k * C + c], v);
+    red_add(buf, off + (size_t)k * C + c, v, red_scale(stats, k));
   }
 }
 
@@ -229,25 +268,40 @@ CFL_DEVICE void bnb_prologue(const BnBwdIn& q, int C, float* co, float* part, bo
     rm = q.ab[3 * C + t];
   }
   float s_lo = 0.f, s_hi = 0.f;                 // sums of element t (and t + NTH when C2 > NTH)
+  const bool det = cfl_det();                   // int64 fixed-point rows: summed as integers, converted once
   if (C2 <= NTH) {
     const int per = NTH / C2, e = t % C2, j = t / C2;
     float v = 0.f;
+    long long vi = 0;
 #pragma unroll
     for (int k = 0; k < BNB_MAX_REPS; ++k) {
       const int r = j + k * per;
-      if (r < reps) v += q.sums[(size_t)r * C2 + e];
+      if (r < reps) {
+        if (det) vi += red_raw(q.sums, (size_t)r * C2 + e);
+        else v += q.sums[(size_t)r * C2 + e];
+      }
     }
-    part[t] = v;
+    part[t] = det ? red_fx(vi, CFL_FX_G) : v;
     __syncthreads();
     if (t < C2)
       for (int k = 0; k < per; ++k) s_lo += part[k * C2 + t];
   } else {                                      // C2 == 2 * NTH at most (C <= 256, NTH = 256)
+    long long lo = 0, hi = 0;
 #pragma unroll
     for (int r = 0; r < BNB_MAX_REPS; ++r)
       if (r < reps) {
-        s_lo += q.sums[(size_t)r * C2 + t];
-        s_hi += q.sums[(size_t)r * C2 + t + NTH];
+        if (det) {
+          lo += red_raw(q.sums, (size_t)r * C2 + t);
+          hi += red_raw(q.sums, (size_t)r * C2 + t + NTH);
+        } else {
+          s_lo += q.sums[(size_t)r * C2 + t];
+          s_hi += q.sums[(size_t)r * C2 + t + NTH];
+        }
       }
+    if (det) {
+      s_lo = red_fx(lo, CFL_FX_G);
+      s_hi = red_fx(hi, CFL_FX_G);
+    }
   }
   // element e < C is s0[e], e >= C is s1[e - C]
   if (t < C2) {

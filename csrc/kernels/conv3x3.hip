@@ -433,12 +433,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       }
     }
     __syncthreads();
-    float* rep = pj ? p.pj.sums + (size_t)(tile_id % (p.pj.reps > 1 ? p.pj.reps : 1)) * 2 * p.N
-               : node ? p.node.sums + (size_t)(tile_id % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                      : p.stats + (size_t)(tile_id % STAT_REPLICAS) * 2 * p.N;
+    // replica row of this block (element offset: the deterministic mode's int64 rows use the same indices)
+    float* rep = pj ? p.pj.sums : node ? p.node.sums : p.stats;
+    const int nrep = pj ? (p.pj.reps > 1 ? p.pj.reps : 1) : node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS;
+    const size_t ro = (size_t)(tile_id % nrep) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
-      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+      red_add(rep, ro + st * p.N + nBlock + cc, sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc],
+              red_scale(!pj && !node, st));
     }
   }
 }
@@ -709,12 +711,13 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
     }
     __syncthreads();
     const int rb = blockIdx.x / nb;                     // replica row (blocks of one column block spread)
-    float* rep = pj ? p.pj.sums + (size_t)(rb % (p.pj.reps > 1 ? p.pj.reps : 1)) * 2 * p.N
-               : node ? p.node.sums + (size_t)(rb % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                      : p.stats + (size_t)(rb % STAT_REPLICAS) * 2 * p.N;
+    float* rep = pj ? p.pj.sums : node ? p.node.sums : p.stats;
+    const int nrep = pj ? (p.pj.reps > 1 ? p.pj.reps : 1) : node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS;
+    const size_t ro = (size_t)(rb % nrep) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
-      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+      red_add(rep, ro + st * p.N + nBlock + cc, sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc],
+              red_scale(!pj && !node, st));
     }
   }
 }
@@ -900,3 +903,6 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   if (hipGetLastError() != hipSuccess) return 3;
   return splits > 1 ? -splits : 0;   // negative: caller must run the split-K epilogue
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv3x3(int v) { return cfl_det_upload(v); }

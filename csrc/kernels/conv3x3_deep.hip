@@ -257,11 +257,12 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_deep_kernel(ConvParams p) {
       }
     }
     __syncthreads();
-    float* rep = node ? p.node.sums + (size_t)(tile % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                      : p.stats + (size_t)(tile % STAT_REPLICAS) * 2 * p.N;
+    float* rep = node ? p.node.sums : p.stats;
+    const size_t ro = (size_t)(tile % (node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS)) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
-      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+      red_add(rep, ro + st * p.N + nBlock + cc, sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc],
+              red_scale(!node, st));
     }
   }
 }
@@ -286,3 +287,6 @@ int conv3x3_deep(const ConvParams& p, hipStream_t st) {
   hipLaunchKernelGGL((conv3x3_deep_kernel<8, 8, 2, 2>), dim3(blocks), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv3x3_deep(int v) { return cfl_det_upload(v); }

@@ -418,12 +418,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
       }
     }
     __syncthreads();
-    float* rep = PJ ? p.pj.sums + (size_t)(tile % (p.pj.reps > 1 ? p.pj.reps : 1)) * 2 * p.N
-               : node ? p.node.sums + (size_t)(tile % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                      : p.stats + (size_t)(tile % STAT_REPLICAS) * 2 * p.N;
+    float* rep = PJ ? p.pj.sums : node ? p.node.sums : p.stats;
+    const int nrep = PJ ? (p.pj.reps > 1 ? p.pj.reps : 1) : node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS;
+    const size_t ro = (size_t)(tile % nrep) * 2 * p.N;
     for (int e = tid; e < 2 * BN; e += NT) {
       const int st = e / BN, cc = e - st * BN;
-      atomicAdd(&rep[st * p.N + nBlock + cc], sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc]);
+      red_add(rep, ro + st * p.N + nBlock + cc, sred[st][0][cc] + sred[st][1][cc] + sred[st][2][cc] + sred[st][3][cc],
+              red_scale(!PJ && !node, st));
     }
   }
 }
@@ -510,3 +511,6 @@ int conv3x3_sk(const ConvParams& p, hipStream_t st) {
   }
   return 1;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv3x3_sk(int v) { return cfl_det_upload(v); }

@@ -144,3 +144,6 @@ int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {
   else hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, false>), grid, dim3(NT), 0, st, p, tiles, splits);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv3x3_wgrad(int v) { return cfl_det_upload(v); }

@@ -356,14 +356,14 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       }
     }
     __syncthreads();
-    float* rep = node ? p.node.sums + (size_t)(blockIdx.x % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                      : p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+    float* rep = node ? p.node.sums : p.stats;
+    const size_t ro = (size_t)(blockIdx.x % (node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS)) * 2 * p.N;
     for (int e = tid; e < 2 * BN_; e += NT) {
       const int st = e / BN_, cc = e - st * BN_;
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
-      atomicAdd(&rep[st * p.N + nBlock + cc], v);
+      red_add(rep, ro + st * p.N + nBlock + cc, v, red_scale(!node, st));
     }
   }
 }
@@ -421,14 +421,14 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
     }
   }
   __syncthreads();
-  float* rep = node ? p.node.sums + (size_t)(blockIdx.x % (p.node.reps > 1 ? p.node.reps : 1)) * 2 * p.N
-                    : p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.N;
+  float* rep = node ? p.node.sums : p.stats;
+  const size_t ro = (size_t)(blockIdx.x % (node ? (p.node.reps > 1 ? p.node.reps : 1) : STAT_REPLICAS)) * 2 * p.N;
   for (int e = threadIdx.x; e < 2 * p.N; e += NT) {
     const int st = e / p.N, cc = e - st * p.N;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) v += red[st][w][cc];
-    atomicAdd(&rep[st * p.N + cc], v);
+    red_add(rep, ro + st * p.N + cc, v, red_scale(!node, st));
   }
 }
 
@@ -572,3 +572,6 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv_igemm(int v) { return cfl_det_upload(v); }

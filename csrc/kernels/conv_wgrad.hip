@@ -193,7 +193,7 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
 
   // epilogue: D[k][n], col n = lane&15, row k = (lane>>4)*4 + r; slab mode spreads the split blocks' atomics
   // over replica rows (every block adding into ONE row serialises at the memory-side atomic units)
-  float* dwb = p.slabs > 0 ? p.dw + (size_t)(bz % p.slabs) * p.K * p.N : p.dw;
+  const size_t ro = p.slabs > 0 ? (size_t)(bz % p.slabs) * p.K * p.N : 0;
 #pragma unroll
   for (int i = 0; i < FK; ++i)
 #pragma unroll
@@ -209,7 +209,7 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
         } else {
           dst = (size_t)k * p.N + n;
         }
-        atomicAdd(&dwb[dst], acc[i][j][r]);
+        red_add(p.dw, ro + dst, acc[i][j][r], CFL_FX_G);
       }
     }
 }
@@ -537,3 +537,6 @@ int conv_wgrad(const WgradParams& p, hipStream_t st) {
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_conv_wgrad(int v) { return cfl_det_upload(v); }

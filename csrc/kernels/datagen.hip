@@ -115,3 +115,6 @@ int resize_batch(const uint8_t* src, const int64_t* offs, const int* dims, uint8
   hipLaunchKernelGGL(resize_batch_kernel, grid, dim3(256), 0, st, src, offs, dims, dst, dh, dw, c, binarize);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_datagen(int v) { return cfl_det_upload(v); }

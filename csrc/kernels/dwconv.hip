@@ -153,10 +153,10 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) 
   __syncthreads();
   // one contiguous 9*C row of atomics per block, spread over `replicas` rows (reduced later by grad_finish):
   // every block adding into ONE row serialises at the memory-side atomic units
-  float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
+  const size_t ro = (size_t)(blockIdx.x % replicas) * 9 * p.C;
   for (int e = threadIdx.x; e < 9 * p.C; e += NT) {
     const int t = e / p.C, c = e - t * p.C;
-    atomicAdd(&dst[t * p.C + c], red[0][t][c] + red[1][t][c] + red[2][t][c] + red[3][t][c]);
+    red_add(p.dw, ro + t * p.C + c, red[0][t][c] + red[1][t][c] + red[2][t][c] + red[3][t][c], CFL_FX_G);
   }
 }
 
@@ -478,19 +478,19 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
     }
     __syncthreads();
     float* dst;
-    int rstride;
+    size_t ro;
     if (MODE == 2) {
-      dst = p.dw + (size_t)(bid % replicas) * 9 * p.C;
-      rstride = p.C;
+      dst = p.dw;
+      ro = (size_t)(bid % replicas) * 9 * p.C;
     } else {
       const int reps = p.node.reps > 1 ? p.node.reps : 1;
-      dst = p.node.sums + (size_t)(bid % reps) * 2 * p.C;
-      rstride = p.C;
+      dst = p.node.sums;
+      ro = (size_t)(bid % reps) * 2 * p.C;
     }
     for (int e = tid; e < NS * CT; e += NT) {
       const int t = e / CT, c = e % CT;
-      atomicAdd(&dst[t * rstride + cbase + c], red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] +
-                                                   red[(2 * NS + t) * CT + c] + red[(3 * NS + t) * CT + c]);
+      red_add(dst, ro + t * p.C + cbase + c, red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] +
+                                                 red[(2 * NS + t) * CT + c] + red[(3 * NS + t) * CT + c], CFL_FX_G);
     }
   }
 }
@@ -741,14 +741,15 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
       for (int j = 0; j < 4; ++j) red[(wid * NS + t) * CT + cg * CPT + j] = part[t][j];
   }
   __syncthreads();
-  float* dwr = p.dw + (size_t)(blockIdx.x % replicas) * 9 * p.C;
+  const size_t dro = (size_t)(blockIdx.x % replicas) * 9 * p.C;
   const int nreps = p.node.reps > 1 ? p.node.reps : 1;
-  float* nsr = node ? p.node.sums + (size_t)(blockIdx.x % nreps) * 2 * p.C : nullptr;
+  const size_t nro = (size_t)(blockIdx.x % nreps) * 2 * p.C;
   for (int e = tid; e < (node ? NS : 9) * CT; e += NT) {
     const int t = e / CT, c = e % CT;
     const float v = red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] + red[(2 * NS + t) * CT + c] +
                     red[(3 * NS + t) * CT + c];
-    atomicAdd(t < 9 ? &dwr[t * p.C + cbase + c] : &nsr[(t - 9) * p.C + cbase + c], v);
+    if (t < 9) red_add(p.dw, dro + t * p.C + cbase + c, v, CFL_FX_G);
+    else red_add(p.node.sums, nro + (t - 9) * p.C + cbase + c, v, CFL_FX_G);
   }
 }
 
@@ -873,3 +874,6 @@ int dw_wgrad(const DwParams& p, hipStream_t st) {
   else hipLaunchKernelGGL(dw_wgrad_kernel<1>, dim3(blocks), dim3(NT), 0, st, p, reps);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_dwconv(int v) { return cfl_det_upload(v); }

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(NT) void entry_fwd_kernel(EntryParams p) {
     }
   }
   if (p.stats) {
-    block_channel_atomics<2>(s, G, p.Cout, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.Cout, red);
+    block_channel_atomics<2>(s, G, p.Cout, p.stats, (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * p.Cout, true, red);
   }
 }
 
@@ -136,10 +136,11 @@ __global__ __launch_bounds__(NT) void entry_wgrad_kernel(EntryParams p, int repl
       for (int j = 0; j < 8; ++j) red[wid][a][c0 + j] = acc[a][j];
   }
   __syncthreads();
-  float* dst = p.dw + (size_t)((blockIdx.x + blockIdx.y * gridDim.x) % replicas) * 27 * p.Cout;
+  const size_t ro = (size_t)((blockIdx.x + blockIdx.y * gridDim.x) % replicas) * 27 * p.Cout;
   for (int e = threadIdx.x; e < 9 * p.Cout; e += NT) {
     const int a = e / p.Cout, c = e - a * p.Cout;
-    atomicAdd(&dst[(ky * 9 + a) * p.Cout + c], red[0][a][c] + red[1][a][c] + red[2][a][c] + red[3][a][c]);
+    red_add(p.dw, ro + (ky * 9 + a) * p.Cout + c, red[0][a][c] + red[1][a][c] + red[2][a][c] + red[3][a][c],
+            CFL_FX_G);
   }
 }
 
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
     buf ^= 1;
   }
   if (p.stats) {
-    block_channel_atomics<2>(s, 4, 32, p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 64, red);
+    block_channel_atomics<2>(s, 4, 32, p.stats, (size_t)(blockIdx.x % STAT_REPLICAS) * 64, true, red);
   }
 }
 
@@ -386,9 +387,9 @@ __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wid][(16 * i + 4 * g + r) * 32 + 16 * j + r16] = acc[i][j][r];
   __syncthreads();
-  float* dst = p.dw + (size_t)(blockIdx.x % replicas) * 27 * 32;
+  const size_t ro = (size_t)(blockIdx.x % replicas) * 27 * 32;
   for (int e = tid; e < 27 * 32; e += NT)
-    atomicAdd(&dst[e], (red[0][e] + red[1][e] + red[2][e] + red[3][e]) * (1.f / 255.f));
+    red_add(p.dw, ro + e, (red[0][e] + red[1][e] + red[2][e] + red[3][e]) * (1.f / 255.f), CFL_FX_G);
 }
 
 bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
@@ -457,3 +458,6 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
                      st, p, reps);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_entry(int v) { return cfl_det_upload(v); }

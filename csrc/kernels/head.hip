@@ -237,17 +237,18 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
   __syncthreads();
   if constexpr (NODE) {
     const int reps = p.node.reps > 1 ? p.node.reps : 1;
-    float* dst = p.node.sums + (size_t)(blockIdx.x % reps) * 2 * CIN;
+    const size_t ro = (size_t)(blockIdx.x % reps) * 2 * CIN;
     if (threadIdx.x < 2 * CIN) {
       float s = 0.f;
       for (int w2 = 0; w2 < NT / 64; ++w2) s += nred[threadIdx.x][w2];
-      atomicAdd(&dst[threadIdx.x], s);
+      red_add(p.node.sums, ro + threadIdx.x, s, CFL_FX_G);
     }
   }
   if (threadIdx.x <= CIN) {
     float s = 0.f;
     for (int w2 = 0; w2 < NT / 64; ++w2) s += red[threadIdx.x][w2];
-    if (threadIdx.x < CIN) atomicAdd(&p.dw[threadIdx.x], s);
+    if (cfl_det()) red_add(p.dwfx, threadIdx.x, s, CFL_FX_G);   // int64 [Cin + 1]; grad_finish GF_FIXED converts
+    else if (threadIdx.x < CIN) atomicAdd(&p.dw[threadIdx.x], s);
     else atomicAdd(p.db, s);
   }
   if constexpr (FWD) {
@@ -285,3 +286,6 @@ int head_bwd(const HeadParams& p, hipStream_t st) {
   else hipLaunchKernelGGL((head_bwd_kernel<32, false, false>), g, dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_head(int v) { return cfl_det_upload(v); }

@@ -26,19 +26,35 @@ struct BnStatsIn {
 
 // Coefficients of channel c from the replica sums - THE arithmetic of bn_finalize (replicas summed in order, all
 // loads issued together), so a consumer-side finalize and a bn_finalize launch agree bit for bit.
+// Deterministic mode (common.h): int64 fixed-point rows summed as integers (exact in any order) and converted once.
+__device__ __forceinline__ bool stat_sums_det(const float* stats, int C, int c, float& s, float& s2) {
+  if (!cfl_det()) return false;
+  long long a = 0, b = 0;
+#pragma unroll
+  for (int r = 0; r < STAT_REPLICAS; ++r) {
+    a += red_raw(stats, (size_t)r * 2 * C + c);
+    b += red_raw(stats, (size_t)r * 2 * C + C + c);
+  }
+  s = red_fx(a, CFL_FX_S0);
+  s2 = red_fx(b, CFL_FX_S1);
+  return true;
+}
+
 __device__ __forceinline__ void bn_coef_from_stats(const BnStatsIn& f, int C, int c, float& a, float& b, float& mean,
                                                    float& rstd) {
-  float v0[STAT_REPLICAS], v1[STAT_REPLICAS];
-#pragma unroll
-  for (int r = 0; r < STAT_REPLICAS; ++r) {
-    v0[r] = f.stats[r * 2 * C + c];
-    v1[r] = f.stats[r * 2 * C + C + c];
-  }
   float s = 0.f, s2 = 0.f;
+  if (!stat_sums_det(f.stats, C, c, s, s2)) {
+    float v0[STAT_REPLICAS], v1[STAT_REPLICAS];
 #pragma unroll
-  for (int r = 0; r < STAT_REPLICAS; ++r) {
-    s += v0[r];
-    s2 += v1[r];
+    for (int r = 0; r < STAT_REPLICAS; ++r) {
+      v0[r] = f.stats[r * 2 * C + c];
+      v1[r] = f.stats[r * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int r = 0; r < STAT_REPLICAS; ++r) {
+      s += v0[r];
+      s2 += v1[r];
+    }
   }
   mean = s / f.count;
   const float var = fmaxf(s2 / f.count - mean * mean, 0.f);
@@ -325,6 +341,8 @@ struct HeadParams {
   bf16_t* dx;              // [B,R,R,Cin]
   float* dw;               // grad slots for w (Cin) and bias (1) - accumulated
   float* db;
+  float* dwfx;             // deterministic mode: int64 fixed-point accumulators [Cin + 1] of dw, db (converted into
+                           // them by grad_finish, GF_FIXED); required when the mode is on
   int B, R, Cin;
   int dice;                // add the Dice loss
   int fused;               // head_bwd: also do the forward (logits, loss / accuracy sums) in the same pass (dice 0)
@@ -404,7 +422,11 @@ int opt_step(const OptParams& p, hipStream_t st);
 // (GF_REDUCE: dst[i] += sum_r src[r*n + i], then the replicas are re-zeroed for the next step; GF_SUM: the same
 // for rows that are fully overwritten every step, so no re-zeroing) or that equals
 // another gradient (GF_COPY: dst[i] = src[i], e.g. a residual conv's bias grad == its BN's beta grad).
-enum GradFinishMode { GF_REDUCE = 0, GF_COPY = 1, GF_SUM = 2 };   // GF_SUM: like GF_REDUCE, rows not re-zeroed
+// GF_SUM: like GF_REDUCE, rows not re-zeroed; GF_FIXED (deterministic mode): dst[i] = int64 fixed-point src[i]
+// converted (CFL_FX_G), src re-zeroed, any n. In the deterministic mode GF_REDUCE rows are int64 fixed point too and
+// every entry is one group per tile (rows summed in order, no atomics); the grid must be re-derived
+// (grad_finish_work) after cfl_det_set.
+enum GradFinishMode { GF_REDUCE = 0, GF_COPY = 1, GF_SUM = 2, GF_FIXED = 3 };
 struct GradFinish {
   float* src;
   float* dst;
@@ -483,6 +505,26 @@ enum TuneKey {
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
+// deterministic reduction mode (common.h): sets the constant flag of every kernel translation unit (before any graph
+// capture: the flag is read by the kernels at run time, so captured graphs follow the value at their replay) and the
+// host copy; 0 on success
+int cfl_det_set(int v);
+int cfl_det_host();
+int cfl_det_upload_bn(int v);
+int cfl_det_upload_conv3x3(int v);
+int cfl_det_upload_conv3x3_deep(int v);
+int cfl_det_upload_conv3x3_sk(int v);
+int cfl_det_upload_conv3x3_wgrad(int v);
+int cfl_det_upload_conv_igemm(int v);
+int cfl_det_upload_conv_wgrad(int v);
+int cfl_det_upload_datagen(int v);
+int cfl_det_upload_dwconv(int v);
+int cfl_det_upload_entry(int v);
+int cfl_det_upload_head(int v);
+int cfl_det_upload_optim(int v);
+int cfl_det_upload_pool_add(int v);
+int cfl_det_upload_pw(int v);
+int cfl_det_upload_sepconv(int v);
 
 // ---------------------------------------------------------------- misc (optim.hip / datagen.hip)
 int fill_f32(float* p, float v, int64_t n, hipStream_t st);

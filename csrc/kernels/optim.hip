@@ -133,17 +133,19 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
     const int C = it.n;
     const float mom = p.momentum;
     for (int c = tid; c < C; c += NT) {
-      float va[STAT_REPLICAS], vb[STAT_REPLICAS];
-#pragma unroll
-      for (int r = 0; r < STAT_REPLICAS; ++r) {
-        va[r] = it.stats[r * 2 * C + c];
-        vb[r] = it.stats[r * 2 * C + C + c];
-      }
       float s = 0.f, s2 = 0.f;
+      if (!stat_sums_det(it.stats, C, c, s, s2)) {
+        float va[STAT_REPLICAS], vb[STAT_REPLICAS];
 #pragma unroll
-      for (int r = 0; r < STAT_REPLICAS; ++r) {
-        s += va[r];
-        s2 += vb[r];
+        for (int r = 0; r < STAT_REPLICAS; ++r) {
+          va[r] = it.stats[r * 2 * C + c];
+          vb[r] = it.stats[r * 2 * C + C + c];
+        }
+#pragma unroll
+        for (int r = 0; r < STAT_REPLICAS; ++r) {
+          s += va[r];
+          s2 += vb[r];
+        }
       }
       const float mean = s / it.count;
       const float var = fmaxf(s2 / it.count - mean * mean, 0.f);
@@ -245,8 +247,9 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
   const int wb = threadIdx.x < n_entries ? e[threadIdx.x].work_begin : 0x7fffffff;
   const int k = __syncthreads_count(wb <= (int)blockIdx.x) - 1;
   const GradFinish g = e[k];
-  const int rows = g.mode == GF_COPY ? 1 : g.replicas;
-  const int ngroups = (rows + GF_ROWS - 1) / GF_ROWS;
+  const int rows = g.mode == GF_COPY || g.mode == GF_FIXED ? 1 : g.replicas;
+  const bool det = cfl_det();
+  const int ngroups = det ? 1 : (rows + GF_ROWS - 1) / GF_ROWS;
   const int local = blockIdx.x - g.work_begin;
   const int tile = local / ngroups, rg = local - tile * ngroups;
   const int i0 = tile * 4 * NT + threadIdx.x;
@@ -254,6 +257,60 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (i0 + u * NT < g.n) g.dst[i0 + u * NT] = g.src[i0 + u * NT];
+    return;
+  }
+  if (g.mode == GF_FIXED) {         // deterministic mode: int64 fixed-point accumulators -> dst, re-zeroed
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT;
+      if (i < g.n) {
+        g.dst[i] = red_fx(red_raw(g.src, i), CFL_FX_G);
+        reinterpret_cast<long long*>(g.src)[i] = 0;
+      }
+    }
+    return;
+  }
+  if (det) {                        // one group per tile, every row in order: no atomics into dst
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    long long q[4] = {0, 0, 0, 0};
+    for (int r0 = 0; r0 < rows; r0 += GF_ROWS) {
+      if (g.mode == GF_REDUCE) {    // int64 fixed-point rows (exact in any order), re-zeroed
+        long long v[GF_ROWS][4];
+#pragma unroll
+        for (int r = 0; r < GF_ROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * NT;
+            v[r][u] = (r0 + r < rows && i < g.n) ? red_raw(g.src, (size_t)(r0 + r) * g.n + i) : 0;
+          }
+#pragma unroll
+        for (int r = 0; r < GF_ROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * NT;
+            q[u] += v[r][u];
+            if (r0 + r < rows && i < g.n) reinterpret_cast<long long*>(g.src)[(size_t)(r0 + r) * g.n + i] = 0;
+          }
+      } else {                      // GF_SUM: plainly stored float rows, summed in row order
+        float v[GF_ROWS][4];
+#pragma unroll
+        for (int r = 0; r < GF_ROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * NT;
+            v[r][u] = (r0 + r < rows && i < g.n) ? g.src[(size_t)(r0 + r) * g.n + i] : 0.f;
+          }
+#pragma unroll
+        for (int r = 0; r < GF_ROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) s[u] += v[r][u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT;
+      if (i < g.n) g.dst[i] += g.mode == GF_REDUCE ? red_fx(q[u], CFL_FX_G) : s[u];
+    }
     return;
   }
   const int r0 = rg * GF_ROWS;
@@ -303,6 +360,21 @@ int g_tune[TUNE_N] = {0};
 }  // namespace
 
 int cfl_tune(int key) { return key >= 0 && key < TUNE_N ? g_tune[key] : 0; }
+
+static int g_det_host = 0;
+int cfl_det_host() { return g_det_host; }
+int cfl_det_set(int v) {
+  v = v ? 1 : 0;
+  int (*const up[])(int) = {cfl_det_upload_bn, cfl_det_upload_conv3x3, cfl_det_upload_conv3x3_deep,
+                            cfl_det_upload_conv3x3_sk, cfl_det_upload_conv3x3_wgrad, cfl_det_upload_conv_igemm,
+                            cfl_det_upload_conv_wgrad, cfl_det_upload_datagen, cfl_det_upload_dwconv,
+                            cfl_det_upload_entry, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
+                            cfl_det_upload_pw, cfl_det_upload_sepconv};
+  for (auto f : up)
+    if (f(v)) return 3;
+  g_det_host = v;
+  return 0;
+}
 void cfl_set_tune(int key, int value) {
   if (key >= 0 && key < TUNE_N) g_tune[key] = value;
 }
@@ -311,9 +383,9 @@ int grad_finish_work(GradFinish* h_entries, int n_entries) {
   int w = 0;
   for (int i = 0; i < n_entries; ++i) {
     GradFinish& g = h_entries[i];
-    const int rows = g.mode == GF_COPY ? 1 : g.replicas;
+    const int rows = g.mode == GF_COPY || g.mode == GF_FIXED ? 1 : g.replicas;
     g.work_begin = w;
-    w += ((g.n / 4 + NT - 1) / NT) * ((rows + GF_ROWS - 1) / GF_ROWS);
+    w += ((g.n + 4 * NT - 1) / (4 * NT)) * (cfl_det_host() ? 1 : (rows + GF_ROWS - 1) / GF_ROWS);
   }
   return w;
 }
@@ -376,3 +448,6 @@ int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int row
   hipLaunchKernelGGL(gather_rows_kernel, dim3(bx, rows), dim3(NT), 0, st, src, idx, dst, rows, row_bytes);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_optim(int v) { return cfl_det_upload(v); }

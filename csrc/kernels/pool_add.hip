@@ -106,3 +106,6 @@ int bn_add_fwd(const BnAddParams& p, hipStream_t st) {
   hipLaunchKernelGGL(bn_add_kernel, dim3(row_blocks(p.B * p.H)), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_pool_add(int v) { return cfl_det_upload(v); }

@@ -270,13 +270,13 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
       }
   }
   __syncthreads();
-  float* rep = p.stats + (size_t)(bid % STAT_REPLICAS) * 2 * p.N;
+  const size_t ro = (size_t)(bid % STAT_REPLICAS) * 2 * p.N;
   for (int e = tid; e < 2 * NB; e += NT) {
     const int st = e / NB, cc = e - st * NB;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
-    atomicAdd(&rep[st * p.N + n0 + cc], v);
+    red_add(p.stats, ro + st * p.N + n0 + cc, v, red_scale(true, st));
   }
 }
 
@@ -372,3 +372,6 @@ int pw_conv(const ConvParams& p, hipStream_t st) {
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_pw(int v) { return cfl_det_upload(v); }

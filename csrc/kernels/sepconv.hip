@@ -273,13 +273,13 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
       }
   }
   __syncthreads();
-  float* rep = p.stats + (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * N;
+  const size_t ro = (size_t)(blockIdx.x % STAT_REPLICAS) * 2 * N;
   for (int e = tid; e < 2 * N; e += NT) {
     const int st = e / N, cc = e - st * N;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) v += sred[st][w][cc];
-    atomicAdd(&rep[st * N + cc], v);
+    red_add(p.stats, ro + st * N + cc, v, red_scale(true, st));
   }
 }
 
@@ -314,3 +314,6 @@ int sep_fwd(const SepParams& p, hipStream_t st) {
   if (p.N == 64) return launch<64, 64, 32>(p, st);
   return launch<64, 128, 32>(p, st);
 }
+
+// deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
+int cfl_det_upload_sepconv(int v) { return cfl_det_upload(v); }

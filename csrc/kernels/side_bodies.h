@@ -103,7 +103,7 @@ CFL_DEVICE void node_pool_body(const NodeBwdParams& p, int bid, int nblocks) {
   }
   if (!p.sums) return;
   const int reps = p.sum_reps > 1 ? p.sum_reps : 1;
-  block_channel_atomics<2>(s, G, p.C, p.sums + (size_t)(bid % reps) * 2 * p.C, red);
+  block_channel_atomics<2>(s, G, p.C, p.sums, (size_t)(bid % reps) * 2 * p.C, false, red);
 }
 
 constexpr int BBA_IPT = 4;

@@ -191,7 +191,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
           dst = ((size_t)tap * p.Cin + c) * p.N + n;
         }
         if (slab) dwb[dst] = acc[tap][u][r];
-        else atomicAdd(&dwb[dst], acc[tap][u][r]);
+        else red_add(p.dw, dst, acc[tap][u][r], CFL_FX_G);
       }
     }
 }

@@ -303,13 +303,13 @@ def test_datagen_matches_numpy():
     assert np.abs(imd.cpu().numpy().astype(int) - imh.astype(int)).max() <= 1
 
 
-def _engine_and_ref(S=64, B=2, seed=0):
+def _engine_and_ref(S=64, B=2, seed=0, deterministic=False):
     from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
     from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
     from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
     table = ParamTable()
     data = make_synthetic_device(8, S, seed=seed)
-    eng = UNetEngine(table, B, S)
+    eng = UNetEngine(table, B, S, deterministic=deterministic)
     eng.bind_data(data.images, data.masks)
     flat = table.init_flat(seed)
     eng.set_flat(flat)
@@ -318,6 +318,51 @@ def _engine_and_ref(S=64, B=2, seed=0):
     x = data.images[:B].float().cpu() / 255.0
     y = data.masks[:B].float().cpu()[..., None]
     return table, eng, flat, x, y
+
+
+@pytest.mark.parametrize("S,B", [(64, 2), (256, 4)])
+def test_deterministic_mode_replays_bitwise(S, B):
+    """CFL_DETERMINISTIC / UNetEngine(deterministic=True): every cross-block reduction accumulates int64 fixed point
+    (common.h red_add), so re-running the same training steps from the same state - eagerly or as graph replays -
+    gives bit-identical parameters (BN moving statistics included), Adam moments and BN batch statistics; and the
+    mode stays within the fixed-point rounding of the default (float-atomic) mode."""
+    C_ = hip()
+    try:
+        table, eng, flat, x, y = _engine_and_ref(S=S, B=B, seed=5, deterministic=True)
+        assert C_.det() == 1
+        runs = []
+        for graph in (False, False, True, True):
+            eng.set_flat(flat)
+            eng.reset_optimizer()
+            for _ in range(3):
+                eng.train_step(use_graph=graph)
+            torch.cuda.synchronize()
+            runs.append((eng.get_flat().copy(), eng.m.cpu().clone(), eng.v.cpu().clone(), eng.grad.cpu().clone()))
+        f0, m0, v0, g0 = runs[0]
+        for f, m, v, g in runs[1:]:
+            assert np.array_equal(f, f0), int((f != f0).sum())
+            assert torch.equal(m, m0) and torch.equal(v, v0) and torch.equal(g, g0)
+        # the default mode from the same state: equal up to the fixed-point / atomic-order rounding
+        _, ref, _, _, _ = _engine_and_ref(S=S, B=B, seed=5, deterministic=False)
+        assert C_.det() == 0
+        ref.set_flat(flat)
+        ref.reset_optimizer()
+        ref.train_step(use_graph=False)
+        eng_f = runs[0][0]
+        with pytest.raises(RuntimeError):              # the det engine refuses to step in the other process mode
+            eng.train_step(use_graph=False)
+        table2, eng1, _, _, _ = _engine_and_ref(S=S, B=B, seed=5, deterministic=True)
+        eng1.set_flat(flat)
+        eng1.reset_optimizer()
+        eng1.train_step(use_graph=False)
+        torch.cuda.synchronize()
+        d = np.abs(eng1.get_flat() - ref.get_flat())
+        # first Adam step moves each weight by ~lr * sign(g): near-zero gradients may flip (as between two default
+        # runs); the bulk must agree
+        assert d.max() < 2.5e-3 and (d > 1e-4).mean() < 0.05, ((d > 1e-4).mean(), d.max())
+        assert eng_f is not None
+    finally:
+        C_.set_det(0)
 
 
 def test_engine_refuses_out_of_range_indices():
