@@ -368,7 +368,7 @@ DwParams dw_wgrad_params(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, in
   p.xf = xf(ab, C, relu);
   p.replicas = replicas < 1 ? 1 : replicas;
   TORCH_CHECK(x.numel() == (int64_t)B * H * W * C && dy.numel() == x.numel() &&
-                  dw.numel() == (int64_t)p.replicas * 9 * C, "dw_wgrad sizes");
+                  dw.numel() == (cfl_det_host() ? 2 : 1) * (int64_t)p.replicas * 9 * C, "dw_wgrad sizes");
   return p;
 }
 
@@ -433,7 +433,8 @@ void entry_wgrad_op(at::Tensor images, at::Tensor idx, at::Tensor dy, at::Tensor
   p.dy = ptr<const bf16_t>(dy, "dy");
   p.dw = ptr<float>(dw, "dw");
   p.B = B; p.S = S; p.Cout = Cout; p.Ho = (S + 1) / 2; p.Wo = (S + 1) / 2;
-  TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout && dw.numel() == (int64_t)p.replicas * 27 * Cout,
+  TORCH_CHECK(dy.numel() == (int64_t)B * p.Ho * p.Wo * Cout &&
+                  dw.numel() == (cfl_det_host() ? 2 : 1) * (int64_t)p.replicas * 27 * Cout,
               "entry_wgrad sizes");
   if (bwd_y) {
     TORCH_CHECK(bwd_ab && bwd_sums, "entry_wgrad: bwd_y needs bwd_ab and bwd_sums");
