@@ -342,7 +342,7 @@ class UNetEngine:
         rows, plain = self.C.conv_wgrad_slabs(B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l)
         n = ks * ks * Cin * N
         slab = self._wslabs.get(key)
-        if slab is None or slab.numel() != rows * n:
+        if slab is None or slab.numel() != rows * n * (1 if plain else self._w):
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("weight-gradient slabs must be allocated before graph capture")
             if key in self._wslabs:
