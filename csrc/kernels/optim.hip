@@ -242,13 +242,16 @@ __global__ void gather_rows_kernel(const uint8_t* src, const int32_t* idx, uint8
 // single row group, else with one atomic per element per group.
 constexpr int GF_ROWS = 16;
 
+// DET (deterministic mode, common.h): a separate instantiation - its int64 row registers would otherwise cost the
+// default kernel 72 -> 246 VGPRs (occupancy 7 -> 2)
+template <bool DET>
 __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __restrict__ e, int n_entries) {
   // entry of this block: entries are sorted by work_begin; count how many begin at or before blockIdx.x
   const int wb = threadIdx.x < n_entries ? e[threadIdx.x].work_begin : 0x7fffffff;
   const int k = __syncthreads_count(wb <= (int)blockIdx.x) - 1;
   const GradFinish g = e[k];
   const int rows = g.mode == GF_COPY || g.mode == GF_FIXED ? 1 : g.replicas;
-  const bool det = cfl_det();
+  constexpr bool det = DET;
   const int ngroups = det ? 1 : (rows + GF_ROWS - 1) / GF_ROWS;
   const int local = blockIdx.x - g.work_begin;
   const int tile = local / ngroups, rg = local - tile * ngroups;
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
       if (i0 + u * NT < g.n) g.dst[i0 + u * NT] = g.src[i0 + u * NT];
     return;
   }
-  if (g.mode == GF_FIXED) {         // deterministic mode: int64 fixed-point accumulators -> dst, re-zeroed
+  if (DET && g.mode == GF_FIXED) {  // deterministic mode: int64 fixed-point accumulators -> dst, re-zeroed
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int i = i0 + u * NT;
@@ -270,21 +273,22 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
     }
     return;
   }
-  if (det) {                        // one group per tile, every row in order: no atomics into dst
+  if constexpr (DET) {              // one group per tile, every row in order: no atomics into dst
+    constexpr int GF_DROWS = 4;     // rows per load round (int64 rows: 16 would need ~250 VGPRs)
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     long long q[4] = {0, 0, 0, 0};
-    for (int r0 = 0; r0 < rows; r0 += GF_ROWS) {
+    for (int r0 = 0; r0 < rows; r0 += GF_DROWS) {
       if (g.mode == GF_REDUCE) {    // int64 fixed-point rows (exact in any order), re-zeroed
-        long long v[GF_ROWS][4];
+        long long v[GF_DROWS][4];
 #pragma unroll
-        for (int r = 0; r < GF_ROWS; ++r)
+        for (int r = 0; r < GF_DROWS; ++r)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int i = i0 + u * NT;
             v[r][u] = (r0 + r < rows && i < g.n) ? red_raw(g.src, (size_t)(r0 + r) * g.n + i) : 0;
           }
 #pragma unroll
-        for (int r = 0; r < GF_ROWS; ++r)
+        for (int r = 0; r < GF_DROWS; ++r)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int i = i0 + u * NT;
@@ -292,16 +296,16 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
             if (r0 + r < rows && i < g.n) reinterpret_cast<long long*>(g.src)[(size_t)(r0 + r) * g.n + i] = 0;
           }
       } else {                      // GF_SUM: plainly stored float rows, summed in row order
-        float v[GF_ROWS][4];
+        float v[GF_DROWS][4];
 #pragma unroll
-        for (int r = 0; r < GF_ROWS; ++r)
+        for (int r = 0; r < GF_DROWS; ++r)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int i = i0 + u * NT;
             v[r][u] = (r0 + r < rows && i < g.n) ? g.src[(size_t)(r0 + r) * g.n + i] : 0.f;
           }
 #pragma unroll
-        for (int r = 0; r < GF_ROWS; ++r)
+        for (int r = 0; r < GF_DROWS; ++r)
 #pragma unroll
           for (int u = 0; u < 4; ++u) s[u] += v[r][u];
       }
@@ -393,7 +397,8 @@ int grad_finish_work(GradFinish* h_entries, int n_entries) {
 int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipStream_t st) {
   if (n_entries <= 0 || total_work <= 0) return 0;
   if (n_entries > NT) return 1;
-  hipLaunchKernelGGL(grad_finish_kernel, dim3(total_work), dim3(NT), 0, st, d_entries, n_entries);
+  if (cfl_det_host()) hipLaunchKernelGGL(grad_finish_kernel<true>, dim3(total_work), dim3(NT), 0, st, d_entries, n_entries);
+  else hipLaunchKernelGGL(grad_finish_kernel<false>, dim3(total_work), dim3(NT), 0, st, d_entries, n_entries);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
