@@ -904,6 +904,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_ONLY") = (int)TUNE_WGRAD_MIX_ONLY;
   m.attr("TUNE_WGRAD_MIX_SKIP") = (int)TUNE_WGRAD_MIX_SKIP;
   m.attr("TUNE_WGRAD_MIX_LIST") = (int)TUNE_WGRAD_MIX_LIST;
+  m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;
   m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;

@@ -415,12 +415,33 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
   const int only = cfl_tune(TUNE_WGRAD_MIX_ONLY), skip = cfl_tune(TUNE_WGRAD_MIX_SKIP);
   static bool listed = false;
   const bool list = cfl_tune(TUNE_WGRAD_MIX_LIST) == 1 && !listed;
+  // item order (TUNE_WGRAD_MIX_ORDER): 0 = every halo item first (the longest blocks start first), 1 = the generic
+  // items first, 2 = halo and generic items alternating (the MFMA-heavy long halo blocks and the HBM-heavy generic
+  // ones co-resident from the start)
+  int order[64], no = 0, hl[64], gl[64], nh = 0, ngn = 0;
+  for (int i = 0; i < n && i < 64; ++i) {
+    if (ps[i].algo != 1 && conv3x3_wgrad_supported(ps[i])) hl[nh++] = i;
+    else gl[ngn++] = i;
+  }
+  const int mode = cfl_tune(TUNE_WGRAD_MIX_ORDER);
+  if (mode == 2) {
+    for (int a = 0, b = 0; a < nh || b < ngn;) {
+      if (a < nh) order[no++] = hl[a++];
+      if (b < ngn) order[no++] = gl[b++];
+    }
+  } else {
+    const int* first = mode == 1 ? gl : hl;
+    const int* second = mode == 1 ? hl : gl;
+    const int n1 = mode == 1 ? ngn : nh, n2 = mode == 1 ? nh : ngn;
+    for (int a = 0; a < n1; ++a) order[no++] = first[a];
+    for (int a = 0; a < n2; ++a) order[no++] = second[a];
+  }
   int idx = -1;
-  for (int pass = 0; pass < 2; ++pass)
-    for (int i = 0; i < n; ++i) {
+  for (int oi = 0; oi < no; ++oi) {
+    {
+      const int i = order[oi];
       const WgradParams& p = ps[i];
       const bool halo = p.algo != 1 && conv3x3_wgrad_supported(p);
-      if (halo != (pass == 0)) continue;
       ++idx;
       if ((only > 0 && idx != only - 1) || (idx < 31 && ((skip >> idx) & 1))) continue;   // timing experiments
       if (g.n == MIX_MAX) {
@@ -452,6 +473,7 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
         fprintf(stderr, "[wgrad_mix] item %2d kind %2d B%d %dx%d Cin %d up %d -> %dx%d N %d ks %d s %d: %d blocks\n", idx,
                 it.kind, p.B, p.Hin, p.Win, p.Cin, p.up_in, p.Ho, p.Wo, p.N, p.ks, p.stride, it.gx * it.gy * zs);
     }
+  }
   if (list) listed = true;
   return flush();
 }

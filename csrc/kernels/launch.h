@@ -501,7 +501,8 @@ enum TuneKey {
   TUNE_WGRAD_MIX_ONLY = 42,    // TIMING ONLY (wrong gradients): mixed wgrad launch keeps only item k - 1 (mix order)
   TUNE_WGRAD_MIX_SKIP = 43,    // TIMING ONLY: mixed wgrad launch drops the items of this bit mask (bit k = item k)
   TUNE_WGRAD_MIX_LIST = 44,    // 1: print the mixed launch's items (index, kind, shape, blocks) to stderr once
-  TUNE_N = 45
+  TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = halo items first, 1 = generic first, 2 = alternating
+  TUNE_N = 46
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

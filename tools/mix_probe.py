@@ -64,6 +64,12 @@ C.set_tune(C.TUNE_WGRAD_MIX_LIST, 1)
 full = timeit()
 C.set_tune(C.TUNE_WGRAD_MIX_LIST, 0)
 print(f"whole mixed launch: {full:.1f} us ({len(wq)} deferred wgrads)", flush=True)
+for mode in (1, 2):                                  # item orders (TUNE_WGRAD_MIX_ORDER)
+    C.set_tune(C.TUNE_WGRAD_MIX_ORDER, mode)
+    print(f"  item order {mode}: {timeit():.1f} us", flush=True)
+C.set_tune(C.TUNE_WGRAD_MIX_ORDER, 0)
+if os.environ.get("MIX_ORDER_ONLY"):
+    sys.exit(0)
 n = len(wq)
 for k in range(n):
     C.set_tune(C.TUNE_WGRAD_MIX_ONLY, k + 1)
