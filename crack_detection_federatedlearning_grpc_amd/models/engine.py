@@ -89,9 +89,10 @@ class UNetEngine:
         self.eval_metrics = torch.zeros(10, dtype=torch.float64, device=dev)
         self.idx = torch.zeros(batch, dtype=torch.int32, device=dev)
         # optional device batch table (bind_batches): the step's first kernel selects idx = table[cursor % nb] and
-        # its last advances the cursor, so replayed steps need no host-issued index copy
+        # advances the cursor, so replayed steps need no host-issued index copy
         self.batch_table: Optional[torch.Tensor] = None
         self.batch_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr_buf = torch.zeros(1, dtype=torch.float32, device=dev)    # the step's Adam rate (_zero_step)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         self._build_pack()
         self._alloc()
@@ -669,17 +670,25 @@ class UNetEngine:
                               bwd_sums=bn0["sums"], bwd_reps=self.RS, bwd_dx=D["dy0"],
                               bwd_dgamma=self.G(names[1], "gamma"), bwd_dbeta=self.G(names[1], "beta"))
 
-    def optimizer_step(self) -> None:
+    def optimizer_step(self, advanced: bool = False) -> None:
+        """The fused optimizer tail (opt_step). ``advanced``: the step's zero_spans launch already advanced the
+        step / cursor and left the Adam rate in ``lr_buf`` (the training step's form: no end-of-launch ticket);
+        otherwise opt_step advances them itself (its last block, by ticket)."""
         self._await_all()
         if self._share is not None:
             raise RuntimeError("optimizer_step on an inference-only engine")
+        if advanced:
+            self.C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable,
+                            self.packed, self.lr, self.b1, self.b2, self.adam_eps, self.momentum, None, None, None,
+                            self.lr_buf)
+            return
         cursor = self.batch_cursor if self.batch_table is not None else None
         self.C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
                         self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
 
     def bind_batches(self, batches: torch.Tensor) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
-        ``cursor % nb`` (selected in the step's zero_spans launch, the cursor advanced by its pack launch) instead of
+        ``cursor % nb`` (selected and the cursor advanced by the step's zero_spans launch) instead of
         a host copy into ``idx``. After graph capture the table buffer is fixed (the graph holds its address and
         row count): a table of the same row count is copied in; a smaller one whose row count divides the bound
         one is tiled into it, so ``cursor % nb`` still wraps onto the NEW rows; anything else is refused.
@@ -723,11 +732,14 @@ class UNetEngine:
         self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra)
 
     def _zero_step(self) -> None:
+        """The step's first launch: zero the gradient / statistics spans, select the batch from the bound table,
+        and advance the Adam step (rate into ``lr_buf``) and batch cursor for this step's optimizer_step."""
+        adv = dict(step=self.step_t, lr_buf=self.lr_buf, lr=self.lr, b1=self.b1, b2=self.b2)
         if self.batch_table is not None:
             self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero, self.batch_table, self.batch_cursor,
-                              self.idx)
+                              self.idx, **adv)
         else:
-            self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero)
+            self.C.zero_spans(self.zero_table, self.n_zero, self.max_zero, **adv)
 
     def _check_idx(self) -> None:
         """Host-side range check of a directly written ``idx`` (eager steps / before capture; bound batch tables are
@@ -749,7 +761,7 @@ class UNetEngine:
         self._zero_step()
         self.forward(True)
         self.backward()
-        self.optimizer_step()
+        self.optimizer_step(advanced=True)
 
     # ------------------------------------------------------------------------------------------------ graph
     def capture(self) -> None:

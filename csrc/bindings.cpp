@@ -696,7 +696,7 @@ at::Tensor make_opt_table(std::vector<std::tuple<int, int, int, int, int, int, i
 
 void opt_step_op(at::Tensor table, int n_items, at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
                  at::Tensor trainable, at::Tensor packed, double lr, double b1, double b2, double eps, double momentum,
-                 at::Tensor step, OptT cursor, at::Tensor ticket) {
+                 OptT step, OptT cursor, OptT ticket, OptT lr_buf) {
   TORCH_CHECK(table.numel() == (int64_t)n_items * (int64_t)sizeof(OptItem), "opt_step: table size");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel() &&
               trainable.numel() == p.numel(), "opt_step sizes");
@@ -710,9 +710,12 @@ void opt_step_op(at::Tensor table, int n_items, at::Tensor p, at::Tensor g, at::
   o.items = ptr<const OptItem>(table, "table");
   o.n_items = n_items;
   o.lr = (float)lr; o.b1 = (float)b1; o.b2 = (float)b2; o.eps = (float)eps; o.momentum = (float)momentum;
-  o.step = ptr<int>(step, "step");
+  o.step = optr<int>(step, "step");
   o.cursor = optr<int>(cursor, "cursor");
-  o.ticket = ptr<int>(ticket, "ticket");
+  o.ticket = optr<int>(ticket, "ticket");
+  o.lr_t = optr<const float>(lr_buf, "lr_buf");
+  TORCH_CHECK(lr_buf ? !step && !cursor : step && ticket,
+              "opt_step: either step + ticket (+ cursor), or lr_buf alone (zero_spans advanced the step)");
   ok(opt_step(o, stream()), "opt_step");
 }
 
@@ -763,7 +766,8 @@ at::Tensor make_zero_table(std::vector<at::Tensor> spans) {
   return cpu.to(spans.at(0).device());
 }
 
-void zero_spans_op(at::Tensor table, int n, int64_t max_bytes, OptT batches, OptT cursor, OptT idx) {
+void zero_spans_op(at::Tensor table, int n, int64_t max_bytes, OptT batches, OptT cursor, OptT idx, OptT step,
+                   OptT lr_buf, double lr, double b1, double b2) {
   TORCH_CHECK(table.numel() == (int64_t)n * (int64_t)sizeof(ZeroSpan), "zero_spans: table size");
   BatchSelect bs{};
   if (batches) {
@@ -771,12 +775,20 @@ void zero_spans_op(at::Tensor table, int n, int64_t max_bytes, OptT batches, Opt
                 batches->scalar_type() == at::kInt && idx->scalar_type() == at::kInt && cursor->numel() >= 1,
                 "zero_spans: batches [nb][B] int32 with cursor and idx [B]");
     bs.table = ptr<const int32_t>(*batches, "batches");
-    bs.cursor = ptr<const int>(*cursor, "cursor");
+    bs.cursor = ptr<int>(*cursor, "cursor");
     bs.idx = ptr<int32_t>(*idx, "idx");
     bs.B = (int)idx->numel();
     bs.nb = (int)batches->size(0);
   }
-  ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream(), bs), "zero_spans");
+  StepAdvance adv{};
+  if (step) {
+    TORCH_CHECK(lr_buf && lr_buf->numel() >= 1 && lr_buf->scalar_type() == at::kFloat && step->numel() >= 1 &&
+                step->scalar_type() == at::kInt, "zero_spans: step advance needs int32 step and float32 lr_buf");
+    adv.step = ptr<int>(*step, "step");
+    adv.lr_t = ptr<float>(*lr_buf, "lr_buf");
+    adv.lr = (float)lr; adv.b1 = (float)b1; adv.b2 = (float)b2;
+  }
+  ok(zero_spans(ptr<const ZeroSpan>(table, "table"), n, max_bytes, stream(), bs, adv), "zero_spans");
 }
 
 // src: uint8 device bytes of n decoded images back to back; offs: int64 [n] byte offsets; dims: int32 [n, 2] (h, w);
@@ -882,7 +894,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_finish", &grad_finish_op);
   m.def("make_zero_table", &make_zero_table);
   m.def("zero_spans", &zero_spans_op, py::arg("table"), py::arg("n"), py::arg("max_bytes"),
-        py::arg("batches") = py::none(), py::arg("cursor") = py::none(), py::arg("idx") = py::none());
+        py::arg("batches") = py::none(), py::arg("cursor") = py::none(), py::arg("idx") = py::none(),
+        py::arg("step") = py::none(), py::arg("lr_buf") = py::none(), py::arg("lr") = 0.0, py::arg("b1") = 0.0,
+        py::arg("b2") = 0.0);
   m.def("set_tune", &cfl_set_tune);
   m.attr("GF_REDUCE") = (int)GF_REDUCE;
   m.attr("GF_COPY") = (int)GF_COPY;
@@ -905,6 +919,9 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_SKIP") = (int)TUNE_WGRAD_MIX_SKIP;
   m.attr("TUNE_WGRAD_MIX_LIST") = (int)TUNE_WGRAD_MIX_LIST;
   m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
+  m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
+  m.attr("TUNE_HEAD_BLOCKS") = (int)TUNE_HEAD_BLOCKS;
+  m.attr("TUNE_OPT_NO_TICKET") = (int)TUNE_OPT_NO_TICKET;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;
   m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;
@@ -955,7 +972,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("make_opt_table", &make_opt_table);
   m.def("opt_step", &opt_step_op, py::arg("table"), py::arg("n_items"), py::arg("p"), py::arg("g"), py::arg("m"),
         py::arg("v"), py::arg("trainable"), py::arg("packed"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
-        py::arg("eps"), py::arg("momentum"), py::arg("step"), py::arg("cursor"), py::arg("ticket"));
+        py::arg("eps"), py::arg("momentum"), py::arg("step"), py::arg("cursor"), py::arg("ticket"),
+        py::arg("lr_buf") = py::none());
   m.attr("OI_FLAT") = (int)OI_FLAT;
   m.attr("OI_TILE") = (int)OI_TILE;
   m.def("render_cracks", &render_cracks_op);

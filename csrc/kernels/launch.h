@@ -414,6 +414,8 @@ struct OptParams {
   int* step;
   int* cursor;             // nullable
   int* ticket;             // one int, zero between launches
+  const float* lr_t;       // nullable: the step's Adam rate, computed by its zero_spans launch (StepAdvance), which
+                           // also advanced the step and cursor - then step / cursor / ticket are unused (no ticket)
 };
 int opt_step(const OptParams& p, hipStream_t st);
 
@@ -441,16 +443,25 @@ struct ZeroSpan {
   int64_t bytes;           // multiple of 16
 };
 // batch: optionally also selects the step's dataset indices on the device, idx[0..B) = table[(*cursor) % nb]
-// (a batch table bound once per epoch; the cursor is advanced by pack_weights at the end of the step), so the
-// replayed step needs no host-issued index copy
+// (a batch table bound once per epoch; the cursor is advanced by this launch's StepAdvance, or else by opt_step /
+// pack_weights at the end of the step), so the replayed step needs no host-issued index copy
 struct BatchSelect {
   const int32_t* table;    // [nb][B] or nullptr
-  const int* cursor;
+  int* cursor;
   int32_t* idx;
   int B, nb;
 };
+// step: optionally advances the training step at its START (the engine's fused step): lr_t = the Adam rate of step
+// *step + 1 (the formula opt_step uses), then *step += 1 and, with a batch table, *cursor += 1 after the batch
+// select - so opt_step reads lr_t and needs no end-of-launch ticket (which kept every one of its blocks alive for a
+// device-scope atomic round trip: 4 us of the step, profiles/README.md)
+struct StepAdvance {
+  int* step;               // nullptr: nothing advanced
+  float* lr_t;
+  float lr, b1, b2;
+};
 int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st,
-               BatchSelect batch = BatchSelect{});
+               BatchSelect batch = BatchSelect{}, StepAdvance adv = StepAdvance{});
 
 // launch-shape tuning knobs (0 = built-in heuristic), set from Python for micro-benchmark sweeps
 enum TuneKey {
@@ -502,7 +513,9 @@ enum TuneKey {
   TUNE_WGRAD_MIX_SKIP = 43,    // TIMING ONLY: mixed wgrad launch drops the items of this bit mask (bit k = item k)
   TUNE_WGRAD_MIX_LIST = 44,    // 1: print the mixed launch's items (index, kind, shape, blocks) to stderr once
   TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = halo items first, 1 = generic first, 2 = alternating
-  TUNE_N = 46
+  TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
+  TUNE_OPT_NO_TICKET = 47,     // TIMING ONLY (the Adam step / batch cursor stop advancing): opt_step without its ticket
+  TUNE_N = 48
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

@@ -26,6 +26,11 @@ CFL_DEVICE float adam_lr(const int* step, float lr, float b1, float b2) {
   return lr * sqrtf(1.f - powf(b2, (float)t)) / (1.f - powf(b1, (float)t));
 }
 
+// opt_step's rate: computed by the step's zero_spans launch (StepAdvance), else from the step counter
+CFL_DEVICE float step_lr(const OptParams& p) {
+  return p.lr_t != nullptr ? *p.lr_t : adam_lr(p.step, p.lr, p.b1, p.b2);
+}
+
 __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
   const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
   const int64_t n4 = p.n / 4;
@@ -124,8 +129,14 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
 // stores that depend on it, i.e. before the block's closing barrier and the ticket atomic after it, so the last block
 // advances the step only after every read of it. The ticket is RELAXED: the ordering it needs is that of loads whose
 // values were already consumed, and nothing the blocks stored is read by the last block (an agent-scope release made
-// every block write back its XCD's L2 before retiring).
-__global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
+// every block write back its XCD's L2 before retiring). With p.lr_t (the engine's training step) the step's
+// zero_spans launch already computed the rate and advanced the step / cursor: no ticket.
+//
+// VEC: a tile whose row length, offsets and row maps are multiples of 4 elements (every GEMM weight of the model)
+// is moved in 16-byte fp32 / 8-byte bf16 pieces - a quarter of the memory instructions of the per-column form.
+// no_ticket (TIMING ONLY, TUNE_OPT_NO_TICKET): the step / cursor are not advanced.
+template <bool VEC>
+__global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p, int no_ticket) {
   const OptItem it = p.items[blockIdx.x];
   const int tid = threadIdx.x;
   __shared__ float tl[64][65];
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
       it.mvar[c] = it.mvar[c] * mom + unbiased * (1.f - mom);
     }
   } else if (it.kind == OI_FLAT) {
-    const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
+    const float lr_t = step_lr(p);
     float w[4], g[4], m[4], v[4];
     bool on[4];
 #pragma unroll
@@ -176,9 +187,62 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
       p.m[e] = m[u];
       p.v[e] = v[u];
     }
+  } else if (VEC && ((it.cols | it.rows | (int)it.src | it.s1 | it.s2 | it.base2 | (int)it.dst_t | (int)it.dst_b) &
+                     3) == 0) {
+    // 64x64 tile, thread (cq, rt) owns columns c0 + 4cq .. + 3 of rows r0 + rt + 16j: float4 loads / stores of the
+    // fp32 arrays, 4 bf16 (8 bytes) per store of both views (the transpose through LDS: thread (rq, cc) writes rows
+    // r0 + 4rq .. + 3 of column cc). Both LDS passes hit 64 distinct banks per wave (row stride 65).
+    const float lr_t = step_lr(p);
+    const int cq = tid & 15, rt = tid >> 4, c = it.c0 + 4 * cq;
+    const bool cok = c < it.cols;                       // cols % 4 == 0: the whole quad is in range
+    float4 w[4], g[4], m[4], v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = it.r0 + rt + 16 * j;
+      // out-of-tile lanes load the tile's first quad (a select of the address, not of a pointer to a zero
+      // constant: that made the compiler stage the constant in scratch and use flat loads); their values are unused
+      const int64_t e = (cok && r < it.rows) ? it.src + (int64_t)r * it.cols + c : it.src;
+      w[j] = *reinterpret_cast<const float4*>(p.p + e);
+      g[j] = *reinterpret_cast<const float4*>(p.g + e);
+      m[j] = *reinterpret_cast<const float4*>(p.m + e);
+      v[j] = *reinterpret_cast<const float4*>(p.v + e);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = it.r0 + rt + 16 * j;
+      if (cok && r < it.rows) {
+        adam_elem(w[j].x, g[j].x, m[j].x, v[j].x, lr_t, p.b1, p.b2, p.eps);
+        adam_elem(w[j].y, g[j].y, m[j].y, v[j].y, lr_t, p.b1, p.b2, p.eps);
+        adam_elem(w[j].z, g[j].z, m[j].z, v[j].z, lr_t, p.b1, p.b2, p.eps);
+        adam_elem(w[j].w, g[j].w, m[j].w, v[j].w, lr_t, p.b1, p.b2, p.eps);
+        const int64_t e = it.src + (int64_t)r * it.cols + c;
+        *reinterpret_cast<float4*>(p.p + e) = w[j];
+        *reinterpret_cast<float4*>(p.m + e) = m[j];
+        *reinterpret_cast<float4*>(p.v + e) = v[j];
+        const uint2 b = make_uint2(pack2bf(w[j].x, w[j].y), pack2bf(w[j].z, w[j].w));
+        *reinterpret_cast<uint2*>(p.packed + it.dst_b + (int64_t)(r % it.q) * it.s1 + (int64_t)(r / it.q) * it.s2 +
+                                  it.base2 + c) = b;
+      }
+      float* row = &tl[rt + 16 * j][4 * cq];
+      row[0] = w[j].x;
+      row[1] = w[j].y;
+      row[2] = w[j].z;
+      row[3] = w[j].w;
+    }
+    __syncthreads();
+    const int rq = tid & 15, r = it.r0 + 4 * rq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ccl = (tid >> 4) + 16 * j, cc = it.c0 + ccl;
+      if (cc < it.cols && r < it.rows) {                 // rows % 4 == 0: the whole quad is in range
+        const uint2 b = make_uint2(pack2bf(tl[4 * rq][ccl], tl[4 * rq + 1][ccl]),
+                                   pack2bf(tl[4 * rq + 2][ccl], tl[4 * rq + 3][ccl]));
+        *reinterpret_cast<uint2*>(p.packed + it.dst_t + (int64_t)cc * it.rows + r) = b;
+      }
+    }
   } else {
     // 64x64 tile, thread (tx, ty) owns column c0 + tx of rows r0 + ty + 4j: coalesced 256-B rows of every fp32 array
-    const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
+    const float lr_t = step_lr(p);
     const int tx = tid & 63, ty = tid >> 6, c = it.c0 + tx;
     const int64_t base = it.src;
     float w[16], g[16], m[16], v[16];
@@ -213,7 +277,7 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (tid == 0 && !no_ticket && p.lr_t == nullptr) {
     const int t = __hip_atomic_fetch_add(p.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {                      // every block has read the step: advance it
       *p.ticket = 0;
@@ -347,10 +411,20 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
   }
 }
 
-__global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs) {
-  if (bs.table != nullptr && blockIdx.x == 0 && blockIdx.y == 0) {   // any batch size (the 512^2 plan: ~1,100)
-    const size_t row = (size_t)(*bs.cursor % bs.nb) * bs.B;
-    for (int i = threadIdx.x; i < bs.B; i += NT) bs.idx[i] = bs.table[row + i];
+__global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs, StepAdvance adv) {
+  if (blockIdx.x == 0 && blockIdx.y == 0) {            // block-uniform: the barrier is safe
+    if (bs.table != nullptr) {                         // any batch size (the 512^2 plan: ~1,100)
+      const size_t row = (size_t)(*bs.cursor % bs.nb) * bs.B;
+      for (int i = threadIdx.x; i < bs.B; i += NT) bs.idx[i] = bs.table[row + i];
+    }
+    if (adv.step != nullptr) {
+      __syncthreads();                                 // every thread has read the cursor
+      if (threadIdx.x == 0) {
+        *adv.lr_t = adam_lr(adv.step, adv.lr, adv.b1, adv.b2);
+        *adv.step += 1;
+        if (bs.table != nullptr) *bs.cursor += 1;
+      }
+    }
   }
   const ZeroSpan z = spans[blockIdx.y];
   uint4* p = reinterpret_cast<uint4*>(z.p);
@@ -402,13 +476,15 @@ int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipS
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st, BatchSelect batch) {
+int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st, BatchSelect batch,
+               StepAdvance adv) {
   if (n_spans <= 0) return 0;
   if (batch.table != nullptr && (batch.B < 1 || batch.nb < 1)) return 1;
+  if (adv.step != nullptr && adv.lr_t == nullptr) return 1;
   int64_t bx = (max_bytes / 16 + NT - 1) / NT;
   if (bx > 1024) bx = 1024;
   if (bx < 1) bx = 1;
-  hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans, batch);
+  hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans, batch, adv);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -434,8 +510,10 @@ int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int
 }
 
 int opt_step(const OptParams& p, hipStream_t st) {
-  if (p.n_items <= 0 || !p.ticket || !p.step) return 1;
-  hipLaunchKernelGGL(opt_step_kernel, dim3(p.n_items), dim3(NT), 0, st, p);
+  if (p.n_items <= 0 || (!p.lr_t && (!p.ticket || !p.step)) || (p.lr_t && (p.step || p.cursor))) return 1;
+  const int nt = cfl_tune(TUNE_OPT_NO_TICKET);
+  if (cfl_tune(TUNE_OPT_SCALAR)) hipLaunchKernelGGL(opt_step_kernel<false>, dim3(p.n_items), dim3(NT), 0, st, p, nt);
+  else hipLaunchKernelGGL(opt_step_kernel<true>, dim3(p.n_items), dim3(NT), 0, st, p, nt);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

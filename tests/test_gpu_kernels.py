@@ -492,10 +492,20 @@ def test_opt_step_adam_magnitude_matches_keras_adam():
     assert int(eng.step_t.item()) == 3
 
 
-def test_fused_opt_step_matches_adam_moving_pack():
+@pytest.mark.parametrize("scalar", [0, 1])
+def test_fused_opt_step_matches_adam_moving_pack(scalar):
     """opt_step (one launch: Adam tiles writing both bf16 views, flat Adam items, BN moving items, step / cursor
-    advance by the last block) vs adam_update + bn_moving_update + pack_weights on the same random state."""
+    advance by the last block) vs adam_update + bn_moving_update + pack_weights on the same random state; both tile
+    forms (16-byte default, per-column TUNE_OPT_SCALAR)."""
     table, eng, flat, x, y = _engine_and_ref(S=64, B=2, seed=6)
+    eng.C.set_tune(eng.C.TUNE_OPT_SCALAR, scalar)
+    try:
+        _opt_step_vs_unfused(table, eng)
+    finally:
+        eng.C.set_tune(eng.C.TUNE_OPT_SCALAR, 0)
+
+
+def _opt_step_vs_unfused(table, eng):
     gen = torch.Generator(device="cpu").manual_seed(3)
     n = table.total
     eng.bind_batches(torch.zeros(4, 2, dtype=torch.int32))
@@ -1945,12 +1955,25 @@ def test_zero_spans_batch_select_any_batch_size(B):
     torch.cuda.synchronize()
     assert torch.equal(idx.cpu(), tab[4 % nb].cpu())
     assert float(buf.abs().sum()) == 0.0
+    assert int(cursor.item()) == 4                      # no step advance requested: the cursor stays
+    # with the step advance (the engine's training step): the batch of the OLD cursor, then step / cursor + 1 and
+    # the Adam rate of the new step in lr_buf (Keras form, the formula opt_step uses)
+    step = torch.tensor([6], dtype=torch.int32, device=DEV)
+    lr_buf = torch.zeros(1, device=DEV)
+    idx.fill_(-1)
+    C_.zero_spans(zt, 1, buf.numel() * 4, tab, cursor, idx, step=step, lr_buf=lr_buf, lr=1e-3, b1=0.9, b2=0.999)
+    torch.cuda.synchronize()
+    assert torch.equal(idx.cpu(), tab[4 % nb].cpu())
+    assert int(cursor.item()) == 5 and int(step.item()) == 7
+    t = 7.0
+    want = 1e-3 * (1.0 - 0.999 ** t) ** 0.5 / (1.0 - 0.9 ** t)
+    assert abs(float(lr_buf.item()) - want) <= 1e-4 * want    # fp32 1 - b2^t cancels ~3 digits at small t
 
 
 def test_engine_device_batch_table_selects_and_advances():
     """UNetEngine.bind_batches: each training step (eager or graph-replayed) takes its dataset indices from row
-    cursor % nb of the bound table - selected by the step's zero_spans launch, the cursor advanced by its pack launch
-    - and trains exactly like the host-copied idx path."""
+    cursor % nb of the bound table - selected and the cursor advanced by the step's zero_spans launch - and trains
+    exactly like the host-copied idx path."""
     table, eng, flat, x, y = _engine_and_ref(seed=3)
     B = eng.B
     tab = torch.tensor([[(3 * r + j) % 8 for j in range(B)] for r in range(3)], dtype=torch.int32)
@@ -1966,6 +1989,7 @@ def test_engine_device_batch_table_selects_and_advances():
     eng.train_step(use_graph=True)          # wraps to row 0
     torch.cuda.synchronize()
     assert torch.equal(eng.idx.cpu(), tab[0])
+    assert int(eng.step_t.item()) == 4      # one Adam step per training step (advanced by zero_spans)
     after_table = eng.get_flat()
     # the same four steps through host-copied indices
     _, eng2, *_ = _engine_and_ref(seed=3)
