@@ -415,15 +415,15 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
   const int only = cfl_tune(TUNE_WGRAD_MIX_ONLY), skip = cfl_tune(TUNE_WGRAD_MIX_SKIP);
   static bool listed = false;
   const bool list = cfl_tune(TUNE_WGRAD_MIX_LIST) == 1 && !listed;
-  // item order (TUNE_WGRAD_MIX_ORDER): 0 = every halo item first (the longest blocks start first), 1 = the generic
-  // items first, 2 = halo and generic items alternating (the MFMA-heavy long halo blocks and the HBM-heavy generic
-  // ones co-resident from the start)
+  // item order (TUNE_WGRAD_MIX_ORDER): 2 (default) = halo and generic items alternating (the MFMA-heavy long halo
+  // blocks and the HBM-heavy generic ones co-resident from the start: 155 vs 160 us per launch, two trace A/Bs), 3 =
+  // every halo item first (the longest blocks start first), 1 = the generic items first (202 us)
   int order[64], no = 0, hl[64], gl[64], nh = 0, ngn = 0;
   for (int i = 0; i < n && i < 64; ++i) {
     if (ps[i].algo != 1 && conv3x3_wgrad_supported(ps[i])) hl[nh++] = i;
     else gl[ngn++] = i;
   }
-  const int mode = cfl_tune(TUNE_WGRAD_MIX_ORDER);
+  const int mode = cfl_tune(TUNE_WGRAD_MIX_ORDER) > 0 ? cfl_tune(TUNE_WGRAD_MIX_ORDER) : 2;
   if (mode == 2) {
     for (int a = 0, b = 0; a < nh || b < ngn;) {
       if (a < nh) order[no++] = hl[a++];

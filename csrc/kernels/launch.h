@@ -512,7 +512,8 @@ enum TuneKey {
   TUNE_WGRAD_MIX_ONLY = 42,    // TIMING ONLY (wrong gradients): mixed wgrad launch keeps only item k - 1 (mix order)
   TUNE_WGRAD_MIX_SKIP = 43,    // TIMING ONLY: mixed wgrad launch drops the items of this bit mask (bit k = item k)
   TUNE_WGRAD_MIX_LIST = 44,    // 1: print the mixed launch's items (index, kind, shape, blocks) to stderr once
-  TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = halo items first, 1 = generic first, 2 = alternating
+  TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = default (2), 1 = generic first, 2 = alternating,
+                               //   3 = halo items first
   TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
   TUNE_OPT_NO_TICKET = 47,     // TIMING ONLY (the Adam step / batch cursor stop advancing): opt_step without its ticket
   TUNE_N = 48

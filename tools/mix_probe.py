@@ -64,7 +64,7 @@ C.set_tune(C.TUNE_WGRAD_MIX_LIST, 1)
 full = timeit()
 C.set_tune(C.TUNE_WGRAD_MIX_LIST, 0)
 print(f"whole mixed launch: {full:.1f} us ({len(wq)} deferred wgrads)", flush=True)
-for mode in (1, 2):                                  # item orders (TUNE_WGRAD_MIX_ORDER)
+for mode in (1, 3):                                  # other item orders (TUNE_WGRAD_MIX_ORDER; default 2)
     C.set_tune(C.TUNE_WGRAD_MIX_ORDER, mode)
     print(f"  item order {mode}: {timeit():.1f} us", flush=True)
 C.set_tune(C.TUNE_WGRAD_MIX_ORDER, 0)
