@@ -496,9 +496,12 @@ bool conv3x3_sk_eligible(const ConvParams& p) {
   // default: the 8-chunk (Cin = 256) convs of the <= 32^2 levels without the decoder node join. In-step per-position
   // trace A/B (tools/gpu_trace_ab.sh, 256^2 / b16): those five calls 1.5-1.9 / 0.3-0.4 us faster each; the Cin = 128
   // calls -0.1 .. +2.4 us and the node-join form +9.7 us (its join loads wait in front of the K loop), so not those.
+  // Only at small M (<= 128k output pixels): at the 512^2 planned batch (1,096 images, M = 1.1M at 32^2) the four
+  // such calls ran 2,627 / 2,742 us vs 1,732 / 1,898 us for the whole-chunk 8x16 kernel (profiles/r4_512) - with
+  // that many tiles the in-block split of K only costs.
   // 3 = every low-resolution candidate (maps <= 32^2, Cin >= 128), 4 = 16^2 maps and 32^2 maps with N <= 128 (A/B).
   const bool low = p.Cin >= 128 && p.Ho * p.Wo <= 32 * 32;
-  if (v == 0) return p.Cin == 256 && p.Ho * p.Wo <= 32 * 32 && !p.pj.v;
+  if (v == 0) return p.Cin == 256 && p.Ho * p.Wo <= 32 * 32 && (int64_t)p.B * p.Ho * p.Wo <= (1 << 17) && !p.pj.v;
   return v == 2 || (v == 3 && low) || (v == 4 && low && (p.Ho * p.Wo <= 16 * 16 || p.N <= 128));
 }
 
