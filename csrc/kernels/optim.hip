@@ -381,6 +381,33 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
     }
     return;
   }
+  if (ngroups == 1) {
+    // single row group (no atomics into dst): thread t owns the 4 consecutive elements 4t .. 4t+3 of the tile, so
+    // every row is one 16-byte load per lane (n % 4 == 0 and 16-byte aligned rows, make_grad_finish_table). The
+    // table's pointers are cast to the global address space: as generic pointers they compiled to flat loads.
+    typedef f4v __attribute__((address_space(1))) gf4;
+    const int i = tile * 4 * NT + 4 * threadIdx.x;
+    if (i >= g.n) return;
+    gf4* src = (gf4*)(g.src + i);
+    gf4* dst = (gf4*)(g.dst + i);
+    const int n4 = g.n >> 2;
+    f4v v[GF_ROWS];
+#pragma unroll
+    for (int r = 0; r < GF_ROWS; ++r) {
+      if (r < rows) v[r] = src[(size_t)r * n4];
+      else v[r] = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < GF_ROWS; ++r) s += v[r];   // the same row order as the per-element form: identical sums
+    if (g.mode == GF_REDUCE) {
+#pragma unroll
+      for (int r = 0; r < GF_ROWS; ++r)
+        if (r < rows) src[(size_t)r * n4] = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+    *dst = *dst + s;
+    return;
+  }
   const int r0 = rg * GF_ROWS;
   float v[GF_ROWS][4];
 #pragma unroll
