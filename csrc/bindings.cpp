@@ -898,6 +898,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("step") = py::none(), py::arg("lr_buf") = py::none(), py::arg("lr") = 0.0, py::arg("b1") = 0.0,
         py::arg("b2") = 0.0);
   m.def("set_tune", &cfl_set_tune);
+  m.def("get_tune", &cfl_tune);
   m.attr("GF_REDUCE") = (int)GF_REDUCE;
   m.attr("GF_COPY") = (int)GF_COPY;
   m.attr("TUNE_NODE_BWD_BLOCKS") = (int)TUNE_NODE_BWD_BLOCKS;

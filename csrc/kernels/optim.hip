@@ -438,6 +438,8 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
   }
 }
 
+constexpr int ZS_CHUNK = 4 * NT;   // zero_spans: 16-byte stores per block per chunk
+
 __global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs, StepAdvance adv) {
   if (blockIdx.x == 0 && blockIdx.y == 0) {            // block-uniform: the barrier is safe
     if (bs.table != nullptr) {                         // any batch size (the 512^2 plan: ~1,100)
@@ -453,11 +455,19 @@ __global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelec
       }
     }
   }
+  // block x of span y zeroes the 16-KB chunks x, x + gridDim.x, ...: four 16-byte stores per thread per chunk, issued
+  // back to back, through a global-address-space pointer (the table's generic pointer compiled to flat stores)
+  typedef u4v __attribute__((address_space(1))) gu4;
   const ZeroSpan z = spans[blockIdx.y];
-  uint4* p = reinterpret_cast<uint4*>(z.p);
+  gu4* p = (gu4*)z.p;
   const int64_t n = z.bytes >> 4;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
-    p[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t c = (int64_t)blockIdx.x * ZS_CHUNK; c < n; c += (int64_t)gridDim.x * ZS_CHUNK) {
+#pragma unroll
+    for (int u = 0; u < ZS_CHUNK / NT; ++u) {
+      const int64_t i = c + u * NT + threadIdx.x;
+      if (i < n) p[i] = u4v{0u, 0u, 0u, 0u};
+    }
+  }
 }
 
 int g_tune[TUNE_N] = {0};
@@ -508,7 +518,7 @@ int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStrea
   if (n_spans <= 0) return 0;
   if (batch.table != nullptr && (batch.B < 1 || batch.nb < 1)) return 1;
   if (adv.step != nullptr && adv.lr_t == nullptr) return 1;
-  int64_t bx = (max_bytes / 16 + NT - 1) / NT;
+  int64_t bx = (max_bytes / 16 + ZS_CHUNK - 1) / ZS_CHUNK;   // one chunk per block for spans up to 16 MB
   if (bx > 1024) bx = 1024;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(zero_spans_kernel, dim3((int)bx, n_spans), dim3(NT), 0, st, d_spans, batch, adv);
