@@ -515,7 +515,7 @@ int grad_finish(const GradFinish* d_entries, int n_entries, int total_work, hipS
 
 int zero_spans(const ZeroSpan* d_spans, int n_spans, int64_t max_bytes, hipStream_t st, BatchSelect batch,
                StepAdvance adv) {
-  if (n_spans <= 0) return 0;
+  if (n_spans <= 0) return batch.table != nullptr || adv.step != nullptr ? 1 : 0;   // nothing to launch them with
   if (batch.table != nullptr && (batch.B < 1 || batch.nb < 1)) return 1;
   if (adv.step != nullptr && adv.lr_t == nullptr) return 1;
   int64_t bx = (max_bytes / 16 + ZS_CHUNK - 1) / ZS_CHUNK;   // one chunk per block for spans up to 16 MB
