@@ -80,6 +80,8 @@ class FLConfig:
     device: str = "auto"                 # auto | cpu | cuda
     dtype: str = "bf16"                  # activation dtype on the GPU path (fp32 master weights)
     use_graph: bool = True               # capture the train step in a hipGraph
+    deterministic: bool = False          # int64 fixed-point cross-block reductions: bitwise-reproducible local
+                                         # training (models/engine.py; ~1.4-2.7 % slower, profiles/README.md)
 
     # --- data ------------------------------------------------------------------------------------
     data: str = "synthetic"              # synthetic | folder

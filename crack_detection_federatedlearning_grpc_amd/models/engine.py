@@ -983,7 +983,8 @@ class HipBackend:
         self.cfg = cfg
         self.table = table
         self.eng = UNetEngine(table, cfg.batch_size, data.img_size, "cuda", cfg.loss, cfg.lr, cfg.beta1, cfg.beta2,
-                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps)
+                              cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps,
+                              deterministic=True if getattr(cfg, "deterministic", False) else None)
         images = data.images if isinstance(data.images, torch.Tensor) else torch.as_tensor(data.images)
         masks = data.masks if isinstance(data.masks, torch.Tensor) else torch.as_tensor(data.masks)
         self.eng.bind_data(images.to(self.eng.dev), masks.to(self.eng.dev))

@@ -57,3 +57,13 @@ def test_preset_512_uses_planner():
     from crack_detection_federatedlearning_grpc_amd.train.factory import planned_batch
     b = planned_batch(cfg, "cpu")
     assert b >= 64 and M.largest_tensor_elems(b, 512) <= M.MAX_ELEMS
+
+
+def test_deterministic_flag_parses(monkeypatch):
+    """--deterministic / FL_DETERMINISTIC select the engine's deterministic reduction mode for the FL product path
+    (models/engine.py HipBackend passes it to UNetEngine)."""
+    from crack_detection_federatedlearning_grpc_amd.config import parse
+    assert parse([]).deterministic is False
+    assert parse(["--deterministic"]).deterministic is True
+    monkeypatch.setenv("FL_DETERMINISTIC", "1")
+    assert parse([]).deterministic is True
