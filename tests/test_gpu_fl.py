@@ -176,3 +176,32 @@ def test_server_evaluator_uses_the_clients_held_out_split():
     want = client.backend.eval_batches(epoch_batches(client.data.val_idx, 4, 0, 0))
     assert np.isclose(got["loss"], want["loss"], rtol=1e-6) and np.isclose(got["accuracy"], want["accuracy"])
     assert 0 < got["loss"] < 10
+
+
+def test_deterministic_local_round_is_bitwise_reproducible():
+    """cfg.deterministic (--deterministic / FL_DETERMINISTIC): a client's local round (fresh Adam, epochs of
+    graph-replayed steps, validation) from the same global weights gives the bit-identical model twice - what a
+    bitwise-reproducible FL round needs from the trainer (the aggregation is a fixed-order weighted sum)."""
+    from crack_detection_federatedlearning_grpc_amd import config as C
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.train.factory import make_trainer
+    cfg = C.from_args(None, preset="gpu1-256", img_size=64, batch_size=4, synthetic_samples=48, val_samples=16,
+                      epochs=2, steps_per_epoch=5, data_seed=2, device="cuda", deterministic=True,
+                      predict_round=99)
+    table = ParamTable()
+    start = table.init_flat(9)
+    try:
+        client = make_trainer(cfg, "c0", 0, table=table, device="cuda")
+        assert client.backend.eng.det
+        outs = []
+        for _ in range(2):
+            client.backend.set_flat(start)
+            m = client.train_round(1)
+            outs.append((client.backend.get_flat().copy(), m["loss"], m["val_loss"]))
+        (f0, l0, v0), (f1, l1, v1) = outs
+        assert np.abs(f0 - start).max() > 1e-4                     # it trained
+        assert np.array_equal(f0, f1), int((f0 != f1).sum())
+        # (the loss / accuracy sums are double atomics outside the mode: equal to double rounding)
+        assert np.isclose(l0, l1, rtol=1e-9) and np.isclose(v0, v1, rtol=1e-9)
+    finally:
+        client.backend.eng.C.set_det(0)
