@@ -922,7 +922,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
   m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
   m.attr("TUNE_HEAD_BLOCKS") = (int)TUNE_HEAD_BLOCKS;
-  m.attr("TUNE_OPT_NO_TICKET") = (int)TUNE_OPT_NO_TICKET;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;
   m.attr("TUNE_WGRAD1_BLOCKS") = (int)TUNE_WGRAD1_BLOCKS;

@@ -515,7 +515,7 @@ enum TuneKey {
   TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = default (2), 1 = generic first, 2 = alternating,
                                //   3 = halo items first
   TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
-  TUNE_OPT_NO_TICKET = 47,     // TIMING ONLY (the Adam step / batch cursor stop advancing): opt_step without its ticket
+  // 47: retired (opt_step timing knob without its ticket; the training step no longer uses the ticket)
   TUNE_N = 48
 };
 int cfl_tune(int key);

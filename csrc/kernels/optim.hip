@@ -134,9 +134,8 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
 //
 // VEC: a tile whose row length, offsets and row maps are multiples of 4 elements (every GEMM weight of the model)
 // is moved in 16-byte fp32 / 8-byte bf16 pieces - a quarter of the memory instructions of the per-column form.
-// no_ticket (TIMING ONLY, TUNE_OPT_NO_TICKET): the step / cursor are not advanced.
 template <bool VEC>
-__global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p, int no_ticket) {
+__global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
   const OptItem it = p.items[blockIdx.x];
   const int tid = threadIdx.x;
   __shared__ float tl[64][65];
@@ -277,7 +276,7 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p, int no_
     }
   }
   __syncthreads();
-  if (tid == 0 && !no_ticket && p.lr_t == nullptr) {
+  if (tid == 0 && p.lr_t == nullptr) {
     const int t = __hip_atomic_fetch_add(p.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {                      // every block has read the step: advance it
       *p.ticket = 0;
@@ -548,9 +547,8 @@ int pack_weights(const float* flat, bf16_t* packed, const PackView* d_views, int
 
 int opt_step(const OptParams& p, hipStream_t st) {
   if (p.n_items <= 0 || (!p.lr_t && (!p.ticket || !p.step)) || (p.lr_t && (p.step || p.cursor))) return 1;
-  const int nt = cfl_tune(TUNE_OPT_NO_TICKET);
-  if (cfl_tune(TUNE_OPT_SCALAR)) hipLaunchKernelGGL(opt_step_kernel<false>, dim3(p.n_items), dim3(NT), 0, st, p, nt);
-  else hipLaunchKernelGGL(opt_step_kernel<true>, dim3(p.n_items), dim3(NT), 0, st, p, nt);
+  if (cfl_tune(TUNE_OPT_SCALAR)) hipLaunchKernelGGL(opt_step_kernel<false>, dim3(p.n_items), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL(opt_step_kernel<true>, dim3(p.n_items), dim3(NT), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
