@@ -337,46 +337,58 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
     return;
   }
   if constexpr (DET) {              // one group per tile, every row in order: no atomics into dst
-    constexpr int GF_DROWS = 4;     // rows per load round (int64 rows: 16 would need ~250 VGPRs)
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    long long q[4] = {0, 0, 0, 0};
-    for (int r0 = 0; r0 < rows; r0 += GF_DROWS) {
-      if (g.mode == GF_REDUCE) {    // int64 fixed-point rows (exact in any order), re-zeroed
-        long long v[GF_DROWS][4];
+    // thread t owns the 4 consecutive elements 4t .. 4t+3 of the tile (n % 4 == 0, 16-byte aligned rows): 16-byte
+    // row pieces through global-address-space pointers, several rows per load round
+    typedef f4v __attribute__((address_space(1))) gf4;
+    typedef long long i2v __attribute__((ext_vector_type(2)));
+    typedef i2v __attribute__((address_space(1))) gi2;
+    const int i = tile * 4 * NT + 4 * threadIdx.x;
+    if (i >= g.n) return;
+    gf4* dst = (gf4*)(g.dst + i);
+    if (g.mode == GF_REDUCE) {      // int64 fixed-point rows (exact in any order), re-zeroed
+      constexpr int GF_DROWS = 8;   // rows per load round (two 16-byte int64 pairs per row)
+      gi2* src = (gi2*)(reinterpret_cast<long long*>(g.src) + i);
+      const size_t n2 = (size_t)g.n >> 1;
+      i2v q0 = {0, 0}, q1 = {0, 0};
+      for (int r0 = 0; r0 < rows; r0 += GF_DROWS) {
+        i2v a[GF_DROWS], b[GF_DROWS];
 #pragma unroll
-        for (int r = 0; r < GF_DROWS; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * NT;
-            v[r][u] = (r0 + r < rows && i < g.n) ? red_raw(g.src, (size_t)(r0 + r) * g.n + i) : 0;
+        for (int r = 0; r < GF_DROWS; ++r) {
+          if (r0 + r < rows) {
+            a[r] = src[(size_t)(r0 + r) * n2];
+            b[r] = src[(size_t)(r0 + r) * n2 + 1];
+          } else {
+            a[r] = i2v{0, 0};
+            b[r] = i2v{0, 0};
           }
+        }
 #pragma unroll
-        for (int r = 0; r < GF_DROWS; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * NT;
-            q[u] += v[r][u];
-            if (r0 + r < rows && i < g.n) reinterpret_cast<long long*>(g.src)[(size_t)(r0 + r) * g.n + i] = 0;
+        for (int r = 0; r < GF_DROWS; ++r) {
+          q0 += a[r];
+          q1 += b[r];
+          if (r0 + r < rows) {
+            src[(size_t)(r0 + r) * n2] = i2v{0, 0};
+            src[(size_t)(r0 + r) * n2 + 1] = i2v{0, 0};
           }
-      } else {                      // GF_SUM: plainly stored float rows, summed in row order
-        float v[GF_DROWS][4];
-#pragma unroll
-        for (int r = 0; r < GF_DROWS; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * NT;
-            v[r][u] = (r0 + r < rows && i < g.n) ? g.src[(size_t)(r0 + r) * g.n + i] : 0.f;
-          }
-#pragma unroll
-        for (int r = 0; r < GF_DROWS; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) s[u] += v[r][u];
+        }
       }
-    }
+      *dst = *dst + f4v{red_fx(q0.x, CFL_FX_G), red_fx(q0.y, CFL_FX_G), red_fx(q1.x, CFL_FX_G),
+                        red_fx(q1.y, CFL_FX_G)};
+    } else {                        // GF_SUM: plainly stored float rows, summed in row order
+      gf4* src = (gf4*)(g.src + i);
+      const size_t n4 = (size_t)g.n >> 2;
+      f4v s = {0.f, 0.f, 0.f, 0.f};
+      for (int r0 = 0; r0 < rows; r0 += GF_ROWS) {
+        f4v v[GF_ROWS];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * NT;
-      if (i < g.n) g.dst[i] += g.mode == GF_REDUCE ? red_fx(q[u], CFL_FX_G) : s[u];
+        for (int r = 0; r < GF_ROWS; ++r) {
+          if (r0 + r < rows) v[r] = src[(size_t)(r0 + r) * n4];
+          else v[r] = f4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int r = 0; r < GF_ROWS; ++r) s += v[r];
+      }
+      *dst = *dst + s;
     }
     return;
   }
