@@ -134,6 +134,13 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* pac
 //
 // VEC: a tile whose row length, offsets and row maps are multiples of 4 elements (every GEMM weight of the model)
 // is moved in 16-byte fp32 / 8-byte bf16 pieces - a quarter of the memory instructions of the per-column form.
+// column swizzle of the 16-byte form's [64][65] transpose tile (ds_*_b32 banks: dword address mod 32, lanes 0-31 /
+// 32-63 per LDS cycle): rows 32 apart and columns 32 apart share banks, so the writes (lanes 0-31: columns 4cq + k,
+// cq = 0..15) and the transposed reads (rows 4rq + i, rq = 0..15) were 2-way conflicted (PMC: 50 % conflict
+// cycles). Rotating a 32-column half by 2 when exactly one of (row >= 32, column >= 32) holds separates both (a
+// bijection per row).
+CFL_DEVICE int opt_swz(int R, int C) { return (C & 32) | ((C + (((R ^ C) >> 5) << 1)) & 31); }
+
 template <bool VEC>
 __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
   const OptItem it = p.items[blockIdx.x];
@@ -222,11 +229,12 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
         *reinterpret_cast<uint2*>(p.packed + it.dst_b + (int64_t)(r % it.q) * it.s1 + (int64_t)(r / it.q) * it.s2 +
                                   it.base2 + c) = b;
       }
-      float* row = &tl[rt + 16 * j][4 * cq];
-      row[0] = w[j].x;
-      row[1] = w[j].y;
-      row[2] = w[j].z;
-      row[3] = w[j].w;
+      const int R = rt + 16 * j;
+      float* row = &tl[R][0];
+      row[opt_swz(R, 4 * cq)] = w[j].x;
+      row[opt_swz(R, 4 * cq + 1)] = w[j].y;
+      row[opt_swz(R, 4 * cq + 2)] = w[j].z;
+      row[opt_swz(R, 4 * cq + 3)] = w[j].w;
     }
     __syncthreads();
     const int rq = tid & 15, r = it.r0 + 4 * rq;
@@ -234,8 +242,9 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
     for (int j = 0; j < 4; ++j) {
       const int ccl = (tid >> 4) + 16 * j, cc = it.c0 + ccl;
       if (cc < it.cols && r < it.rows) {                 // rows % 4 == 0: the whole quad is in range
-        const uint2 b = make_uint2(pack2bf(tl[4 * rq][ccl], tl[4 * rq + 1][ccl]),
-                                   pack2bf(tl[4 * rq + 2][ccl], tl[4 * rq + 3][ccl]));
+        const int R = 4 * rq;
+        const uint2 b = make_uint2(pack2bf(tl[R][opt_swz(R, ccl)], tl[R + 1][opt_swz(R + 1, ccl)]),
+                                   pack2bf(tl[R + 2][opt_swz(R + 2, ccl)], tl[R + 3][opt_swz(R + 3, ccl)]));
         *reinterpret_cast<uint2*>(p.packed + it.dst_t + (int64_t)cc * it.rows + r) = b;
       }
     }
