@@ -135,12 +135,22 @@ CFL_DEVICE void bba_body(const BnBwdApplyParams& p, int bid, int nblocks) {
   bnb_prologue<NT>(q, p.C, co, part, bid == 0);
   // this thread's channel group: constant over its items. 16-byte reads: 8-float rows at an 8-float stride read as
   // scalars were 8-way LDS bank conflicts per read (SQ_LDS_BANK_CONFLICT 43 %, profiles/r3_final/pmc_summary.txt)
+  // The two 16-byte halves are read in swapped order by the channel groups with bit 3 set: a ds_read_b128 lane group
+  // holds 16 channel groups, whose 32-byte rows put groups l and l + 8 on the same banks (8 l dwords mod 64) when
+  // C >= 128 (PMC: 14.6 % conflict cycles)
+  const int sw = (c0 >> 6) & 1;
   float a[8], mean[8], rstd[8], k1[8], k2[8];
-  load_f8(co + c0, a);
-  load_f8(co + p.C + c0, mean);
-  load_f8(co + 2 * p.C + c0, rstd);
-  load_f8(co + 3 * p.C + c0, k1);
-  load_f8(co + 4 * p.C + c0, k2);
+  auto load_co = [&](const float* r, float* f) {
+    const float4 h0 = *reinterpret_cast<const float4*>(r + 4 * sw);
+    const float4 h1 = *reinterpret_cast<const float4*>(r + 4 - 4 * sw);
+    const float4 lo = sw ? h1 : h0, hi = sw ? h0 : h1;
+    f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w; f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
+  };
+  load_co(co + c0, a);
+  load_co(co + p.C + c0, mean);
+  load_co(co + 2 * p.C + c0, rstd);
+  load_co(co + 3 * p.C + c0, k1);
+  load_co(co + 4 * p.C + c0, k2);
   // BBA_IPT items per thread per iteration, all loads issued before any math (memory-level parallelism: the small
   // layers launch few blocks, so one item in flight per thread would leave HBM latency-bound)
   for (; t0 < total; t0 += BBA_IPT * S) {
