@@ -402,11 +402,12 @@ int entry_fwd(const EntryParams& p, hipStream_t st) {
   if (p.Cout % 8 || p.Cout > 64 || !pow2(p.Cout / 8)) return 1;
   const int rows = p.B * p.Ho;
   if (p.S % 4) return 1;
-  // grid cap: 512 at 256^2 / batch 16 (2,048 row steps; A/B-measured - fewer same-address statistics atomics); the
-  // many-step problems (512^2 planned batch: 561k steps) need more resident blocks to hide each block's one-step-ahead
-  // row prefetch: kbench 512^2 / b256 cap 512 / 1,024 / 2,048 = 583 / 432 / 424 us
+  // grid cap: 1,024 at 256^2 / batch 16 (2,048 row steps: two per block; per-position trace A/Bs 15.7 / 15.7 vs
+  // 16.6 / 17.0 us for 512, 20.2 us for 2,048 - round 1 had picked 512 for fewer same-address statistics atomics);
+  // the many-step problems (512^2 planned batch: 561k steps) need more resident blocks to hide each block's
+  // one-step-ahead row prefetch: kbench 512^2 / b256 cap 512 / 1,024 / 2,048 = 583 / 432 / 424 us
   const int cap = cfl_tune(TUNE_ENTRY_FWD_BLOCKS) > 0 ? cfl_tune(TUNE_ENTRY_FWD_BLOCKS)
-                                                     : rows * ((p.Wo + ECH - 1) / ECH) >= 65536 ? 2048 : 512;
+                                                     : rows * ((p.Wo + ECH - 1) / ECH) >= 65536 ? 2048 : 1024;
   if (use_mfma(p)) {
     const int nch = (p.Wo + ECH - 1) / ECH, steps = rows * nch;
     hipLaunchKernelGGL(entry_fwd_mfma_kernel, dim3(steps < cap ? steps : cap), dim3(NT), 0, st, p, nch, steps);

@@ -470,7 +470,7 @@ enum TuneKey {
   TUNE_WGRAD3_MINTILES = 4,    // halo wgrad: min pixel tiles per block (default 32)
   TUNE_IGEMM_CFG = 5,          // generic implicit GEMM: force a tile config 1..7 (see conv_igemm.hip)
   TUNE_CONV3_WB = 6,           // conv3x3: 1 = whole-chunk weight staging (default), 2 = per-tap double buffer
-  TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 512)
+  TUNE_ENTRY_FWD_BLOCKS = 7,   // entry conv forward grid cap (default 1,024; 2,048 at >= 64k row steps)
   TUNE_DW_STREAM_BLOCKS = 8,   // depthwise row-streaming kernels: target grid size (default 768)
   TUNE_CONV3_SMALL = 9,        // conv3x3 low-M layers: 0 = heuristic, 1 = split-K (+ epilogue launch), 2 = 8x8x32 tiles
   TUNE_CONV3_BN = 10,          // conv3x3 whole-chunk path: output-channel tile (0 = 64 when N % 64 == 0, else 32)
