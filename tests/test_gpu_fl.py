@@ -204,4 +204,5 @@ def test_deterministic_local_round_is_bitwise_reproducible():
         # (the loss / accuracy sums are double atomics outside the mode: equal to double rounding)
         assert np.isclose(l0, l1, rtol=1e-9) and np.isclose(v0, v1, rtol=1e-9)
     finally:
-        client.backend.eng.C.set_det(0)
+        from crack_detection_federatedlearning_grpc_amd._native_loader import hip
+        hip().set_det(0)                        # the mode is per process: back to the default for later tests
