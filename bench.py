@@ -10,7 +10,9 @@ value = N * epochs * local_steps * batch / round_seconds (whole node, training i
 validation images are reported separately; weak scaling: per-client work fixed).
 Data: synthetic crack images/masks rendered on the device (per-client shard); weights: Keras-default random init.
 
-Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Launch: ``python bench.py`` (1 GPU); ``python bench.py --gpus N`` spawns the N ranks itself (parallel/spawn.py: one
+child process per GPU with the torch.distributed environment, no GPU call in the parent); under
+``torchrun --nproc-per-node N bench.py --gpus N`` (WORLD_SIZE set) each process is one rank.
 """
 from __future__ import annotations
 
@@ -68,7 +70,22 @@ def main() -> int:
     ap.add_argument("--tune", default="",
                     help="launch-shape knobs for A/B sweeps, 'KEY=V,...' (csrc/kernels/launch.h TuneKey names without "
                          "the TUNE_ prefix, e.g. WGRAD3_BLOCKS=256); default: the built-in heuristics")
+    ap.add_argument("--spawn-timeout", type=float, default=0.0,
+                    help="self-launch only (--gpus N > 1 without WORLD_SIZE): seconds before the ranks are stopped "
+                         "(0: no limit)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here (fresh child processes, one per GPU) and relay rank 0's JSON line.
+        # The parent touches no GPU (device_count does not initialise HIP on this image) and never execs.
+        if args.dist_backend == "nccl":
+            import torch
+            ndev = torch.cuda.device_count()
+            if args.gpus > ndev:
+                raise SystemExit(f"bench.py: --gpus {args.gpus} with the nccl (RCCL) backend needs {args.gpus} "
+                                 f"visible GPUs, found {ndev} (use --dist-backend gloo to rehearse N ranks on fewer)")
+        from crack_detection_federatedlearning_grpc_amd.parallel.spawn import spawn_local_ranks
+        return spawn_local_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                                 timeout=args.spawn_timeout or None)
     if os.environ.get("CFL_BENCH_TUNE"):                 # knob sweeps by name from the environment (tools/gpu_ab3.sh)
         args.tune = ",".join(t for t in (args.tune, os.environ["CFL_BENCH_TUNE"]) if t)
 
@@ -83,6 +100,9 @@ def main() -> int:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 ranks with "
                          f"torch.distributed.run --nproc-per-node {args.gpus} (one rank per GPU)")
     ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} visible GPUs, found {ndev} (RCCL refuses two "
+                         f"ranks on one GPU; --dist-backend gloo rehearses N ranks on fewer)")
     torch.cuda.set_device(local % ndev)               # local % ndev: a gloo rehearsal may share one GPU
     dev = torch.device("cuda", local % ndev)
     if world == 1 and args.fedavg_1rank:

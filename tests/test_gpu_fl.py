@@ -102,6 +102,27 @@ def test_bench_two_ranks_share_one_gpu():
     assert p.stdout.count("[bench] rank ") == 2                                 # each rank logged its view
 
 
+def test_bench_self_launch_two_ranks_without_torchrun():
+    """``python bench.py --gpus 2`` with no launcher (no WORLD_SIZE): bench.py spawns the two ranks itself
+    (parallel/spawn.py) and relays rank 0's single JSON line (verdict r4 item 2)."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+            "--epochs", "1", "--local-steps", "6", "--val-steps", "2", "--samples", "256", "--dist-backend", "gloo",
+            "--spawn-timeout", "200"]
+    p = subprocess.run(args, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=240)
+    print(p.stdout[-2000:], p.stderr[-3000:])
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and p.stdout.strip() == p.stdout.strip().splitlines()[-1]   # one line, rank 0's
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["dist_backend"] == "gloo" and out["value"] > 0
+    for k in ("allreduce_ms", "allreduce_exposed_ms", "overlap_fraction"):
+        assert k in out, (k, sorted(out))
+
+
 
 def test_fl_rccl_product_path_two_clients_one_gpu(tmp_path):
     """The FL product path's device data plane (verdict r2 item 1): an in-process FLServer and TWO ``fl_client.py``
