@@ -86,7 +86,7 @@ def main() -> int:
         from crack_detection_federatedlearning_grpc_amd.parallel.spawn import spawn_local_ranks
         return spawn_local_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
                                  timeout=args.spawn_timeout or None)
-    if os.environ.get("CFL_BENCH_TUNE"):                 # knob sweeps by name from the environment (tools/gpu_ab3.sh)
+    if os.environ.get("CFL_BENCH_TUNE"):                 # knob sweeps by name from the environment (tools/gpu/bench_ab.sh)
         args.tune = ",".join(t for t in (args.tune, os.environ["CFL_BENCH_TUNE"]) if t)
 
     import numpy as np

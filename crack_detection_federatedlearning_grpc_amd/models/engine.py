@@ -936,13 +936,17 @@ class UNetEngine:
 
     def eval_batch_for(self, n_images: int, cap: int = 0) -> int:
         """Largest eval batch <= cap that is a multiple of B and divides ``n_images`` (a whole number of the
-        reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 2048
-        images up to 256^2, 1024 above - the inference engine holds forward activations only (21.7 MB per 256^2
-        image: 38.5 GB for the bench's 1,776-image split in ONE launch, vs three 592-image launches under a 1024 cap:
-        13,069 vs 13,037 img/s), and batches of several hundred images fill the chip where the 16-48-image forward is
-        launch / latency-bound."""
+        reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 1024
+        images, further bounded to a quarter of the device's free HBM at ~21.7 MB of forward activations per 256^2
+        image (scaled by resolution) - several clients may share one device in a rehearsal. Round 4's 2048 cap (the
+        bench's 1,776-image split in ONE launch, 38.5 GB) measured 13,069 vs 13,037 img/s against three 592-image
+        launches: noise, for 2.6x the footprint (profiles/r5_evalcap)."""
         if cap <= 0:
-            cap = int(os.environ.get("CFL_EVAL_CAP", "2048" if self.S <= 256 else "1024"))
+            cap = int(os.environ.get("CFL_EVAL_CAP", "1024"))
+            if self.dev.type == "cuda":
+                free, _total = torch.cuda.mem_get_info(self.dev)
+                per_img = 21.7e6 * (self.S / 256.0) ** 2
+                cap = max(self.B, min(cap, int(free / 4 / per_img)))
         nb = n_images // self.B
         best = 1
         for k in range(1, nb + 1):

@@ -2,7 +2,7 @@
 # Whole-bench A/B: driver-style bench.py runs of each variant, in REPS interleaved passes (run-to-run drift spreads
 # over every variant). VARIANTS: ';'-separated list of "ENV=V ... -- bench args" (either side may be empty; "-" =
 # the default). -> gpurun_out/bab/*.log, one summary line per run
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out/bab
 IFS=';' read -ra VS <<< "${VARIANTS:--}"

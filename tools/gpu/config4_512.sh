@@ -1,9 +1,9 @@
 #!/bin/bash
-# Config 4 (512^2, planned batch) round-4 evidence -> gpurun_out/r4_512: bench (bf16, x2), steady-state kernel
+# Config 4 (512^2, planned batch) evidence -> gpurun_out/$OUT (default config4_512): bench (bf16, x2), steady-state kernel
 # trace summary in step order, per-call roofline at batch 256
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
-O=$R/gpurun_out/r4_512
+O=$R/gpurun_out/${OUT:-config4_512}
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 rm -rf $O; mkdir -p $O
 for i in 1 2; do

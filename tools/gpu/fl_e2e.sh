@@ -1,7 +1,7 @@
 #!/bin/bash
 # End-to-end FL on the GPU box: server + 1 GPU client (HIP engine, hipGraph, evaluator) for 2 short rounds -> FIN,
 # then a tensorboard/h5 artefact check.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out/fl
 timeout -k 10 400 python -m crack_detection_federatedlearning_grpc_amd.fl.launch --preset gpu1-256 \

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 product-path evidence -> gpurun_out/r4_fl: FL product bench (gRPC server + client, HIP engine), a kernel
+# Product-path evidence -> gpurun_out/$OUT (default fl_product): FL product bench (gRPC server + client, HIP engine), a kernel
 # trace of the 1-rank overlapped FedAvg path (tools/overlap_summary.py), and a short end-to-end FL launch to FIN
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
-O=$R/gpurun_out/r4_fl
+O=$R/gpurun_out/${OUT:-fl_product}
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 rm -rf $O; mkdir -p $O
 timeout -k 10 500 python bench.py --fl --steps 2 --warmup 1 > $O/bench_fl.log 2>&1 || { tail -20 $O/bench_fl.log; exit 1; }

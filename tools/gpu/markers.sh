@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 marker + kernel trace of a short FL round (roctx phase ranges from utils/trace.py).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1 CFL_ROCTX=1
 mkdir -p gpurun_out

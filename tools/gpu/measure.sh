@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full measurement pass at HEAD -> gpurun_out/$OUT: bench (bf16 x2), steady-state kernel trace,
 # PMC counter passes, per-call roofline (kbench). Copy the summaries you keep into profiles/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=${OUT:-measure}
 O=$R/gpurun_out/$OUT

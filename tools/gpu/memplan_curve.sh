@@ -1,7 +1,7 @@
 #!/bin/bash
 # Config 4: U-Net 512^2 batch curve on one MI355X (per-client batch 256 / 512 / the HBM planner's, ~1016):
 # images/s and peak HBM per client. One FL round per timed step.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out/memplan
 for b in 256 512 0; do

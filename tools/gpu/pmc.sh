@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC counter passes over graph-replayed training steps (256^2, B=16); one pass per counter group,
 # each within the per-block slot limits (SQ 8, TCC 4 with FETCH_SIZE=3 / WRITE_SIZE=2). Summary: tools/pmc_summary.py
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 mkdir -p gpurun_out/pmc

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Stock PyTorch-ROCm comparator (MIOpen) on the bench shapes: bf16 eager, bf16 hipGraph, fp32 eager.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for a in "" "--graph" "--fp32"; do

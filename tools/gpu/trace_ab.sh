@@ -2,7 +2,7 @@
 # Kernel-trace A/B of the steady-state step: one rocprofv3 --kernel-trace run of bench.py --profile-steps per
 # variant (VARIANTS: space-separated --tune strings, "-" = default), then tools/trace_diff.py of each against the
 # first. -> gpurun_out/ta/<i>/ (+ prof_summary of the first)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 export TMPDIR=/tmp CFL_NO_JIT_BUILD=1
 rm -rf $R/gpurun_out/ta; mkdir -p $R/gpurun_out/ta

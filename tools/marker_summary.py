@@ -1,4 +1,4 @@
-"""Kernel time per roctx phase range from a rocprofv3 --marker-trace --kernel-trace run (tools/gpu_markers.sh).
+"""Kernel time per roctx phase range from a rocprofv3 --marker-trace --kernel-trace run (tools/gpu/markers.sh).
 
 A kernel belongs to the innermost range whose host push/pop interval contains the kernel's dispatch (correlation)
 on the host side; graph replays are attributed by their launch time, so the GPU work of an asynchronously enqueued

@@ -1,4 +1,4 @@
-"""Per-kernel instruction-issue activity from a tools/pmc_valu.txt pass (rocprofv3 --pmc CSV):
+"""Per-kernel instruction-issue activity from a pass over SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES (rocprofv3 --pmc CSV):
 SQ_ACTIVE_INST_{VALU,LDS,ANY} / SQ_WAVE_CYCLES = the share of a wave's resident cycles in which it issued that
 instruction class (MFMA issue counts as VALU). Low ANY with high wait means the kernel is latency-bound.
 

@@ -1,4 +1,4 @@
-"""Per-kernel summary of the rocprofv3 PMC passes written by tools/gpu_pmc.sh (gpurun_out/pmc/p*/).
+"""Per-kernel summary of the rocprofv3 PMC passes written by tools/gpu/pmc.sh (gpurun_out/pmc/p*/).
 
 Per kernel (all dispatches of one kernel name, over the profiled steps):
   time       sum of dispatch durations in the pass (counter collection serialises dispatches)
