@@ -159,36 +159,54 @@ class FLClient:
         if self.cfg.client_weight_file:   # trainer -> driver hand-off file (client_fit_model.py:238-240)
             codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
 
-    def _payload(self) -> tuple:
-        """(weights to upload or None, data plane). RCCL mode: the weighted all-reduce runs here (in place on the
-        GPU, or over host arrays); rank 0 alone uploads the average for the server's copy (its host copy is taken
-        here, before the next round can touch the weights), the other ranks send nothing. A failed collective
-        leaves the local model unchanged (fedavg_device rolls back) and the client continues on the gRPC plane."""
+    def _fallback(self, e: BaseException) -> None:
+        print(f"[{self.name}] RCCL aggregation failed ({type(e).__name__}: {e}); aborting the "
+              f"communicator, falling back to the gRPC data plane")
+        if self.aggregator is not None:
+            self.aggregator.abort()
+        self.aggregator = None
+        self.fallbacks += 1
+
+    def _payload(self, async_ok: bool = False) -> tuple:
+        """(weights to upload or None, data plane, pending device FedAvg or None). RCCL mode: the weighted
+        all-reduce is issued here (in place on the GPU, or over host arrays). With ``async_ok`` and a device
+        buffer the collective is NOT waited for: the ``PendingFedAvg`` goes to the round report, which learns the
+        verdict from its watchdog, while this thread starts the next round. Otherwise the verdict is awaited here:
+        rank 0 alone uploads the average for the server's copy (host copy of the average kept by the side stream),
+        the other ranks send nothing; a failed collective leaves the local model unchanged (rolled back) and the
+        client continues on the gRPC plane."""
         n = getattr(self.trainer, "n_samples", 0)
         arrays = None
         plane = ""
+        pending = None
         if self.aggregator is not None:
             try:
-                dev = getattr(self.trainer, "fedavg_device", None)
-                if dev is not None and dev(self.aggregator, n):
-                    pass                                         # averaged in place on the GPU (no host staging)
+                adev = getattr(self.trainer, "fedavg_device_async", None)
+                pending = adev(self.aggregator, n) if adev is not None else None
+                if pending is not None:
+                    if async_ok:
+                        return None, "rccl", pending
+                    self.trainer.settle_fedavg(pending)          # waits for the watchdog's verdict
+                    if self.aggregator.rank == 0:
+                        arrays = self.trainer.table.to_list(pending.host_average())
                 else:
-                    arrays = self.aggregator.average(self.trainer.get_weights(), n)   # host-array trainers
-                    self.trainer.set_weights(arrays)             # local model <- global average
+                    dev = getattr(self.trainer, "fedavg_device", None)
+                    if dev is not None and dev(self.aggregator, n):
+                        pass                                     # averaged in place (no host staging)
+                    else:
+                        arrays = self.aggregator.average(self.trainer.get_weights(), n)   # host-array trainers
+                        self.trainer.set_weights(arrays)         # local model <- global average
             except Exception as e:                               # peer lost / collective timed out
-                print(f"[{self.name}] RCCL aggregation failed ({type(e).__name__}: {e}); aborting the "
-                      f"communicator, falling back to the gRPC data plane")
-                self.aggregator.abort()
-                self.aggregator = None
-                self.fallbacks += 1
+                self._fallback(e)
                 arrays = None
+                pending = None
             else:
                 plane = "rccl"
                 if self.aggregator.rank != 0:
-                    return None, plane                           # rank 0 alone uploads the server's copy
+                    return None, plane, pending                  # rank 0 alone uploads the server's copy
         if arrays is None:
             arrays = self.trainer.get_weights()
-        return arrays, plane
+        return arrays, plane, pending
 
     def _encode(self, arrays) -> bytes:
         if arrays is None:
@@ -239,6 +257,24 @@ class FLClient:
             return                      # RCCL mode: local weights already hold the all-reduced average
         self.trainer.set_weights(codec.decode(blob)[0])
 
+    def _discard_round(self, box: Dict, res: Dict, fell_back: bool) -> None:
+        """Undo the round trained while an asynchronous report was pending (its start was not the run's global
+        model): drop its history entry and reset the local model to the global one - the server's reply when it
+        carries parameters (always after a gRPC fallback), else the average this client's collective produced."""
+        pend = box["pending"]
+        if self.history:
+            self.history.pop()
+        if res.get("blob") and (fell_back or self.aggregator is None):
+            self.trainer.set_weights(codec.decode(res["blob"])[0])
+        elif pend is None:
+            self.trainer.set_weights(box["avg"])            # host path: the average taken after the collective
+        elif fell_back:
+            self.trainer.restore_flat(pend.host_backup())
+        else:
+            self.trainer.restore_flat(pend.avg)
+        if self.cfg.client_weight_file:
+            codec.save_weight_file(self.cfg.client_weight_file, self.trainer.get_weights())
+
     # -- main loop ------------------------------------------------------------------------------------------
     def run(self) -> str:
         with grpc.insecure_channel(self.target, options=channel_options(self.cfg.max_message_mb)) as ch:
@@ -262,7 +298,7 @@ class FLClient:
             self._train(cr)
             while cr <= mtr:
                 join_s = 0.0
-                if self._pending is not None:     # the previous round's TRAIN_DONE / VERSION exchange
+                if self._pending is not None:     # the previous round's collective verdict + TRAIN_DONE / VERSION
                     tj = time.perf_counter()
                     th, box = self._pending
                     th.join()
@@ -270,10 +306,19 @@ class FLClient:
                     join_s = time.perf_counter() - tj
                     if "error" in box:
                         raise box["error"]
-                    res = box["res"]
+                    res, pend = box["res"], box["pending"]
+                    fell_back = box.get("fallback", False)
                     self._log_phase(dict(res["phase"], aggregate_s=box["aggregate_s"], join_wait_s=join_s,
-                                         exposed_s=box["aggregate_s"] + join_s, async_upload=True))
+                                         exposed_s=box["aggregate_s"] + join_s, async_upload=True,
+                                         **(pend.stats() if pend is not None else {})))
+                    if pend is not None and pend.engine is not None:
+                        pend.engine.stall_log = None
+                    if fell_back:                 # the collective failed: this client continues on gRPC
+                        self._fallback(pend.error)
                     if res["state"] == "FIN":     # the server finished the run (e.g. fewer rounds than advertised)
+                        # the round trained meanwhile is not part of the run: the client ends at the run's global
+                        # model (the server's reply after a fallback, else the average this round all-reduced)
+                        self._discard_round(box, res, fell_back)
                         cr, mv = res["cr"], res["mv"]
                         self.final_state = "FIN"
                         break
@@ -281,25 +326,44 @@ class FLClient:
                         print(f"[{self.name}] unexpected state {res['state']!r}; exiting")
                         self.final_state = res["state"]
                         break
-                    if (res["cr"], res["mv"]) != (cr, mv):
-                        print(f"[{self.name}] server moved to round {res['cr']} / version {res['mv']} (expected "
-                              f"{cr} / {mv}); following it")
+                    if fell_back or (res["cr"], res["mv"]) != (cr, mv):
+                        # the round just trained started from a failed average or a round the server did not
+                        # advance to: drop it and train the server's round from the server's model
+                        print(f"[{self.name}] server round {res['cr']} / version {res['mv']} (trained {cr} / {mv}"
+                              f"{' from a failed collective' if fell_back else ''}); re-training from the global")
+                        self._discard_round(box, res, fell_back)
                         cr, mv = res["cr"], res["mv"]
+                        self._train(cr)
+                        continue
                 print(f"### Deliver model state: TRAIN DONE to server ### round {cr}")
                 if self.cfg.fault_delay_s:
                     time.sleep(self.cfg.fault_delay_s)
                 t0 = time.perf_counter()
+                async_ok = self.cfg.async_upload and cr < mtr
                 with trace_phase("fl/aggregate"):
-                    arrays, plane = self._payload()        # RCCL mode: the all-reduce runs here
+                    arrays, plane, pend = self._payload(async_ok)   # RCCL mode: the all-reduce is issued here
                 agg_s = time.perf_counter() - t0
-                if plane == "rccl" and self.cfg.async_upload and cr < mtr:
-                    # this client already holds the round's average: report it (rank 0: upload it) from a
-                    # background thread and start the next round now, off the server's aggregation path
-                    box: Dict = {"aggregate_s": agg_s}
+                if plane == "rccl" and async_ok:
+                    # device path: the collective runs on the GPU's side stream; the round's report (rank 0: upload
+                    # of the average) waits for its verdict in a background thread while this thread starts the
+                    # next round (whose first step waits per bucket on the device), off the server's aggregation
+                    # path. Host-array path: the collective is done; only the report goes to the thread.
+                    box: Dict = {"aggregate_s": agg_s, "pending": pend,
+                                 "avg": None if pend is not None else self.trainer.get_weights()}
+                    rank0 = self.aggregator.rank == 0
 
-                    def report(cr=cr, mv=mv, arrays=arrays, plane=plane, box=box):
+                    def report(cr=cr, mv=mv, pend=pend, box=box, rank0=rank0, arrays=arrays):
                         try:
-                            box["res"] = self._report(stub, cr, mv, arrays, plane)
+                            if pend is None:
+                                arr, pl = arrays, "rccl"
+                            elif pend.wait(rollback=False):
+                                arr, pl = (self.trainer.table.to_list(pend.host_average()) if rank0 else None), "rccl"
+                            else:          # collective lost: report the local model over gRPC
+                                print(f"[{self.name}] round {cr} collective failed ({pend.error}); reporting the "
+                                      f"local model over gRPC")
+                                arr, pl = self.trainer.table.to_list(pend.host_backup()), ""
+                                box["fallback"] = True
+                            box["res"] = self._report(stub, cr, mv, arr, pl)
                             self._training(stub)
                         except BaseException as e:   # re-raised by the main thread at the join
                             box["error"] = e
@@ -310,7 +374,9 @@ class FLClient:
                     self._train(cr)
                     continue
                 res = self._report(stub, cr, mv, arrays, plane)
-                phase = dict(res["phase"], aggregate_s=agg_s)
+                phase = dict(res["phase"], aggregate_s=agg_s, **(pend.stats() if pend is not None else {}))
+                if pend is not None and pend.engine is not None:
+                    pend.engine.stall_log = None
                 st = res["state"]
                 self._log_phase(phase)
                 if st in ("NOT_WAIT", "RESP_ARY"):

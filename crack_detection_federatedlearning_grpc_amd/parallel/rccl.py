@@ -139,7 +139,7 @@ class RcclAggregator:
     ``backend``: "nccl" (RCCL over xGMI, the product path) or "gloo" (CPU clients, and the one-GPU rehearsal of
     N clients sharing a card, which RCCL refuses). Collectives stay asynchronous to the host - no
     ``TORCH_NCCL_BLOCKING_WAIT``, which would serialise the bucketed all-reduce bucket by bucket on the host: the
-    side stream waits on each bucket's collective, and a dead peer is detected by ``wait_complete``'s host-side
+    side stream waits on each bucket's collective, and a dead peer is detected by the ``PendingFedAvg`` watchdog's
     deadline (``timeout_s``), which fires before the process group's own timeout so this process aborts the
     communicator first and the client can fall back to gRPC."""
 
@@ -161,6 +161,7 @@ class RcclAggregator:
         self.device = device if cuda else torch.device("cpu")
         self._cached = None
         self._backup: Optional[torch.Tensor] = None
+        self._avg: Optional[torch.Tensor] = None
         print(f"[rccl] rank {rank}/{world} world_size {world} backend {dist.get_backend()} device "
               f"{self.device if not cuda else torch.cuda.get_device_name(device)} ({self.device})", flush=True)
 
@@ -199,52 +200,63 @@ class RcclAggregator:
         all-reduce on a side stream (no host staging); returns the per-bucket events for ``defer_until``."""
         return self._reducer(flat, first_bucket).average_async(float(max(n_local, 1)), on_bucket=on_bucket)
 
-    def wait_complete(self, events: Sequence[Tuple[slice, object]]) -> None:
-        """Host-side completion check with a deadline: poll the last bucket's event (recorded after every earlier
-        bucket on the same side stream) without blocking inside the runtime, so a collective that can never
-        finish (dead peer) raises ``TimeoutError`` here instead of hanging the client."""
-        if not events:
-            return
-        ev = events[-1][1]
-        end = time.monotonic() + self.timeout_s
-        while not ev.query():
-            if time.monotonic() > end:
-                raise TimeoutError(f"FedAvg all-reduce not complete after {self.timeout_s:.0f} s (peer lost?)")
-            time.sleep(5e-5)
+    def fedavg_device_async(self, flat: torch.Tensor, n_local: float,
+                            on_bucket: Optional[Callable[[slice], None]] = None,
+                            first_bucket: int = 0) -> "PendingFedAvg":
+        """The product path's FedAvg, off the host's critical path: the local model is copied (``backup``, 8 MB
+        device copy on the compute stream), the bucketed weighted all-reduce is issued in place on the side stream
+        (``average_device``), and after the last bucket the side stream also copies the average into ``avg`` (the
+        round's global model, kept for rank 0's upload and for a restore when the server ends the run while the next
+        round trains). Nothing here waits: the returned ``PendingFedAvg`` carries the bucket events for the engine's
+        per-layer waits (``defer_until``) and a watchdog thread that polls the last event against the deadline
+        (``timeout_s``) - on expiry it aborts the communicator and drains the side stream, and the caller's next
+        ``wait()`` reports the failure (the rollback and the gRPC fallback run there). A failure while ISSUING
+        (e.g. a dead peer under gloo, whose collectives run on the host) is rolled back here already."""
+        if self._backup is None or self._backup.numel() != flat.numel() or self._backup.device != flat.device:
+            self._backup = torch.empty_like(flat)
+            self._avg = torch.empty_like(flat)
+        self._backup.copy_(flat)
+        red = self._reducer(flat, first_bucket)
+        red.timing = flat.device.type == "cuda"
+        n_b, seen = len(red.buckets), [0]
+        avg = self._avg
+
+        def hook(sl: slice) -> None:
+            if on_bucket is not None:
+                on_bucket(sl)
+            seen[0] += 1
+            if seen[0] == n_b:              # on the side stream, behind every bucket's collective and repack
+                avg.copy_(flat)
+        try:
+            evs = red.average_async(float(max(n_local, 1)), on_bucket=hook)
+        except BaseException as e:
+            self.abort()
+            self._drain_side(flat)
+            flat.copy_(self._backup)
+            return PendingFedAvg(self, flat, [], None, avg, self._backup, error=e)
+        timing = red.timings[-1] if red.timing and red.timings else None
+        red.timings = []
+        return PendingFedAvg(self, flat, evs, timing, avg, self._backup)
 
     def fedavg_device(self, flat: torch.Tensor, n_local: float,
                       on_bucket: Optional[Callable[[slice], None]] = None,
                       first_bucket: int = 0) -> List[Tuple[slice, object]]:
-        """``average_device`` + ``wait_complete`` with rollback: the buckets are pre-scaled (w_k * n_k / sum n) and
-        reduced in place, so a failure part-way would leave ``flat`` a mix of scaled, reduced and untouched
-        buckets. The buffer is copied first (8 MB device copy); on any failure the communicator is aborted, the
-        side stream drained (no queued bucket work lands after the restore), the local model restored and the
-        error re-raised - the caller then uploads its unchanged local weights over gRPC.
+        """Blocking form of ``fedavg_device_async`` (the synchronous report of the last round, host-array callers,
+        tests): issue, wait for the watchdog's verdict, roll back and re-raise on failure. The buckets are pre-scaled
+        (w_k * n_k / sum n) and reduced in place, so a failure part-way would leave ``flat`` a mix of scaled, reduced
+        and untouched buckets: the rollback restores the pre-FedAvg copy after the side stream has drained (no queued
+        bucket work lands after the restore); the caller then uploads its unchanged local weights over gRPC."""
+        pending = self.fedavg_device_async(flat, n_local, on_bucket=on_bucket, first_bucket=first_bucket)
+        if not pending.wait():
+            raise pending.error
+        return pending.events
 
-        The host waits (with the deadline) for the last bucket here, so the rollback needs nothing later; in the
-        product path that wait is the collective itself plus the ranks' arrival skew - the control-plane chain
-        behind it (rank 0's upload, the server's aggregation, the VERSION long-poll) is taken off the round's
-        critical path by the client's asynchronous report (fl/client.py, ``async_upload``)."""
-        if self._backup is None or self._backup.numel() != flat.numel() or self._backup.device != flat.device:
-            self._backup = torch.empty_like(flat)
-        self._backup.copy_(flat)
-        try:
-            evs = self.average_device(flat, n_local, on_bucket=on_bucket, first_bucket=first_bucket)
-            self.wait_complete(evs)
-            return evs
-        except BaseException:
-            self.abort()
-            self._drain_side(flat)
-            flat.copy_(self._backup)
-            raise
-
-    def _drain_side(self, flat: torch.Tensor, drain_s: float = 30.0) -> None:
+    def _drain_side(self, flat: torch.Tensor, drain_s: float = 30.0, order: bool = True) -> None:
         """After an abort, work still queued on the aggregation side stream (the in-place all-reduce output of an
         issued bucket, the per-bucket bf16 repacks) could land AFTER the rollback and overwrite the restored
-        weights with a partly reduced bucket. Wait (host deadline) for the side stream to drain and order the
-        current stream behind it; if it never drains the weights cannot be trusted: exit non-zero."""
-        red = self._cached[1] if self._cached is not None else None
-        side = red._side if red is not None else None
+        weights with a partly reduced bucket. Wait (host deadline) for the side stream to drain and (``order``)
+        order the current stream behind it; if it never drains the weights cannot be trusted: exit non-zero."""
+        side = self.side_stream()
         if side is None or flat.device.type != "cuda":
             return
         ev = torch.cuda.Event()
@@ -256,7 +268,12 @@ class RcclAggregator:
                       f"weights may be partly overwritten - exiting", flush=True)
                 os._exit(70)
             time.sleep(1e-3)
-        torch.cuda.current_stream(flat.device).wait_stream(side)
+        if order:
+            torch.cuda.current_stream(flat.device).wait_stream(side)
+
+    def side_stream(self):
+        red = self._cached[1] if self._cached is not None else None
+        return red._side if red is not None else None
 
     def abort(self) -> None:
         """A peer died or a collective timed out: tear the communicator down without a collective shutdown
@@ -276,3 +293,107 @@ class RcclAggregator:
     def close(self) -> None:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+class PendingFedAvg:
+    """An issued device FedAvg of the FL product path (``RcclAggregator.fedavg_device_async``).
+
+    The reference blocks completely around its aggregation (gather -> NumPy mean -> 20 s poll,
+    /root/reference/fl_server.py:92-135, fl_client.py:136-155). Here the collective runs on the side stream while
+    the training thread goes on: ``events`` feed the engine's per-layer waits, and a daemon WATCHDOG thread polls
+    the last bucket's event (1 ms period, no spin on the training thread) against the aggregator's deadline. On
+    expiry it records the failure, aborts the communicator and drains the side stream; ``wait()`` - called where
+    the client needs the verdict (the round report, or the join before the next FedAvg) - then orders the caller's
+    stream behind the drained side stream and restores the pre-FedAvg local model (``rollback``) unless told not
+    to. ``stats()`` gives the hipEvent split of the collective: ``allreduce_ms`` (issue -> last bucket reduced) and
+    ``allreduce_exposed_ms`` (how long the next round's first step actually stalled for it, when an engine's
+    ``stall_log`` recorded that step's waits)."""
+
+    poll_s = 1e-3
+
+    def __init__(self, agg: "RcclAggregator", flat: torch.Tensor, events, timing, avg: torch.Tensor,
+                 backup: torch.Tensor, error: Optional[BaseException] = None):
+        import threading
+        self.agg, self.flat, self.events, self.timing = agg, flat, list(events), timing
+        self.avg, self.backup = avg, backup
+        self.error = error
+        self.engine = None                  # set by the trainer: its stall_log holds the next step's waits
+        self._done = threading.Event()
+        self._rolled = error is not None    # an issue-time failure was rolled back by the aggregator already
+        if error is not None or not self.events:
+            self._done.set()
+            self._t = None
+        else:
+            self._t = threading.Thread(target=self._watch, name="fedavg-watchdog", daemon=True)
+            self._t.start()
+
+    def _poll_done(self, ev) -> bool:
+        return bool(ev.query())
+
+    def _watch(self) -> None:
+        ev = self.events[-1][1]
+        end = time.monotonic() + self.agg.timeout_s
+        try:
+            while not self._poll_done(ev):
+                if time.monotonic() > end:
+                    raise TimeoutError(f"FedAvg all-reduce not complete after {self.agg.timeout_s:.0f} s "
+                                       f"(peer lost?)")
+                time.sleep(self.poll_s)
+        except BaseException as e:           # a peer died / the collective can never finish
+            self.error = e
+            self.agg.abort()
+            self.agg._drain_side(self.flat, order=False)
+        finally:
+            self._done.set()
+
+    @property
+    def done(self) -> bool:
+        return self._done.is_set()
+
+    def wait(self, rollback: bool = True) -> bool:
+        """True iff the collective completed. On failure (after the watchdog has aborted the communicator and the
+        side stream has drained) the caller's stream is ordered behind the side stream and, with ``rollback``, the
+        flat buffer is restored to the pre-FedAvg local model."""
+        self._done.wait()
+        if self.error is None:
+            return True
+        side = self.agg.side_stream()
+        if side is not None and self.flat.device.type == "cuda":
+            torch.cuda.current_stream(self.flat.device).wait_stream(side)
+        if rollback and not self._rolled:
+            self.flat.copy_(self.backup)
+            self._rolled = True
+        return False
+
+    def _host(self, t: torch.Tensor) -> np.ndarray:
+        """Host copy of a buffer written on the compute or the side stream, taken on a private stream that waits for
+        the collective's last event (not on the compute stream, which may already run the next round)."""
+        if t.device.type != "cuda":
+            return t.detach().numpy().copy()
+        s = torch.cuda.Stream(device=t.device)
+        if self.events:
+            s.wait_event(self.events[-1][1])
+        with torch.cuda.stream(s):
+            out = t.cpu().numpy().copy()
+        return out
+
+    def host_average(self) -> np.ndarray:
+        """The round's global model (valid after a successful ``wait``)."""
+        return self._host(self.avg)
+
+    def host_backup(self) -> np.ndarray:
+        """The pre-FedAvg local model (what a failed round uploads over gRPC)."""
+        return self._host(self.backup)
+
+    def stats(self) -> Dict[str, float]:
+        """hipEvent timings, read once the events are complete (e.g. after the next round)."""
+        out: Dict[str, float] = {}
+        if self.timing is None or self.error is not None:
+            return out
+        t_issue, t_ar, _t_last = self.timing
+        out["allreduce_ms"] = float(t_issue.elapsed_time(t_ar))
+        st = getattr(self.engine, "stall_log", None) if self.engine is not None else None
+        if st and len(st) >= 2:
+            (_b0, a0), (b1, a1) = st[0], st[1]
+            out["allreduce_exposed_ms"] = float(t_issue.elapsed_time(a0) + b1.elapsed_time(a1))
+        return out

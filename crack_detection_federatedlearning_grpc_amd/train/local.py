@@ -127,23 +127,60 @@ class LocalFit:
     def get_weights(self) -> List[np.ndarray]:
         return self.table.to_list(self.backend.get_flat())
 
-    def fedavg_device(self, aggregator, n_local: float) -> bool:
-        """Device-resident FedAvg (RCCL data plane): reduce the engine's flat fp32 parameter buffer in place,
-        bucketed on a side stream (first bucket = the encoder's parameters) with each bucket's layers repacked to
-        bf16 there, and wait (host deadline) for the last bucket. On failure the aggregator has restored the local parameters; the bf16 copies, which the
-        side stream may have partly repacked, are rebuilt from them before the error propagates (the client
-        then uploads its local model over gRPC). False when the backend holds no device buffer."""
+    def fedavg_device_async(self, aggregator, n_local: float):
+        """Device-resident FedAvg (RCCL data plane) without a host wait: the engine's flat fp32 parameter buffer is
+        reduced in place, bucketed on a side stream (first bucket = the encoder's parameters) with each bucket's
+        layers repacked to bf16 there; the next round's first step waits per bucket on the device
+        (``defer_until``) and records its stalls (``stall_log``) for the exposed-time split. Returns the
+        ``PendingFedAvg`` (its watchdog owns the deadline), or None when the backend holds no device buffer. A failure
+        while issuing was rolled back by the aggregator; the bf16 copies are rebuilt and the error raised."""
         eng = getattr(self.backend, "eng", None)
-        if eng is None or eng.flat.device.type != "cuda" or not hasattr(aggregator, "fedavg_device"):
-            return False
-        try:
-            evs = aggregator.fedavg_device(eng.flat, n_local, on_bucket=eng.pack_bucket, first_bucket=eng.split_at)
-        except BaseException:
+        if eng is None or eng.flat.device.type != "cuda" or not hasattr(aggregator, "fedavg_device_async"):
+            return None
+        eng.stall_log = []
+        pending = aggregator.fedavg_device_async(eng.flat, n_local, on_bucket=eng.pack_bucket,
+                                                 first_bucket=eng.split_at)
+        if pending.error is not None:
+            eng.stall_log = None
             eng.defer_until([])
             eng.pack()
-            raise
-        eng.defer_until(evs)
+            raise pending.error
+        pending.engine = eng
+        eng.defer_until(pending.events)
+        return pending
+
+    def fedavg_device(self, aggregator, n_local: float) -> bool:
+        """Blocking form (the last round's synchronous report): issue, wait for the watchdog's verdict; on failure
+        the local parameters are restored (after the side stream drained) and the bf16 copies, which the side
+        stream may have partly repacked, rebuilt before the error propagates (the client then uploads its local
+        model over gRPC). False when the backend holds no device buffer."""
+        pending = self.fedavg_device_async(aggregator, n_local)
+        if pending is None:
+            return False
+        self.settle_fedavg(pending)
         return True
+
+    def settle_fedavg(self, pending) -> bool:
+        """Wait for ``pending``; on failure roll the local model back (pre-FedAvg copy) and raise."""
+        eng = pending.engine
+        if pending.wait(rollback=True):
+            return True
+        if eng is not None:
+            eng.defer_until([])
+            eng.stall_log = None
+            eng.pack()
+        raise pending.error
+
+    def restore_flat(self, flat: "np.ndarray | object") -> None:
+        """Replace the local model by a device or host flat buffer (e.g. the round's average kept by a
+        ``PendingFedAvg`` when the server ends the run while the next round was already training)."""
+        eng = getattr(self.backend, "eng", None)
+        if eng is not None and not isinstance(flat, np.ndarray):
+            eng.defer_until([])
+            eng.flat.copy_(flat)
+            eng.pack()
+        else:
+            self.backend.set_flat(np.asarray(flat))
 
     def _log(self, rec: Dict) -> None:
         line = json.dumps(rec)

@@ -3,8 +3,9 @@ import numpy as np
 
 
 class FakeTrainer:
-    def __init__(self, table, delta=1.0, n_samples=10):
+    def __init__(self, table, delta=1.0, n_samples=10, sleep_s=0.0):
         self.table = table
+        self.sleep_s = sleep_s
         self.flat = np.zeros(table.total, np.float32)
         self.delta = delta
         self.n_samples = n_samples
@@ -18,6 +19,9 @@ class FakeTrainer:
 
     def train_round(self, cr):
         self.rounds.append(cr)
+        if self.sleep_s:
+            import time
+            time.sleep(self.sleep_s)
         for e in self.table.entries:
             self.flat[e.offset:e.offset + e.size] += self.delta
         return {"loss": 0.0, "accuracy": 1.0}

@@ -136,8 +136,8 @@ def test_fl_rccl_product_path_two_clients_one_gpu(tmp_path):
     from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
     from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
     table = ParamTable()
-    common = dict(max_rounds=2, epochs=1, steps_per_epoch=12, synthetic_samples=256, val_samples=192,
-                  num_clients=2, data_plane="rccl", dist_backend="gloo", rccl_timeout_s=120.0)
+    common = dict(max_rounds=3, epochs=1, steps_per_epoch=12, synthetic_samples=256, val_samples=192,
+                  num_clients=2, data_plane="rccl", dist_backend="gloo", rccl_timeout_s=120.0, deterministic=True)
     cfg = config.from_args(None, preset="gpu8-256", work_dir=str(tmp_path), server_weight_file="", **common)
     srv = FLServer(cfg, table=table)
     port = srv.start(0)
@@ -163,16 +163,23 @@ def test_fl_rccl_product_path_two_clients_one_gpu(tmp_path):
     for o in outs:
         print(o[-3000:])
     assert all(p.returncode == 0 for p in procs), [o[-2000:] for o in outs]
-    assert [h.round for h in srv.state.history] == [1, 2] and srv.state.finished
+    assert [h.round for h in srv.state.history] == [1, 2, 3] and srv.state.finished
     assert all("world_size 2 backend gloo" in o for o in outs)                   # both joined the 2-rank group
     finals = [table.from_list(codec.load_weight_file(str(tmp_path / f"final{r}.pickle"))) for r in range(2)]
     assert np.array_equal(finals[0], finals[1])                                   # same global average, bit-equal
     assert np.array_equal(finals[0], srv.state.global_flat)                       # == the server's copy
     assert np.abs(finals[0] - table.init_flat(cfg.seed)).max() > 1e-3              # and it trained
     phases = [[json.loads(x) for x in open(tmp_path / f"c{r}.jsonl") if '"phases"' in x] for r in range(2)]
-    assert all(len(ph) == 2 and all(p["data_plane"] == "rccl" for p in ph) for ph in phases), phases
+    assert all(len(ph) == 3 and all(p["data_plane"] == "rccl" for p in ph) for ph in phases), phases
     pay = sorted([p["payload_bytes"] for p in ph] for ph in phases)
-    assert pay[0] == [0, 0] and all(b > 0 for b in pay[1]), pay                   # rank 1 uploads nothing
+    assert pay[0] == [0, 0, 0] and all(b > 0 for b in pay[1]), pay                # rank 1 uploads nothing
+    # the collective is off the host's critical path (verdict r4 item 3): rounds 1-2 reported asynchronously with
+    # the hipEvent split of the all-reduce - its duration and the next round's first-step stall - the last round
+    # synchronously (FIN)
+    for ph in phases:
+        assert [p.get("async_upload", False) for p in ph] == [True, True, False], ph
+        assert all(p["allreduce_ms"] >= 0.0 for p in ph), ph
+        assert all(p["allreduce_exposed_ms"] >= 0.0 for p in ph[:2]), ph
     assert all(p.get("reply_bytes", 0) == 0 for ph in phases for p in ph)         # no parameters shipped back
 
 

@@ -886,18 +886,20 @@ def test_overlapped_fedavg_bucket_repack_and_split_graph_step():
         dist.destroy_process_group()
 
 
-def test_rccl_rollback_waits_for_queued_side_stream_work():
+def test_rccl_rollback_waits_for_queued_side_stream_work(monkeypatch):
     """RcclAggregator.fedavg_device failing while bucket work is still queued on the aggregation side stream (here a
-    long spin kernel followed by a write into the buffer): the rollback drains the side stream before restoring, so
-    the restored weights are exactly the pre-FedAvg copy (advisor r3: the restore raced the queued kernels)."""
+    long spin kernel followed by a write into the buffer): the PendingFedAvg watchdog aborts and drains the side
+    stream, and the rollback restores exactly the pre-FedAvg copy (advisor r3: the restore raced the queued
+    kernels). The non-blocking form returns before the collective completes and reports the verdict at wait()."""
     import socket
     import torch.distributed as dist
-    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+    from crack_detection_federatedlearning_grpc_amd.parallel import rccl
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    agg = RcclAggregator(0, 1, "127.0.0.1", port, torch.device("cuda", torch.cuda.current_device()), timeout_s=30)
+    agg = rccl.RcclAggregator(0, 1, "127.0.0.1", port, torch.device("cuda", torch.cuda.current_device()),
+                              timeout_s=30)
     try:
         flat = torch.randn(3 << 20, device=DEV)
         want = flat.clone()
@@ -906,9 +908,19 @@ def test_rccl_rollback_waits_for_queued_side_stream_work():
             torch.cuda._sleep(20_000_000)
             flat[sl].add_(1.0)
 
-        def fail(events):
+        # healthy non-blocking FedAvg: returns at once (the watchdog thread owns the deadline), the average lands
+        pend = agg.fedavg_device_async(flat, 1.0, on_bucket=slow_bucket)
+        assert pend.events and not pend.done              # issued, not waited for
+        assert pend.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(flat, want + 1.0) and torch.equal(pend.avg, flat)   # 1 rank: identity (+ the clobber)
+        assert np.array_equal(pend.host_backup(), want.cpu().numpy())
+        assert pend.stats()["allreduce_ms"] >= 0.0
+        flat.copy_(want)
+
+        def fail(self, ev):
             raise TimeoutError("injected: collective lost with buckets still queued")
-        agg.wait_complete = fail
+        monkeypatch.setattr(rccl.PendingFedAvg, "_poll_done", fail)
         with pytest.raises(TimeoutError):
             agg.fedavg_device(flat, 1.0, on_bucket=slow_bucket)
         torch.cuda.synchronize()

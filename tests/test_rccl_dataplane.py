@@ -189,3 +189,53 @@ def test_rccl_failure_mid_bucket_uploads_local_model(tmp_path):
     assert np.isclose(srv.state.global_flat[table.entries[0].offset], 8.0)
     assert all(p["data_plane"] == "grpc" for ph in phases.values() for p in ph)
     assert all(p["payload_bytes"] > 0 for ph in phases.values() for p in ph)
+
+
+def _client_proc_fin(port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.client import FLClient
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import RcclAggregator
+    from fakes import FakeTrainer
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=1, register_window_s=20, ready_stall_s=0,
+                   poll_period_s=0.05, long_poll_s=1.0, max_rounds=3, client_weight_file="", rpc_timeout_s=60)
+    table = ParamTable()
+    tr = FakeTrainer(table, 1.0, n_samples=10, sleep_s=1.5)
+    c = FLClient(cfg, lambda: tr, name="c0", target=f"127.0.0.1:{port}",
+                 aggregator_factory=lambda info: RcclAggregator.from_ready_info(info, cfg))
+    st = c.run()
+    e = table.entries[0]
+    q.put((st, float(tr.flat[e.offset]), [h["round"] for h in c.history], list(tr.rounds)))
+
+
+def test_async_report_fin_restores_the_round_average(tmp_path):
+    """Advisor r4: with the asynchronous round report the client trains round r+1 before it learns the server's
+    answer to round r. When that answer is FIN (here: the server ends the run after round 1 although it advertised
+    3 rounds), the extra round is dropped from the history and the client ends at round 1's global model."""
+    from crack_detection_federatedlearning_grpc_amd.config import FLConfig
+    from crack_detection_federatedlearning_grpc_amd.fl.server import FLServer
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    cfg = FLConfig(device="cpu", data_plane="rccl", num_clients=1, register_window_s=20, ready_stall_s=0,
+                   max_rounds=3, work_dir=str(tmp_path), server_weight_file="", long_poll_s=1.0)
+    srv = FLServer(cfg, global_flat=np.zeros(table.total, np.float32), table=table)
+    port = srv.start(0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_client_proc_fin, args=(port, q))
+    p.start()
+    try:
+        assert srv.state.wait_window_closed(60) == 1
+        srv.state.max_rounds = 1                  # the run ends at round 1 (after the READY advertised 3)
+        st, final, hist, trained = q.get(timeout=120)
+    finally:
+        p.join(30)
+        srv.stop()
+    assert st == "FIN"
+    assert trained == [1, 2]                      # round 2 trained while round 1's report was pending ...
+    assert hist == [1]                            # ... and was dropped
+    assert np.isclose(final, 1.0)                 # the client ends at round 1's average (1 rank: its model)
+    assert np.isclose(srv.state.global_flat[table.entries[0].offset], 1.0)
