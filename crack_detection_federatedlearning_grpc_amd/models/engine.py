@@ -751,6 +751,13 @@ class UNetEngine:
         if lo < 0 or hi >= self.n_data:
             raise ValueError(f"idx holds [{lo}, {hi}] but the bound dataset has {self.n_data} images")
 
+    def check_fixed_point(self) -> None:
+        """Deterministic mode: raise if any fixed-point reduction add was clamped (a partial sum beyond the
+        documented bounds of common.h red_add, or a NaN) since the mode was set - the totals are then wrong."""
+        if self.det and self.C.fx_overflow():
+            raise FloatingPointError("deterministic-mode fixed-point reduction overflowed (clamped at 2^62): the "
+                                     "step's statistics / gradients exceed the int64 range at their scale")
+
     def _check_det(self) -> None:
         if self.C.det() != int(self.det):
             raise RuntimeError(f"engine built for deterministic={self.det} but the process mode is "
@@ -1017,6 +1024,7 @@ class HipBackend:
         for _ in range(dev_b.shape[0]):
             e.train_step(self.use_graph)
         m = e.read_metrics("train")
+        e.check_fixed_point()
         if e.dice:
             m["loss"] = m["loss"] + m["dice_sum"] / max(1, len(batches))
         return m

@@ -887,6 +887,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(), py::arg("bwd_reps") = 1,
         py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(), py::arg("bwd_dbeta") = py::none());
   m.def("make_grad_finish_table", &make_grad_finish_table);
+  m.def("fx_overflow", []() {
+    const int r = cfl_fx_overflow();
+    ok(r == 3 ? 3 : 0, "fx_overflow");
+    return r;
+  }, "1 if a deterministic-mode fixed-point add was clamped since the last set_det (common.h red_add)");
   m.def("set_det", [](int v) { ok(cfl_det_set(v), "set_det"); },
         "deterministic reduction mode (int64 fixed-point cross-block sums) on / off; before any graph capture");
   m.def("det", []() { return cfl_det_host(); });

@@ -133,24 +133,41 @@ CFL_DEVICE int imax(int a, int b) { return a > b ? a : b; }
 // any graph capture). The host copy (cfl_det_host) sizes grad_finish's work split.
 namespace {
 __constant__ int g_cfl_det;
+__device__ unsigned int g_cfl_fx_ovf;   // set when a fixed-point add fell outside +-2^62 (clamped)
 }
 #define CFL_FX_S0 16777216.0
 #define CFL_FX_S1 65536.0
 #define CFL_FX_G 1099511627776.0
 CFL_DEVICE bool cfl_det() { return g_cfl_det != 0; }
 // element i of a reduction buffer += v: a float atomic, or (deterministic) an int64 fixed-point atomic at `scale`
+// A fixed-point add beyond +-2^62 (a partial sum past the documented bounds, or a NaN / inf) would make the int64
+// conversion undefined and the total silently wrong: it is clamped (NaN -> 0) and the TU's overflow flag raised
+// (read by cfl_fx_overflow(); the engine checks it after deterministic-mode rounds).
 CFL_DEVICE void red_add(float* buf, size_t i, float v, double scale) {
-  if (cfl_det())
-    atomicAdd(reinterpret_cast<unsigned long long*>(buf) + i, (unsigned long long)__double2ll_rn((double)v * scale));
-  else
+  if (cfl_det()) {
+    constexpr double kFxMax = 4611686018427387904.0;     // 2^62
+    double q = (double)v * scale;
+    if (!(fabs(q) <= kFxMax)) {
+      q = q > 0.0 ? kFxMax : (q < 0.0 ? -kFxMax : 0.0);
+      atomicOr(&g_cfl_fx_ovf, 1u);
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(buf) + i, (unsigned long long)__double2ll_rn(q));
+  } else {
     atomicAdd(buf + i, v);
+  }
 }
 // raw int64 element i of a deterministic-mode reduction buffer
 CFL_DEVICE long long red_raw(const float* buf, size_t i) { return reinterpret_cast<const long long*>(buf)[i]; }
 CFL_DEVICE float red_fx(long long q, double scale) { return (float)((double)q / scale); }
 // scale of the epilogue sums of a BN layer's statistics (st 0: sums, 1: sums of squares) or of node sums
 CFL_DEVICE double red_scale(bool stats, int st) { return stats ? (st ? CFL_FX_S1 : CFL_FX_S0) : CFL_FX_G; }
+// v >= 0: set this TU's mode flag and clear its overflow flag (0 ok, 3 error); v < 0: read the overflow flag
+// (0 clear, 1 raised, 3 error)
 static inline int cfl_det_upload(int v) {
+  unsigned int f = 0;
+  if (v < 0)
+    return hipMemcpyFromSymbol(&f, HIP_SYMBOL(g_cfl_fx_ovf), sizeof(f)) == hipSuccess ? (f ? 1 : 0) : 3;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_fx_ovf), &f, sizeof(f)) != hipSuccess) return 3;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_det), &v, sizeof(int)) == hipSuccess ? 0 : 3;
 }
 

@@ -524,6 +524,7 @@ void cfl_set_tune(int key, int value);
 // capture: the flag is read by the kernels at run time, so captured graphs follow the value at their replay) and the
 // host copy; 0 on success
 int cfl_det_set(int v);
+int cfl_fx_overflow();
 int cfl_det_host();
 int cfl_det_upload_bn(int v);
 int cfl_det_upload_conv3x3(int v);
