@@ -887,6 +887,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bwd_ab") = py::none(), py::arg("bwd_sums") = py::none(), py::arg("bwd_reps") = 1,
         py::arg("bwd_dx") = py::none(), py::arg("bwd_dgamma") = py::none(), py::arg("bwd_dbeta") = py::none());
   m.def("make_grad_finish_table", &make_grad_finish_table);
+  m.def("mfma_scale_probe", [](at::Tensor a, at::Tensor b, at::Tensor sa, at::Tensor sb, int shape) {
+    TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kInt && a.numel() == 512 && b.numel() == 512 &&
+                sa.numel() == 64 && sb.numel() == 64 && b.scalar_type() == at::kInt, "mfma_scale_probe operands");
+    auto d = at::zeros({64, shape == 16 ? 4 : 16}, a.options().dtype(at::kFloat));
+    ok(mfma_scale_probe(a.data_ptr<int>(), b.data_ptr<int>(), sa.data_ptr<int>(), sb.data_ptr<int>(),
+                        d.data_ptr<float>(), shape, stream()), "mfma_scale_probe");
+    return d;
+  }, "one block-scaled fp8 MFMA (16: 16x16x128, 32: 32x32x64) on raw lane registers");
   m.def("fx_overflow", []() {
     const int r = cfl_fx_overflow();
     ok(r == 3 ? 3 : 0, "fx_overflow");
@@ -926,6 +934,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_LIST") = (int)TUNE_WGRAD_MIX_LIST;
   m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
   m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
+  m.attr("TUNE_WGRAD3_SK") = (int)TUNE_WGRAD3_SK;
+  m.attr("TUNE_WGRAD3_SK_MINTILES") = (int)TUNE_WGRAD3_SK_MINTILES;
   m.attr("TUNE_HEAD_BLOCKS") = (int)TUNE_HEAD_BLOCKS;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;

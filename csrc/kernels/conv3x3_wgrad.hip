@@ -20,6 +20,7 @@
 #include "launch.h"
 
 #include "wgrad3_body.h"
+#include "wgrad3_sk_body.h"
 
 namespace {
 
@@ -55,7 +56,22 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_group_kernel(const Wgrad3
   wgrad3_body<BNO, TR>(I.p, I.tiles, I.splits, bx, r % I.gy, r / I.gy, smem);
 }
 
+template <bool TR>
+__global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_sk_kernel(WgradParams p, int tiles_total, int splits) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wg3s::LDS_BYTES];
+  wg3s::wgrad3sk_body<TR>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
 }  // namespace
+
+// the split-K-in-block body (wgrad3_sk_body.h) for this halo wgrad? TUNE_WGRAD3_SK: 1 = never, 2 = every halo
+// wgrad, 0 / 3 = maps <= 64^2 (the levels whose combo-split blocks walk 32 serial tiles)
+static bool wgrad3_sk_use(const WgradParams& p) {
+  const int v = cfl_tune(TUNE_WGRAD3_SK);
+  if (v == 1) return false;
+  if (p.Cin % wg3s::CB || p.N % wg3s::NB) return false;
+  return v == 2 || p.Ho * p.Wo <= 64 * 64;
+}
 
 bool conv3x3_wgrad_supported(const WgradParams& p) {
   return p.ks == 3 && p.stride == 1 && p.pad_t == 1 && p.pad_l == 1 && p.Cin % CB == 0 && p.N % 32 == 0 &&
@@ -63,8 +79,17 @@ bool conv3x3_wgrad_supported(const WgradParams& p) {
 }
 
 void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits) {
-  bno = p.N % 64 == 0 ? 64 : 32;
   tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
+  if (wgrad3_sk_use(p)) {
+    // split-K-in-block body: 32 x 32 x 9-tap block tiles; pixel splits for ~16 tiles per block (each split is one
+    // plain-stored slab row that grad_finish reads)
+    bno = wg3s::NB;
+    const int mt = cfl_tune(TUNE_WGRAD3_SK_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_SK_MINTILES) : 16;
+    splits = (tiles + mt - 1) / mt;
+    if (splits < 1) splits = 1;
+    return;
+  }
+  bno = p.N % 64 == 0 ? 64 : 32;
   const int xy = (p.Cin / CB) * (p.N / bno);
   const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 512;
   // >= 16 pixel tiles per block: the engine launches the decoder's halo wgrads grouped (conv3x3_wgrad_grouped), so
@@ -90,12 +115,16 @@ int conv3x3_wgrad_splits(const WgradParams& p) {
   return splits;
 }
 
-// tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>
+// tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>; split-K-in-block
+// body: 4 = TR, 5 = HWIO
 int conv3x3_wgrad_config(const WgradParams& p) {
+  if (wgrad3_sk_use(p)) return p.dst_mode == 1 ? 4 : 5;
   int bno, tiles, splits;
   conv3x3_wgrad_shape(p, bno, tiles, splits);
   return (bno == 64 ? 0 : 2) + (p.dst_mode == 1 ? 0 : 1);
 }
+
+int conv3x3_wgrad(const WgradParams& p, hipStream_t st);
 
 // n problems of ONE tile config (conv3x3_wgrad_config) in grouped launches of up to WG_MAX
 int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
@@ -109,6 +138,11 @@ int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
       conv3x3_wgrad_shape(p, bno, tiles, splits);
       if (p.slabs > 0 && p.slabs != splits) return 2;
       const int c = conv3x3_wgrad_config(p);
+      if (c >= 4) {                                   // split-K-in-block body: launched on its own
+        const int rc = conv3x3_wgrad(p, st);
+        if (rc) return rc;
+        continue;
+      }
       if (cfg >= 0 && c != cfg) return 4;
       cfg = c;
       Wgrad3Item& it = g.it[g.n++];
@@ -120,6 +154,7 @@ int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
       it.block0 = blocks;
       blocks += it.gx * it.gy * splits;
     }
+    if (g.n == 0) continue;
     switch (cfg) {
       case 0: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<64, true>), dim3(blocks), dim3(NT), 0, st, g); break;
       case 1: hipLaunchKernelGGL((conv3x3_wgrad_group_kernel<64, false>), dim3(blocks), dim3(NT), 0, st, g); break;
@@ -138,6 +173,11 @@ int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {
   if (p.slabs > 0 && p.slabs != splits) return 2;
   dim3 grid(p.Cin / CB, p.N / bno, splits);
   const bool tr = p.dst_mode == 1;
+  if (wgrad3_sk_use(p)) {
+    if (tr) hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<true>), grid, dim3(NT), 0, st, p, tiles, splits);
+    else hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<false>), grid, dim3(NT), 0, st, p, tiles, splits);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   if (bno == 64 && tr) hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, true>), grid, dim3(NT), 0, st, p, tiles, splits);
   else if (bno == 64) hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, false>), grid, dim3(NT), 0, st, p, tiles, splits);
   else if (tr) hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, true>), grid, dim3(NT), 0, st, p, tiles, splits);

@@ -516,7 +516,10 @@ enum TuneKey {
                                //   3 = halo items first
   TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
   // 47: retired (opt_step timing knob without its ticket; the training step no longer uses the ticket)
-  TUNE_N = 48
+  TUNE_WGRAD3_SK = 48,         // halo wgrad split-K-in-block body (wgrad3_sk_body.h): 0 = default (maps <= 64^2), 1 = off,
+                               //   2 = every halo wgrad
+  TUNE_WGRAD3_SK_MINTILES = 49, // ... min 128-pixel tiles per block (default 16)
+  TUNE_N = 50
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
@@ -524,6 +527,9 @@ void cfl_set_tune(int key, int value);
 // capture: the flag is read by the kernels at run time, so captured graphs follow the value at their replay) and the
 // host copy; 0 on success
 int cfl_det_set(int v);
+// one scaled fp8 MFMA on raw lane registers (fp8.hip): a, b [64][8] int32, sa, sb [64], d [64][4] (16x16x128) or
+// [64][16] (32x32x64)
+int mfma_scale_probe(const int* a, const int* b, const int* sa, const int* sb, float* d, int shape, hipStream_t st);
 int cfl_fx_overflow();
 int cfl_det_host();
 int cfl_det_upload_bn(int v);
@@ -536,6 +542,7 @@ int cfl_det_upload_conv_wgrad(int v);
 int cfl_det_upload_datagen(int v);
 int cfl_det_upload_dwconv(int v);
 int cfl_det_upload_entry(int v);
+int cfl_det_upload_fp8(int v);
 int cfl_det_upload_head(int v);
 int cfl_det_upload_optim(int v);
 int cfl_det_upload_pool_add(int v);

@@ -501,7 +501,7 @@ int cfl_det_host() { return g_det_host; }
 static int (*const g_det_up[])(int) = {cfl_det_upload_bn, cfl_det_upload_conv3x3, cfl_det_upload_conv3x3_deep,
                             cfl_det_upload_conv3x3_sk, cfl_det_upload_conv3x3_wgrad, cfl_det_upload_conv_igemm,
                             cfl_det_upload_conv_wgrad, cfl_det_upload_datagen, cfl_det_upload_dwconv,
-                            cfl_det_upload_entry, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
+                            cfl_det_upload_entry, cfl_det_upload_fp8, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
                             cfl_det_upload_pw, cfl_det_upload_sepconv};
 // 1 if any TU's fixed-point overflow flag is raised (cleared by cfl_det_set), 0 if none, 3 on a copy error
 int cfl_fx_overflow() {
@@ -518,7 +518,7 @@ int cfl_det_set(int v) {
   int (*const up[])(int) = {cfl_det_upload_bn, cfl_det_upload_conv3x3, cfl_det_upload_conv3x3_deep,
                             cfl_det_upload_conv3x3_sk, cfl_det_upload_conv3x3_wgrad, cfl_det_upload_conv_igemm,
                             cfl_det_upload_conv_wgrad, cfl_det_upload_datagen, cfl_det_upload_dwconv,
-                            cfl_det_upload_entry, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
+                            cfl_det_upload_entry, cfl_det_upload_fp8, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
                             cfl_det_upload_pw, cfl_det_upload_sepconv};
   for (auto f : up)
     if (f(v)) return 3;

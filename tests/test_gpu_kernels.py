@@ -719,6 +719,70 @@ def test_conv3x3_halo_wgrad_matches_generic_and_autograd(B, Hs, Cin, N, up, use_
     assert rel(outs[1].view(w.shape), w.grad) < 1e-2
 
 
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,dst_mode", [
+    (2, 16, 256, 256, 0, True, 1),   # the 16^2 decoder ConvT shape (Cin 256 -> N 256)
+    (2, 16, 256, 128, 1, True, 1),   # upsampled 16^2 -> 32^2 (Cin 256 -> N 128)
+    (3, 6, 32, 64, 1, True, 1),      # ragged 12x12 output
+    (2, 20, 96, 96, 0, False, 0),    # Keras HWIO layout, ragged rows and columns, 3 channel chunks
+])
+def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
+    """The split-K-in-block halo weight gradient (wgrad3_sk_body.h, TUNE_WGRAD3_SK = 2) against the combo-split
+    body (TUNE_WGRAD3_SK = 1) and fp32 autograd; its slab rows (one per pixel split, plain stores) summed by
+    grad_finish equal the direct (atomic) result, and in the deterministic mode two runs are bit-identical."""
+    torch.manual_seed(29)
+    C_ = hip()
+    Ho = Hs * (2 if up else 1)
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, N))
+    ab, a, b = ab_for(Cin, 15)
+    abd = ab.to(DEV) if use_ab else None
+    K = 9 * Cin
+    outs = {}
+    try:
+        for sk in (1, 2):
+            C_.set_tune(C_.TUNE_WGRAD3_SK, sk)
+            dw = torch.zeros(K * N, device=DEV)
+            C_.conv_wgrad(xb, dyb, dw, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0)
+            outs[sk] = dw.cpu()
+        assert rel(outs[2], outs[1]) < 2e-3
+        # slab rows of the sk body (TUNE_WGRAD3_SK_MINTILES = 1: one pixel tile per split, the most rows)
+        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 1)
+        rows, plain = C_.conv_wgrad_slabs(B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1)
+        assert plain and rows == B * ((Ho + 7) // 8) * ((Ho + 15) // 16)
+        slab = torch.full((rows * K * N,), float("nan"), device=DEV)       # plain rows overwrite all
+        C_.conv_wgrad(xb, dyb, slab, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0, 0, rows)
+        dst = torch.zeros(K * N, device=DEV)
+        table, work = C_.make_grad_finish_table([(slab, dst, K * N, rows, C_.GF_SUM)])
+        C_.grad_finish(table, 1, work)
+        assert rel(dst.cpu(), outs[2]) < 1e-5
+        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 0)
+        # deterministic mode: int64 fixed-point atomics, bitwise reproducible
+        C_.set_det(1)
+        det = []
+        for _ in range(2):
+            d = torch.zeros(2 * K * N, device=DEV)
+            C_.conv_wgrad(xb, dyb, d, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0)
+            det.append(d.view(torch.int64).cpu())
+        assert torch.equal(det[0], det[1])
+        assert rel(det[0].double() / 2.0 ** 40, outs[2].double()) < 1e-5
+    finally:
+        C_.set_det(0)
+        C_.set_tune(C_.TUNE_WGRAD3_SK, 0)
+        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 0)
+    t = (xf * a + b) if use_ab else xf
+    xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    if dst_mode == 1:
+        w = torch.zeros(3, 3, N, Cin, requires_grad=True)
+        out = R.convt_same(xin, w, None)
+    else:
+        w = torch.zeros(3, 3, Cin, N, requires_grad=True)
+        out = R.conv2d_same(xin, w, None, 1)
+    (out.permute(0, 2, 3, 1) * dyf).sum().backward()
+    assert rel(outs[2].view(w.shape), w.grad) < 1e-2
+
+
 @pytest.mark.parametrize("ks,stride,up,Cin,N,H", [(3, 1, 0, 64, 64, 16), (3, 1, 1, 32, 32, 8), (1, 1, 0, 32, 64, 8),
                                                   (1, 2, 0, 64, 32, 16), (3, 1, 0, 32, 32, 128)])
 def test_conv_wgrad_slab_rows_sum_to_direct(ks, stride, up, Cin, N, H):

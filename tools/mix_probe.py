@@ -4,6 +4,10 @@ as a whole, with only item k (TUNE_WGRAD_MIX_ONLY) and without item k (TUNE_WGRA
 restricted launches leave the other items' slabs stale.
 
     python tools/mix_probe.py [img] [batch]
+
+Env: CFL_TUNE="KEY=V,..." sets launch knobs (launch.h TuneKey names without TUNE_) before the engine is built (e.g.
+WGRAD3_SK=1 for the combo-split halo body); MIX_ORDER_ONLY=1 stops after the whole-launch timings; MIX_ALONE_ONLY=1
+times each item alone but skips the "mix without it" runs.
 """
 import os
 import sys
@@ -18,6 +22,11 @@ from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  #
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 dev = torch.device("cuda")
+if os.environ.get("CFL_TUNE"):
+    from crack_detection_federatedlearning_grpc_amd._native_loader import hip
+    for kv in os.environ["CFL_TUNE"].split(","):
+        k, v = kv.split("=")
+        hip().set_tune(getattr(hip(), "TUNE_" + k.strip().upper()), int(v))
 table = ParamTable()
 data = make_synthetic_device(max(64, B), S, seed=0)   # every index of the probe batch must be a bound image
 eng = UNetEngine(table, B, S, dev)
@@ -75,6 +84,9 @@ for k in range(n):
     C.set_tune(C.TUNE_WGRAD_MIX_ONLY, k + 1)
     alone = timeit()
     C.set_tune(C.TUNE_WGRAD_MIX_ONLY, 0)
+    if os.environ.get("MIX_ALONE_ONLY"):
+        print(f"item {k:2d}: alone {alone:6.1f} us", flush=True)
+        continue
     C.set_tune(C.TUNE_WGRAD_MIX_SKIP, 1 << k)
     without = timeit()
     C.set_tune(C.TUNE_WGRAD_MIX_SKIP, 0)
