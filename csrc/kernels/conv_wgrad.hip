@@ -489,8 +489,8 @@ static bool mix_ok(const WgradParams& p) {
 
 
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
-  static thread_local WgradParams by_cfg[4][16], gen_cfg[7][32];
-  int cnt[4] = {0, 0, 0, 0}, gcnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  static thread_local WgradParams by_cfg[6][16], gen_cfg[7][32];   // halo configs 0-5 (conv3x3_wgrad_config)
+  int cnt[6] = {0, 0, 0, 0, 0, 0}, gcnt[7] = {0, 0, 0, 0, 0, 0, 0};
   const bool group = cfl_tune(TUNE_WGRAD_GROUP) != 1;
   const bool group1 = group && cfl_tune(TUNE_WGRAD_GROUP) != 2;
   if (group1 && cfl_tune(TUNE_WGRAD_MIX) != 1) {            // default: one mixed launch (plus any odd ones out)
@@ -512,7 +512,7 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
     if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
     if (p.algo != 1 && conv3x3_wgrad_supported(p) && group) {
       const int c = conv3x3_wgrad_config(p);
-      if (cnt[c] == 16) return 5;
+      if (c < 0 || c >= 6 || cnt[c] == 16) return 5;
       by_cfg[c][cnt[c]++] = p;
     } else if (!(p.algo != 1 && conv3x3_wgrad_supported(p)) && group1 && generic_ok(p)) {
       int bko, bno, rm;
@@ -538,7 +538,7 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
     }
     if (rc) return rc;
   }
-  for (int c = 0; c < 4; ++c)
+  for (int c = 0; c < 6; ++c)
     if (cnt[c]) {
       const int rc = conv3x3_wgrad_grouped(by_cfg[c], cnt[c], st);
       if (rc) return rc;
