@@ -67,6 +67,9 @@ def main() -> int:
     ap.add_argument("--deterministic", action="store_true",
                     help="deterministic reduction mode (int64 fixed-point cross-block sums: bitwise-reproducible "
                          "steps; models/engine.py UNetEngine(deterministic=True), env CFL_DETERMINISTIC=1)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="block-scaled fp8 (e4m3, e8m0 per 32 channels) MFMA for every decoder 3x3 conv - ConvT "
+                         "forward and data gradient (csrc/kernels/fp8.hip; BASELINE config 5); env CFL_CONV_DTYPE=fp8")
     ap.add_argument("--tune", default="",
                     help="launch-shape knobs for A/B sweeps, 'KEY=V,...' (csrc/kernels/launch.h TuneKey names without "
                          "the TUNE_ prefix, e.g. WGRAD3_BLOCKS=256); default: the built-in heuristics")
@@ -148,7 +151,8 @@ def main() -> int:
     data = make_synthetic_device(args.samples, args.img, seed=1000 + rank,
                                  split=min(6213, max(args.batch, int(args.samples * 0.7766))))
     det = args.deterministic or os.environ.get("CFL_DETERMINISTIC", "0") == "1"
-    eng = UNetEngine(table, args.batch, args.img, dev, deterministic=det)
+    conv_dtype = "fp8" if args.fp8 or os.environ.get("CFL_CONV_DTYPE") == "fp8" else "bf16"
+    eng = UNetEngine(table, args.batch, args.img, dev, deterministic=det, conv_dtype=conv_dtype)
     eng.bind_data(data.images, data.masks)
     eng.set_flat(table.init_flat(0))                     # same global init on every client
     agg = None
@@ -308,7 +312,8 @@ def main() -> int:
         out = {"metric": "images/sec/node per FL round", "value": round(value, 2), "unit": "images/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(round_s * 1000.0, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-rendered crack masks, random init)",
+               "vs_baseline": None,
+               "dtype": "bf16" if conv_dtype == "bf16" else "fp8 (block-scaled e4m3 decoder 3x3 convs) + bf16", "data": "synthetic (device-rendered crack masks, random init)",
                "wall_clock_per_round_s": round(round_s, 4),
                "ms_per_iteration": round(round_s * 1000.0 / (args.epochs * args.local_steps), 4),
                "val_images_per_round": world * args.epochs * val_steps * args.batch,
@@ -316,7 +321,7 @@ def main() -> int:
                "peak_hbm_gb_per_client": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "dist_backend": (dist.get_backend() if world > 1 else None),
-               "deterministic": det,
+               "deterministic": det, "conv_dtype": conv_dtype,
                **({"fedavg_max_abs_err": fedavg_err} if fedavg_err is not None else {}),
                **fedavg_stats,
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",

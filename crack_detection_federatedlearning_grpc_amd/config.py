@@ -79,6 +79,8 @@ class FLConfig:
     predict_round: int = 5               # client_fit_model.py:235 (cr == 5)
     device: str = "auto"                 # auto | cpu | cuda
     dtype: str = "bf16"                  # activation dtype on the GPU path (fp32 master weights)
+    conv_dtype: str = "bf16"             # bf16 | fp8: decoder 3x3 convs (ConvT fwd + dgrad) on the block-scaled fp8
+                                         # MFMA (csrc/kernels/fp8.hip; BASELINE config 5)
     use_graph: bool = True               # capture the train step in a hipGraph
     deterministic: bool = False          # int64 fixed-point cross-block reductions: bitwise-reproducible local
                                          # training (models/engine.py; ~1.4-2.7 % slower, profiles/README.md)
@@ -130,6 +132,9 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # config 4: 512x512 large batch, activation memory sized for 288 GB HBM.
     "gpu8-512": dict(device="cuda", img_size=512, batch_size=0, ready_stall_s=0.0, num_clients=8,
                      register_window_s=30.0, data_plane="rccl", poll_period_s=0.5),
+    # config 5: config 4 with the block-scaled fp8 ConvT path (+ the asynchronous RCCL aggregation of every rccl run)
+    "gpu8-512-fp8": dict(device="cuda", img_size=512, batch_size=0, ready_stall_s=0.0, num_clients=8,
+                         register_window_s=30.0, data_plane="rccl", poll_period_s=0.5, conv_dtype="fp8"),
 }
 
 

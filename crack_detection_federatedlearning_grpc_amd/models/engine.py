@@ -48,7 +48,7 @@ class UNetEngine:
     def __init__(self, table: ParamTable, batch: int, img: int, device="cuda", loss: str = "bce",
                  lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-7,
                  bn_momentum: float = 0.99, bn_eps: float = 1e-3, share: Optional["UNetEngine"] = None,
-                 deterministic: Optional[bool] = None):
+                 deterministic: Optional[bool] = None, conv_dtype: Optional[str] = None):
         """``share``: an inference-only engine (see ``evaluator``) reading another engine's parameters and packed
         weights in place (no copy, no repack).
 
@@ -56,13 +56,24 @@ class UNetEngine:
         statistics, BN-backward sums, weight-gradient replica rows, the head's dW / db) accumulates 64-bit
         fixed-point integers instead of float atomics (csrc/kernels/common.h), so replays of the same step are
         bitwise equal. The mode is per PROCESS (each kernel module's constant flag): an engine refuses to step when
-        the process mode differs from its own (its reduction buffers are laid out for one of the two)."""
+        the process mode differs from its own (its reduction buffers are laid out for one of the two).
+
+        ``conv_dtype`` (default: env CFL_CONV_DTYPE, else "bf16"): "fp8" runs every decoder 3x3 convolution - each
+        Conv2DTranspose forward and data gradient - on the block-scaled fp8 MFMA (csrc/kernels/fp8.hip: e4m3 operands,
+        one e8m0 scale per 32 channels of a pixel / weight row, fp32 accumulation; BASELINE config 5). The bf16
+        packed weights stay the source of truth (fp32 master + Adam unchanged): one quant_w8 launch at the start of
+        every step (and of every inference forward) re-quantises the ConvT views."""
         if img % 16:
             raise ValueError("image size must be a multiple of 16")
         self.C = hip()
         if deterministic is None:
             deterministic = share.det if share is not None else os.environ.get("CFL_DETERMINISTIC", "0") == "1"
         self.det = bool(deterministic)
+        if conv_dtype is None:
+            conv_dtype = share.conv_dtype if share is not None else os.environ.get("CFL_CONV_DTYPE", "bf16")
+        if conv_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"conv_dtype must be bf16 or fp8, got {conv_dtype!r}")
+        self.conv_dtype = conv_dtype
         self.C.set_det(1 if self.det else 0)
         self._w = 2 if self.det else 1       # float slots per reduction-buffer element (int64 in the mode)
         self._pending: List[tuple] = []
@@ -95,6 +106,7 @@ class UNetEngine:
         self.lr_buf = torch.zeros(1, dtype=torch.float32, device=dev)    # the step's Adam rate (_zero_step)
         self.ws = torch.zeros(0, dtype=torch.float32, device=dev)     # split-K workspace
         self._build_pack()
+        self._build_fp8()
         self._alloc()
         # the optimizer tail (Adam + BN moving statistics + bf16 repack + step / cursor advance) as ONE opt_step
         # launch (training engines only)
@@ -184,6 +196,34 @@ class UNetEngine:
         self._view_src = {(v[0], ly): v for ly, v in zip([k[0] for k in self.packed_at], views)}
         self._bucket_packs: Dict[Tuple[int, int], object] = {}
         self.n_views, self.max_pack = len(views), max_el
+
+    def _build_fp8(self) -> None:
+        """fp8 mode: e4m3 copies (+ e8m0 scales per 32 K-elements) of every ConvT's two packed views (PK_CONVT for the
+        forward, PK_CONVT_DGRAD for the data gradient), rewritten from the bf16 packs by one quant_w8 launch."""
+        self.w8: Dict[Tuple[str, int], Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._q8 = []
+        if self.conv_dtype != "fp8":
+            return
+        if self._share is not None and getattr(self._share, "w8", None):
+            self.w8, self._q8 = self._share.w8, self._share._q8
+            return
+        for (layer, kind), (off, n) in self.packed_at.items():
+            if kind in (PK_CONVT, PK_CONVT_DGRAD):
+                w8 = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+                s8 = torch.zeros(n // 32, dtype=torch.uint8, device=self.dev)
+                self.w8[(layer, kind)] = (w8, s8)
+                self._q8.append((self.packed[off:off + n], w8, s8))
+
+    def _quant_fp8(self) -> None:
+        if self._q8:
+            self.C.quant_w8(self._q8)
+
+    def _f8(self, layer: str, kind: int) -> Dict[str, torch.Tensor]:
+        """conv_igemm kwargs of a ConvT view's fp8 operands (empty in bf16 mode)."""
+        if not self.w8:
+            return {}
+        w8, s8 = self.w8[(layer, kind)]
+        return {"wt8": w8, "ws8": s8}
 
     def _build_opt(self) -> None:
         """Work items of opt_step (launch.h): 64x64 Adam tiles of every GEMM weight, each writing both bf16 views of
@@ -459,6 +499,7 @@ class UNetEngine:
             if self._pending:
                 self._await_all()
             C.bn_eval_coefs(self.eval_table, len(self.bn_names))
+            self._quant_fp8()
         n = iter(self.names)
         e_conv, e_bn = next(n), next(n)
         st = self.bn[e_bn]["stats"] if train else None
@@ -590,7 +631,8 @@ class UNetEngine:
                         F, 1, 1, 0, 0, 0)
             # dgrad of convT2 with the BN_A node (ReLU mask + sums) fused into its epilogue
             self._igemm(D[f"d{k}_dc"], self.W(t2, PK_CONVT_DGRAD), None, D[f"d{k}_g"], None, None,
-                        0, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1))
+                        0, B, Rk, Rk, F, 0, Rk, Rk, F, 3, 1, 1, 1, node=(A[f"d{k}_c1"], bnA, 1),
+                        **self._f8(t2, PK_CONVT_DGRAD))
             # convT2: input relu(BN_A(c1))
             self._wgrad(A[f"d{k}_c1"], D[f"d{k}_dc"], t2, bnA["ab"], 1, B, Rk, Rk, F, 0, Rk, Rk,
                         F, 3, 1, 1, 1, 1)
@@ -605,7 +647,8 @@ class UNetEngine:
                 pjkw = dict(pj_v=prev_t, pj_add=D[f"d{k}_dres"], pj_out=D[f"d{k}_dprev"], pj_sy=A[f"d{k - 1}_c2"],
                             pj_sab=bprev["ab"], pj_sums=bprev["sums"], pj_reps=self.RS)
             self._igemm(D[f"d{k}_dc2"], self.W(t1, PK_CONVT_DGRAD), None,
-                        D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1, **pjkw)
+                        D[f"d{k}_dxin"], None, None, 0, B, Rk, Rk, F, 0, Rk, Rk, cprev, 3, 1, 1, 1, **pjkw,
+                        **self._f8(t1, PK_CONVT_DGRAD))
             # convT1: input relu(up?(prev))
             self._wgrad(prev_t, D[f"d{k}_dc2"], t1, None, 1, B, prevres, prevres, cprev, up, Rk,
                         Rk, F, 3, 1, 1, 1, 1)
@@ -729,7 +772,7 @@ class UNetEngine:
         consumer-side finalize kwargs of the input's BN. (Round 4 removed the fp8 e4m3 forward path: on the
         non-scaled fp8 MFMA, which issues at the bf16 rate on gfx950, it measured slower at 256^2 and 512^2 -
         profiles/README.md.)"""
-        self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra)
+        self._conv(x, layer, PK_CONVT, y, N, 3, 1, up_in, Ho, bias, stats, **extra, **self._f8(layer, PK_CONVT))
 
     def _zero_step(self) -> None:
         """The step's first launch: zero the gradient / statistics spans, select the batch from the bound table,
@@ -766,6 +809,7 @@ class UNetEngine:
     def train_step_eager(self) -> None:
         self._check_det()
         self._zero_step()
+        self._quant_fp8()                    # fp8 mode: the ConvT views of this step's weights
         self.forward(True)
         self.backward()
         self.optimizer_step(advanced=True)
@@ -913,7 +957,8 @@ class UNetEngine:
         if ev is None:
             share = ParamSnapshot(self) if snapshot else self
             ev = UNetEngine(self.table, batch, self.S, self.dev, "bce", self.lr, self.b1, self.b2, self.adam_eps,
-                            self.momentum, self.bn_eps, share=share, deterministic=self.det)
+                            self.momentum, self.bn_eps, share=share, deterministic=self.det,
+                            conv_dtype=self.conv_dtype)
             ev.snap = share if snapshot else None
             if self.images is not None:
                 ev.bind_data(self.images, self.masks)
@@ -995,7 +1040,8 @@ class HipBackend:
         self.table = table
         self.eng = UNetEngine(table, cfg.batch_size, data.img_size, "cuda", cfg.loss, cfg.lr, cfg.beta1, cfg.beta2,
                               cfg.adam_eps, cfg.bn_momentum, cfg.bn_eps,
-                              deterministic=True if getattr(cfg, "deterministic", False) else None)
+                              deterministic=True if getattr(cfg, "deterministic", False) else None,
+                              conv_dtype=getattr(cfg, "conv_dtype", None) or None)
         images = data.images if isinstance(data.images, torch.Tensor) else torch.as_tensor(data.images)
         masks = data.masks if isinstance(data.masks, torch.Tensor) else torch.as_tensor(data.masks)
         self.eng.bind_data(images.to(self.eng.dev), masks.to(self.eng.dev))

@@ -134,7 +134,8 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
                    OptT bwd_dbeta, OptT pj_v, OptT pj_add, OptT pj_out, OptT pj_sy, OptT pj_sab, OptT pj_sums,
                    int pj_reps, OptT jfin_stats, OptT jfin_gamma, OptT jfin_beta, double jfin_count,
                    double jfin_eps, OptT xfin_stats, OptT xfin_gamma, OptT xfin_beta, double xfin_count,
-                   double xfin_eps, OptT sum2x2, py::object side_bba, py::object side_pool) {
+                   double xfin_eps, OptT sum2x2, py::object side_bba, py::object side_pool, OptT wt8,
+                   OptT ws8) {
   ConvParams p{};
   p.algo = algo;
   p.x = ptr<const bf16_t>(x, "x");
@@ -218,6 +219,15 @@ void conv_igemm_op(at::Tensor x, at::Tensor wt, OptT bias, at::Tensor y, OptT st
     p.sum2x2 = ptr<const bf16_t>(*sum2x2, "sum2x2");
   }
   p.side = side_job(side_bba, side_pool);
+  if (wt8) {                        // block-scaled fp8 operands of a 3x3 conv (fp8.hip)
+    TORCH_CHECK(ws8 && wt8->scalar_type() == at::kByte && ws8->scalar_type() == at::kByte &&
+                wt8->numel() >= (int64_t)N * p.K && ws8->numel() >= (int64_t)N * (p.K / 32),
+                "conv_igemm: wt8 [N][K] e4m3 bytes with ws8 [N][K/32] e8m0 scales");
+    p.wt8 = ptr<const uint8_t>(*wt8, "wt8");
+    p.ws8 = ptr<const uint8_t>(*ws8, "ws8");
+    TORCH_CHECK(conv3x3_f8_supported(p), "conv_igemm: fp8 operands need a 3x3 / stride-1 conv, Cin % 32 == 0, "
+                "Cin <= 256, N % 32 == 0, no BN-backward fold");
+  }
   ok(conv_igemm(p, stream()), "conv_igemm");
 }
 
@@ -840,7 +850,26 @@ PYBIND11_MODULE(_C, m) {
         py::arg("jfin_gamma") = py::none(), py::arg("jfin_beta") = py::none(), py::arg("jfin_count") = 0.0,
         py::arg("jfin_eps") = 1e-3, py::arg("xfin_stats") = py::none(), py::arg("xfin_gamma") = py::none(),
         py::arg("xfin_beta") = py::none(), py::arg("xfin_count") = 0.0, py::arg("xfin_eps") = 1e-3,
-        py::arg("sum2x2") = py::none(), py::arg("side_bba") = py::none(), py::arg("side_pool") = py::none());
+        py::arg("sum2x2") = py::none(), py::arg("side_bba") = py::none(), py::arg("side_pool") = py::none(),
+        py::arg("wt8") = py::none(), py::arg("ws8") = py::none());
+  m.def("quant_w8", [](py::list views) {
+    // [(src bf16 [N][K] as int16, dst uint8 [N][K], scales uint8 [N][K/32]), ...] in ONE launch
+    std::vector<const bf16_t*> src;
+    std::vector<uint8_t*> dst, sc;
+    std::vector<int> nblk;
+    for (auto h : views) {
+      const py::tuple t = h.cast<py::tuple>();
+      TORCH_CHECK(t.size() == 3, "quant_w8: (src, dst, scales)");
+      const at::Tensor a = t[0].cast<at::Tensor>(), d = t[1].cast<at::Tensor>(), c = t[2].cast<at::Tensor>();
+      TORCH_CHECK(a.numel() % 32 == 0 && d.numel() >= a.numel() && c.numel() >= a.numel() / 32 &&
+                  d.scalar_type() == at::kByte && c.scalar_type() == at::kByte, "quant_w8: sizes / dtypes");
+      src.push_back(ptr<const bf16_t>(a, "src"));
+      dst.push_back(ptr<uint8_t>(d, "dst"));
+      sc.push_back(ptr<uint8_t>(c, "scales"));
+      nblk.push_back((int)(a.numel() / 32));
+    }
+    ok(quant_w8(src.data(), dst.data(), sc.data(), nblk.data(), (int)src.size(), stream()), "quant_w8");
+  }, "e4m3 + e8m0-per-32 quantisation of packed bf16 weight views (fp8.hip), one launch");
   m.attr("JOIN_POOL") = (int)JOIN_POOL;
   m.attr("JOIN_ADD") = (int)JOIN_ADD;
   m.attr("JOIN_ADD_UP") = (int)JOIN_ADD_UP;

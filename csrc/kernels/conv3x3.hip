@@ -849,6 +849,7 @@ bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_deep(const ConvParams& p, hipStream_t st);
 
 int conv3x3(const ConvParams& p, hipStream_t st) {
+  if (p.wt8) return conv3x3_f8(p, st);      // block-scaled fp8 operands (fp8.hip)
   if (!conv3x3_supported(p)) return 1;
   if (p.bwd.y) return 6;                    // the BN-backward operand is applied by a separate pass (conv_igemm)
   // low-resolution deep-K layers: K split over the block's waves, 32x32 MFMA register tiles (conv3x3_sk.hip)

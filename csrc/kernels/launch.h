@@ -172,7 +172,12 @@ struct ConvParams {
   const bf16_t* sum2x2;  // optional: x = the 2x2-block sums of this [B, 2*Hin, 2*Win, Cin] gradient (node_bwd
                          // GM_SUM2X2 order), formed on load by the streaming 1x1 kernel and stored into x (const cast)
                          // for the weight gradient; other kernels run node_bwd into x first (same results)
+  const uint8_t* wt8;    // optional fp8 operands of a 3x3 conv (fp8.hip): e4m3 weights [N][K] (quant_w8 of wt) ...
+  const uint8_t* ws8;    // ... and their e8m0 block scales [N][K / 32]; the activations are quantised on load
 };
+bool conv3x3_f8_supported(const ConvParams& p);
+int conv3x3_f8(const ConvParams& p, hipStream_t st);
+int quant_w8(const bf16_t* const* src, uint8_t* const* dst, uint8_t* const* sc, const int* nblk, int n, hipStream_t st);
 int conv_igemm(const ConvParams& p, hipStream_t st);
 // plain 1x1 / stride-1 convs (no input transform, epilogue = bias + optional BN statistics; input optionally formed
 // on load: bwd = BN-backward apply, sum2x2 = 2x2-block sums): streaming MFMA kernel with swapped operands and resident

@@ -1,5 +1,6 @@
 """HIP kernel numerics vs plain fp32 PyTorch references (run on an MI355X via gpurun; marked gpu)."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -15,6 +16,7 @@ from crack_detection_federatedlearning_grpc_amd._native_loader import hip  # noq
 from crack_detection_federatedlearning_grpc_amd.models import unet_ref as R  # noqa: E402
 
 DEV = torch.device("cuda")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PK_CONV, PK_CONV_DGRAD1x1, PK_CONVT, PK_CONVT_DGRAD, PK_PW, PK_PW_DGRAD = range(6)
 
 
@@ -781,6 +783,151 @@ def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
         out = R.conv2d_same(xin, w, None, 1)
     (out.permute(0, 2, 3, 1) * dyf).sum().backward()
     assert rel(outs[2].view(w.shape), w.grad) < 1e-2
+
+
+def test_fp8_scaled_mfma_lane_maps():
+    """The block-scaled fp8 MFMA's operand / scale lane maps the fp8 kernels assume (fp8.hip), on exact small-integer
+    e4m3 data against a host GEMM: 16x16x128 and 32x32x64, unscaled and with random per-32-element e8m0 scales."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fp8_layout", os.path.join(ROOT, "tools", "fp8_layout.py"))
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    rng = np.random.default_rng(1)
+    for shape in (16, 32):
+        K = 128 if shape == 16 else 64
+        A = rng.integers(-4, 5, (shape, K)).astype(np.float64)
+        Bm = rng.integers(-4, 5, (K, shape)).astype(np.float64)
+        sa = rng.integers(124, 131, (shape, K // 32))
+        sb = rng.integers(124, 131, (shape, K // 32))
+        D, ref = L.run(shape, A, Bm, sa, sb)
+        assert np.array_equal(D, ref), (shape, np.abs(D - ref).max())
+
+
+def _quant_w8(wb, N, K):
+    C_ = hip()
+    w8 = torch.zeros(N * K, dtype=torch.uint8, device=DEV)
+    s8 = torch.zeros(N * K // 32, dtype=torch.uint8, device=DEV)
+    C_.quant_w8([(wb, w8, s8)])
+    return w8, s8
+
+
+def test_quant_w8_roundtrip():
+    """quant_w8: e4m3 bytes x 2^(e - 127) per 32-element block reproduce torch's e4m3 rounding of the block scaled
+    by the same power of two; every block's largest magnitude lands in (224, 448]."""
+    torch.manual_seed(41)
+    N, K = 64, 9 * 96
+    w = torch.randn(N, K) * torch.logspace(-3, 1, N)[:, None]
+    wb = w.to(torch.bfloat16).view(torch.int16).contiguous().to(DEV)
+    w8, s8 = _quant_w8(wb, N, K)
+    e = s8.cpu().long().view(N, K // 32) - 127
+    q = w8.cpu().view(torch.float8_e4m3fn).float().view(N, K // 32, 32)
+    deq = (q * torch.pow(2.0, e.double()).float()[..., None]).view(N, K)
+    wref = w.to(torch.bfloat16).float()
+    scaled = (wref.view(N, K // 32, 32) / torch.pow(2.0, e.double()).float()[..., None])
+    assert torch.equal(q, scaled.to(torch.float8_e4m3fn).float())
+    amax = q.abs().amax(-1)
+    assert bool(((amax > 224) & (amax <= 448)).all())
+    assert rel(deq, wref) < 0.04
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,S", [
+    (2, 16, 64, 32, 0, True, 1),     # N = 32: 4 x 1 waves
+    (2, 8, 32, 64, 1, False, 1),     # upsampled input, Cin 32 (one chunk)
+    (2, 12, 128, 128, 0, True, 1),   # ragged 12 x 12 output, 4 chunks
+    (1, 16, 256, 64, 0, True, 16),   # Cin 256 (8 chunks)
+])
+def test_conv3x3_fp8_matches_fp32(B, Hs, Cin, N, up, use_ab, S):
+    """fp8 3x3 conv (block-scaled e4m3 operands, fp32 accumulation; fp8.hip) vs the fp32 conv of the same bf16
+    inputs: the error is the e4m3 rounding of both operands (3 mantissa bits, per-32 scales): rel. L2 < 5e-2, and the
+    fused BN statistics equal the statistics of the stored output."""
+    torch.manual_seed(43)
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    wk = torch.randn(3, 3, N, Cin) * 0.03
+    wb = pack(PK_CONVT, wk, 3, Cin, N)
+    ab, a, b = ab_for(Cin, 16)
+    Ho = Hs * (2 if up else 1)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    w8, s8 = _quant_w8(wb, N, 9 * Cin)
+    y = torch.zeros(B, Ho, Ho, N, dtype=torch.int16, device=DEV)
+    stats = torch.zeros(hip().STAT_REPLICAS * 2 * N, device=DEV)
+    hip().conv_igemm(xb, wb, bias, y, stats, ab.to(DEV) if use_ab else None, 1, B, Hs, Hs, Cin, up, Ho, Ho, N,
+                     3, 1, 1, 1, None, 0, wt8=w8, ws8=s8)
+    out = from_bits(y)
+    t = xf * a + b if use_ab else xf
+    xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    ref = R.convt_same(xin, wk.to(torch.bfloat16).float(), bias.cpu()).permute(0, 2, 3, 1)
+    assert rel(out, ref) < 5e-2, rel(out, ref)
+    st = stats.view(-1, 2, N).sum(0).cpu()
+    assert torch.allclose(st[0], out.sum((0, 1, 2)), rtol=1e-3, atol=5e-2)
+    assert torch.allclose(st[1], (out * out).sum((0, 1, 2)), rtol=1e-3, atol=5e-2)
+
+
+def test_conv3x3_fp8_dgrad_node_epilogue():
+    """fp8 3x3 data gradient with the fused BN-node epilogue (ReLU mask + BN-backward sums; the ConvT2 dgrad form)
+    against the bf16 kernel's identical call: outputs agree to the e4m3 rounding, the node sums likewise."""
+    torch.manual_seed(47)
+    C_ = hip()
+    B, H, F = 2, 16, 64
+    gb, _ = bf(torch.randn(B, H, H, F))
+    wk = torch.randn(3, 3, F, F) * 0.05
+    wd = pack(PK_CONVT_DGRAD, wk, 3, F, F)
+    yb, _ = bf(torch.randn(B, H, H, F))
+    ab, _, _ = ab_for(F, 17)
+    ab[3 * F:] = torch.rand(F) + 0.5
+    ab[2 * F:3 * F] = torch.randn(F) * 0.1
+    w8, s8 = _quant_w8(wd, F, 9 * F)
+    outs = []
+    for f8 in (False, True):
+        g = torch.zeros(B, H, H, F, dtype=torch.int16, device=DEV)
+        sums = torch.zeros(4 * 2 * F, device=DEV)
+        kw = dict(wt8=w8, ws8=s8) if f8 else {}
+        C_.conv_igemm(gb, wd, None, g, None, None, 0, B, H, H, F, 0, H, H, F, 3, 1, 1, 1, None, 0,
+                      node_y=yb, node_ab=ab.to(DEV), node_sums=sums, node_reps=4, node_relu=1, **kw)
+        outs.append((from_bits(g), sums.view(4, 2, F).sum(0).cpu()))
+    (g0, s0), (g1, s1) = outs
+    assert rel(g1, g0) < 5e-2
+    assert torch.equal(g1 == 0, g0 == 0) or float(((g1 == 0) != (g0 == 0)).float().mean()) < 1e-3   # same mask
+    assert rel(s1, s0) < 8e-2
+
+
+def test_engine_fp8_step_tracks_bf16():
+    """UNetEngine(conv_dtype="fp8"): every decoder 3x3 conv (ConvT forward + dgrad) on the fp8 kernels. One training
+    step from the same state: the loss within 2 % of the bf16 engine's, the gradient direction kept (cosine > 0.97,
+    per ConvT kernel > 0.9), the inference forward runs on fp8 too."""
+    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
+    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    table = ParamTable()
+    data = make_synthetic_device(8, 64, seed=9)
+    flat = table.init_flat(9)
+    res = {}
+    for dt in ("bf16", "fp8"):
+        eng = UNetEngine(table, 4, 64, conv_dtype=dt)
+        assert bool(eng.w8) == (dt == "fp8")
+        eng.bind_data(data.images, data.masks)
+        eng.set_flat(flat)
+        eng.idx.copy_(torch.arange(4, dtype=torch.int32, device=DEV))
+        eng._zero_step()
+        eng._quant_fp8()
+        eng.forward(True)
+        eng.backward()
+        loss = eng.read_metrics("train")["loss"]
+        ev = eng.evaluator(8)
+        ev.idx.copy_(torch.arange(8, dtype=torch.int32, device=DEV))
+        ev.eval_step(use_graph=False)
+        res[dt] = (loss, eng.grad.clone(), ev.read_metrics("eval")["loss"], eng)
+    (l0, g0, e0, eng0), (l1, g1, e1, eng1) = res["bf16"], res["fp8"]
+    assert abs(l1 - l0) / l0 < 0.02 and abs(e1 - e0) / e0 < 0.05, (l0, l1, e0, e1)
+    cos = float((g0 * g1).sum() / (g0.norm() * g1.norm()))
+    assert cos > 0.97, cos
+    for ly in table.weighted_layers():
+        if ly.kind == "convt":
+            e = table.entry(ly.name, "kernel")
+            a, b = g0[e.offset:e.offset + e.size], g1[e.offset:e.offset + e.size]
+            c = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+            assert c > 0.9, (ly.name, c)
 
 
 @pytest.mark.parametrize("ks,stride,up,Cin,N,H", [(3, 1, 0, 64, 64, 16), (3, 1, 1, 32, 32, 8), (1, 1, 0, 32, 64, 8),
