@@ -332,28 +332,28 @@ __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
     }
 #pragma unroll 1
     for (int s = 0; s < 5; ++s) {               // (not unrolled: all five steps' fragments in flight spill)
-      const int tap0 = 2 * s + kh;
-      const bool live = tap0 < 9;                           // the 10th tap slot: zero weights
-      const int tap = live ? tap0 : 8;
-      const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;
+      const int t0 = 2 * s, t1 = t0 + 1;                  // K-block 0 / 1 of this step
+      const bool live1 = t1 < 9;                          // the 10th tap slot: zero weights
+      const int t1c = live1 ? t1 : t0;
+      const int ky0 = (t0 * 11) >> 5, kx0 = t0 - 3 * ky0, ky1 = (t1c * 11) >> 5, kx1 = t1c - 3 * ky1;
       i8v af[FM], bw[FN];
       int sa[FM], sb[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int r = fhp[i] + ky * HW + kx;
-        const uint4 lo = *reinterpret_cast<const uint4*>(sH + f8_off(r, 0));
-        const uint4 hi = *reinterpret_cast<const uint4*>(sH + f8_off(r, 1));
+        const int r0 = fhp[i] + ky0 * HW + kx0, r1 = fhp[i] + ky1 * HW + kx1;
+        const uint4 lo = *reinterpret_cast<const uint4*>(sH + f8_off(r0, kh));
+        const uint4 hi = *reinterpret_cast<const uint4*>(sH + f8_off(r1, kh));
         af[i] = i8v{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-        sa[i] = sHs[r];
+        sa[i] = sHs[kh ? r1 : r0];
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int r = tap * BN_ + bcol + j * 32;
-        const uint4 lo = *reinterpret_cast<const uint4*>(sW + f8_off(r, 0));
-        const uint4 hi = *reinterpret_cast<const uint4*>(sW + f8_off(r, 1));
-        bw[j] = live ? i8v{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w}
-                     : i8v{0, 0, 0, 0, 0, 0, 0, 0};
-        sb[j] = sWs[r];
+        const int n = bcol + j * 32, w0 = t0 * BN_ + n, w1 = t1c * BN_ + n;
+        const uint4 lo = *reinterpret_cast<const uint4*>(sW + f8_off(w0, kh));
+        uint4 hi = *reinterpret_cast<const uint4*>(sW + f8_off(w1, kh));
+        if (!live1) hi = make_uint4(0, 0, 0, 0);
+        bw[j] = i8v{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+        sb[j] = sWs[kh ? w1 : w0];
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)

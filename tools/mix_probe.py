@@ -5,7 +5,7 @@ restricted launches leave the other items' slabs stale.
 
     python tools/mix_probe.py [img] [batch]
 
-Env: CFL_TUNE="KEY=V,..." sets launch knobs (launch.h TuneKey names without TUNE_) before the engine is built (e.g.
+Env: CFL_MIX_TUNE="KEY=V,..." sets launch knobs (launch.h TuneKey names without TUNE_) before the engine is built (e.g.
 WGRAD3_SK=1 for the combo-split halo body); MIX_ORDER_ONLY=1 stops after the whole-launch timings; MIX_ALONE_ONLY=1
 times each item alone but skips the "mix without it" runs.
 """
@@ -22,9 +22,9 @@ from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable  #
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 dev = torch.device("cuda")
-if os.environ.get("CFL_TUNE"):
+if os.environ.get("CFL_MIX_TUNE"):
     from crack_detection_federatedlearning_grpc_amd._native_loader import hip
-    for kv in os.environ["CFL_TUNE"].split(","):
+    for kv in os.environ["CFL_MIX_TUNE"].split(","):
         k, v = kv.split("=")
         hip().set_tune(getattr(hip(), "TUNE_" + k.strip().upper()), int(v))
 table = ParamTable()
