@@ -64,11 +64,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_sk_kernel(WgradParams p, 
 
 }  // namespace
 
-// the split-K-in-block body (wgrad3_sk_body.h) for this halo wgrad? TUNE_WGRAD3_SK: 1 = never, 2 = every halo
-// wgrad, 0 / 3 = maps <= 64^2 (the levels whose combo-split blocks walk 32 serial tiles)
+// the split-K-in-block body (wgrad3_sk_body.h) for this halo wgrad? TUNE_WGRAD3_SK: 0 / 1 = never (default), 2 =
+// every halo wgrad, 3 = maps <= 64^2 (the levels whose combo-split blocks walk 32 serial tiles).
+// Measured (profiles/r5_wgrad/wgrad_ab.txt, tools/mix_probe.py at 256^2 / b16): each <= 64^2 halo item alone 30-32 us
+// instead of 68-70, but the whole mixed launch 196.6 us (16 tiles per block), 208.1 (8), 185.2 (32) against 164.6 us
+// with the combo-split body: a block's 128-pixel tile step costs ~2 us either way (36 or 72 MFMAs per wave per
+// tile), so halving the block tile doubles the block-slot time the slot-bound mixed launch pays. Kept as an option.
 static bool wgrad3_sk_use(const WgradParams& p) {
   const int v = cfl_tune(TUNE_WGRAD3_SK);
-  if (v == 1) return false;
+  if (v <= 1) return false;
   if (p.Cin % wg3s::CB || p.N % wg3s::NB) return false;
   return v == 2 || p.Ho * p.Wo <= 64 * 64;
 }

@@ -521,8 +521,8 @@ enum TuneKey {
                                //   3 = halo items first
   TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
   // 47: retired (opt_step timing knob without its ticket; the training step no longer uses the ticket)
-  TUNE_WGRAD3_SK = 48,         // halo wgrad split-K-in-block body (wgrad3_sk_body.h): 0 = default (maps <= 64^2), 1 = off,
-                               //   2 = every halo wgrad
+  TUNE_WGRAD3_SK = 48,         // halo wgrad split-K-in-block body (wgrad3_sk_body.h): 0 / 1 = off (default; measured
+                               //   slower in the mixed launch), 2 = every halo wgrad, 3 = maps <= 64^2
   TUNE_WGRAD3_SK_MINTILES = 49, // ... min 128-pixel tiles per block (default 16)
   TUNE_N = 50
 };

@@ -748,6 +748,7 @@ def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
             outs[sk] = dw.cpu()
         assert rel(outs[2], outs[1]) < 2e-3
         # slab rows of the sk body (TUNE_WGRAD3_SK_MINTILES = 1: one pixel tile per split, the most rows)
+        C_.set_tune(C_.TUNE_WGRAD3_SK, 2)
         C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 1)
         rows, plain = C_.conv_wgrad_slabs(B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1)
         assert plain and rows == B * ((Ho + 7) // 8) * ((Ho + 15) // 16)
@@ -758,6 +759,7 @@ def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
         C_.grad_finish(table, 1, work)
         assert rel(dst.cpu(), outs[2]) < 1e-5
         C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 0)
+        C_.set_tune(C_.TUNE_WGRAD3_SK, 2)
         # deterministic mode: int64 fixed-point atomics, bitwise reproducible
         C_.set_det(1)
         det = []
