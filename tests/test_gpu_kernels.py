@@ -1735,17 +1735,21 @@ def test_training_parity_vs_plain_fp32():
         assert v >= min(0.85, cos_ac[k] - 0.05), (k, v, cos_ac[k])
     del eng, data
     # trained to segmentation quality, side by side
-    recs = run(img=S, batch=B, steps=1200, every=200, samples=1024, val=128, quiet=True)
+    # the same run also trains the fp8 engine (every decoder 3x3 conv on the block-scaled e4m3 MFMA, BASELINE config
+    # 5) on the same batches: its trained IoU must land within 0.05 of the bf16 engine's (verdict r4 item 4)
+    recs = run(img=S, batch=B, steps=1200, every=200, samples=1024, val=128, quiet=True, fp8=True)
     for r in recs:
         print(json.dumps(r))
     first, last = recs[0], recs[-1]
     te, tr = first["train_loss_engine"], first["train_loss_fp32"]
     assert abs(te - tr) < 0.05 * tr                                         # trajectories coincide early
-    e, f = last["engine"], last["fp32"]
+    e, f, e8 = last["engine"], last["fp32"], last["engine_fp8"]
     assert f["val_iou"] >= 0.5, f"the fp32 oracle does not segment yet: val IoU {f['val_iou']:.3f}"
     assert abs(e["val_iou"] - f["val_iou"]) <= 0.05, (e, f)
     assert abs(e["val_loss"] - f["val_loss"]) <= 0.10 * f["val_loss"], (e, f)
     assert abs(e["val_acc"] - f["val_acc"]) <= 0.005, (e, f)
+    assert abs(e8["val_iou"] - e["val_iou"]) <= 0.05, (e8, e)
+    assert abs(e8["val_loss"] - e["val_loss"]) <= 0.15 * e["val_loss"], (e8, e)
 
 
 @pytest.mark.parametrize("kind,B,H,K,N,s2,off", [
