@@ -849,7 +849,17 @@ bool conv3x3_deep_eligible(const ConvParams& p);
 int conv3x3_deep(const ConvParams& p, hipStream_t st);
 
 int conv3x3(const ConvParams& p, hipStream_t st) {
-  if (p.wt8) return conv3x3_f8(p, st);      // block-scaled fp8 operands (fp8.hip)
+  if (p.wt8) {
+    // block-scaled fp8 operands (fp8.hip). TUNE_CONV3_F8: 0 = default - fp8 unless the bf16 weight-stationary kernel
+    // takes the call (Cin <= 64 at the high-resolution levels, where it beat the fp8 per-tile kernel at 512^2:
+    // profiles/r5_fp8), 1 = never, 2 = every call that carries fp8 operands
+    const int v = cfl_tune(TUNE_CONV3_F8);
+    if (v == 2 || (v == 0 && !ws_eligible(p))) return conv3x3_f8(p, st);
+    ConvParams q = p;
+    q.wt8 = nullptr;
+    q.ws8 = nullptr;
+    return conv3x3(q, st);
+  }
   if (!conv3x3_supported(p)) return 1;
   if (p.bwd.y) return 6;                    // the BN-backward operand is applied by a separate pass (conv_igemm)
   // low-resolution deep-K layers: K split over the block's waves, 32x32 MFMA register tiles (conv3x3_sk.hip)

@@ -18,7 +18,11 @@
 // the current chunk's MFMAs. One 32x32x64 MFMA covers TWO taps of a chunk (k-half h = lane >> 5 of the fragment =
 // tap 2s + h), so a chunk is 5 k-steps (the 10th tap slot has zero weights): 10 % padding against the 2x rate.
 // LDS rows are 32 bytes (a pixel's chunk or a weight row's chunk) with the two 16-byte halves swapped in every other
-// group of 4 rows (conflicts of the 32-lane fragment reads), plus one scale byte per row.
+// group of 8 rows, plus one scale byte per row. Fragment rows are PERMUTED (f8_perm): a ds_read_b128 serves its 64
+// lanes in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, + 32), so fragment row rho of lane l & 31
+// holds pixel / output channel f8_perm(rho), which gives every group 16 CONSECUTIVE rows - with the 8-row half swap,
+// all 64 banks for any start row (tap shifts move it). The first build (natural order, 4-row swap) measured 20-32 %
+// LDS bank conflicts (profiles/r5_fp8/pmc_compare.txt).
 //
 // mfma_scale_probe: one wave runs ONE scaled MFMA on caller-supplied lane registers (32 fp8 bytes of A and of B per
 // lane, one int32 scale word each) and returns the raw accumulator registers - the operand lane maps are checked
@@ -113,8 +117,13 @@ __global__ __launch_bounds__(256) void quant_w8_kernel(const Q8Table t) {
 // ---------------------------------------------------------------- 3x3 / stride-1 / same conv, fp8 operands
 constexpr int F8_NT = 256;
 constexpr int F8_BK = 32;
-// byte offset of 16-byte half h of LDS row r (32-byte rows; halves swapped in every other group of 4 rows)
-CFL_DEVICE int f8_off(int r, int h) { return r * 32 + ((h ^ ((r >> 2) & 1)) << 4); }
+// byte offset of 16-byte half h of LDS row r (32-byte rows; halves swapped in every other group of 8 rows)
+CFL_DEVICE int f8_off(int r, int h) { return r * 32 + ((h ^ ((r >> 3) & 1)) << 4); }
+// fragment row rho (0..31) -> pixel / channel index within the 32-row fragment: the ds_read_b128 lane group
+// {0-3, 12-15, 20-27} gets rows 0..15, {4-11, 16-19, 28-31} rows 16..31
+CFL_DEVICE int f8_perm(int rho) {
+  return rho < 4 ? rho : rho < 12 ? rho + 12 : rho < 16 ? rho - 8 : rho < 20 ? rho + 8 : rho < 28 ? rho - 12 : rho;
+}
 
 template <int TH, int TW, int BN_, int WM, int WN, bool PJ, bool XFIN>
 __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
@@ -267,14 +276,15 @@ __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
 
   // fragment rows: A = pixel (lane & 31) of fragment i, B = output channel (lane & 31) of fragment j; the lane's
   // k-half kh = lane >> 5 is tap 2 s + kh of k-step s
+  const int prow = f8_perm(lane & 31);
   int fhp[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int pp = wm * TM + i * 32 + (lane & 31);
+    const int pp = wm * TM + i * 32 + prow;
     fhp[i] = (pp / TW) * HW + pp % TW;
   }
   const int kh = lane >> 5;
-  const int bcol = wn * TN + (lane & 31);
+  const int bcol = wn * TN + prow;
 
   // decoder node join: this thread's half-resolution pixel (loads in flight during the K loop)
   uint4 pjv = make_uint4(0, 0, 0, 0), pja = pjv, pjy = pjv;
@@ -372,6 +382,7 @@ __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
   }
 
   // ---- epilogue (conv3x3.hip): C map of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  //      (fragment rows / cols in f8_perm order)
   auto out_m = [&](int row, int& m) -> bool {
     const int py = row / TW, px = row % TW;
     const int oy = ty0 + py, ox = tx0 + px;
@@ -381,13 +392,13 @@ __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
   bf16_t (*sC)[LDC] = reinterpret_cast<bf16_t (*)[LDC]>(smem);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int cl = wn * TN + j * 32 + (lane & 31);
+    const int cl = wn * TN + j * 32 + prow;
     const float bias = p.bias ? p.bias[nBlock + cl] : 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        sC[wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][cl] = f2bf(acc[i][j][r] + bias);
+        sC[wm * TM + i * 32 + f8_perm((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5))][cl] = f2bf(acc[i][j][r] + bias);
   }
   __syncthreads();
   constexpr int CG = BN_ / 8, ROWS_PER_PASS = NT / CG;
