@@ -170,8 +170,20 @@ __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) 
 // keeps the kernel at 3 waves per SIMD without spilling.
 namespace dws {
 constexpr int CT = 32, CPT = 4, G = CT / CPT, P = NT / G, SL = 4, TW = 32, SR = P / (TW / SL);
-constexpr int HWp = TW + 2, NRING = 2 * SR + 2, LDP = CT + 8;
+constexpr int HWp = TW + 2, NRING = 2 * SR + 2;
 static_assert(TW * G == NT, "staging map: one thread per (column, channel group) of a row");
+// Ring rows are 34 unpadded 64-byte pixels (x0 - 1 .. x0 + 32), pixel px at position pxo(px) = px ^ ((px >> 2) & 3):
+// a wave reads 8 pixels 4 apart (its threads' 4-pixel strips) x 8 channel groups, and a plain 64-B pixel stride puts
+// those 8 pixels in the same 16 banks; the XOR rotates each group of 4 pixels over all 64 banks (2 passes, the minimum
+// for 512 B), and a wave's staging writes (8 consecutive pixels) stay conflict-free. (The previous 80-byte padded
+// pixels: 13.7 % bank-conflict cycles in dw_stream, 8.8 % in the fused backward, r5_final/pmc_summary.txt.)
+CFL_DEVICE int pxo(int px) { return px ^ ((px >> 2) & 3); }
+// SWZ = false: the 80-byte padded pixels (pixel px at px) - the fused backward's two-ring kernel keeps them: the
+// swizzled offsets cost it 10 registers it does not have (256 VGPRs at 2 blocks per CU: spills)
+template <bool SWZ>
+constexpr int ldp() { return SWZ ? CT : CT + 8; }
+template <bool SWZ>
+CFL_DEVICE int pxs(int px) { return SWZ ? pxo(px) : px; }
 
 CFL_DEVICE void unpack4(const uint2& v, float* f) {
   f[0] = __uint_as_float(v.x << 16);
@@ -240,12 +252,13 @@ CFL_DEVICE uint2 xform4(uint2 t, bool on, const float* a4, const float* b4, int 
   return pack4(f);
 }
 
-template <int NR>
+template <int NR, bool SWZ>
 CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0, bool xform, const float* a4,
                     const float* b4, int relu) {
   const int tid = threadIdx.x, q = tid % G;
   const int slot0 = (row0 + NRING) % NRING;                  // row0 >= -1
-  bf16_t* col = sH + (tid / G) * LDP + q * CPT;
+  constexpr int LDP = ldp<SWZ>();
+  bf16_t* col = sH + pxs<SWZ>(tid / G) * LDP + q * CPT;
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int slot = slot0 + r >= NRING ? slot0 + r - NRING : slot0 + r;
@@ -256,7 +269,7 @@ CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0
     const int re = tid / (2 * G), hxe = TW + (tid % (2 * G)) / G;
     const int slot = slot0 + re >= NRING ? slot0 + re - NRING : slot0 + re;
     const bool ok = (okm >> NR) & 1u;
-    *reinterpret_cast<uint2*>(sH + (slot * HWp + hxe) * LDP + q * CPT) =
+    *reinterpret_cast<uint2*>(sH + (slot * HWp + pxs<SWZ>(hxe)) * LDP + q * CPT) =
         xform4(ok ? v[NR] : make_uint2(0, 0), xform && ok, a4, b4, relu);
   }
 }
@@ -266,6 +279,7 @@ CFL_DEVICE void put(bf16_t* sH, const uint2 (&v)[NR + 1], uint32_t okm, int row0
 template <int MODE>
 CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, int bid, int nblocks) {
   using namespace dws;
+  constexpr int LDP = ldp<true>();
   __shared__ __attribute__((aligned(16))) bf16_t sH[NRING * HWp * LDP];
   __shared__ __attribute__((aligned(16))) float sNode[MODE == 1 ? 4 * CT : 4];   // dgrad node coefficients
 
@@ -325,7 +339,7 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
     uint2 v[SR + 3];
     uint32_t okm;
     fetch<SR + 2>(src_b, p, x0, ybeg - 1, true, v, okm);
-    put<SR + 2>(sH, v, okm, ybeg - 1, has_ab || relu, a4, b4, relu);
+    put<SR + 2, true>(sH, v, okm, ybeg - 1, has_ab || relu, a4, b4, relu);
   }
   // wgrad: this thread's dy strip of the current step (prefetched one step ahead like the halo rows)
   constexpr int NG = MODE == 2 ? SL : 1;
@@ -383,7 +397,7 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
       const int slot = (oy - 1 + ky + NRING) % NRING;
-      const bf16_t* hrow = &sH[(slot * HWp + sc) * LDP + cg * CPT];
+      const bf16_t* hrow = &sH[slot * HWp * LDP + cg * CPT];
       float wt[MODE == 2 ? 1 : 3][4];
       if (MODE != 2) {
 #pragma unroll
@@ -392,7 +406,7 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
 #pragma unroll
       for (int cx = 0; cx < SL + 2; ++cx) {
         float f[4];
-        unpack4(*reinterpret_cast<const uint2*>(hrow + cx * LDP), f);
+        unpack4(*reinterpret_cast<const uint2*>(hrow + pxo(sc + cx) * LDP), f);
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int o = cx - kx;
@@ -433,7 +447,7 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
           *reinterpret_cast<uint2*>(p.y + off0 + (size_t)i * p.C) = v;
         }
     }
-    if (more) put<SR>(sH, cur, curok, a + SR + 1, has_ab || relu, a4, b4, relu);
+    if (more) put<SR, true>(sH, cur, curok, a + SR + 1, has_ab || relu, a4, b4, relu);
     if (MODE == 2) {
 #pragma unroll
       for (int i = 0; i < NG; ++i) gq[i] = gn[i];
@@ -534,6 +548,7 @@ __global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) 
 template <bool NODE>
 __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int replicas, int seg_rows) {
   using namespace dws;
+  constexpr int LDP = ldp<false>();
   __shared__ __attribute__((aligned(16))) bf16_t sG[NRING * HWp * LDP];   // dy rows
   __shared__ __attribute__((aligned(16))) bf16_t sX[NRING * HWp * LDP];   // transformed x rows
   __shared__ __attribute__((aligned(16))) float sW[9 * CT];               // flipped taps (dgrad)
@@ -571,8 +586,8 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     uint32_t okv, oku;
     fetch<SR + 2>(g_b, p, x0, ybeg - 1, true, v, okv);
     fetch<SR + 2>(x_b, p, x0, ybeg - 1, true, u, oku);
-    put<SR + 2>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
-    put<SR + 2>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);   // transformed x (padding stays zero)
+    put<SR + 2, false>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
+    put<SR + 2, false>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);   // transformed x (padding stays zero)
   }
   __syncthreads();
 
@@ -706,8 +721,8 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
         }
     }
     if (more) {
-      put<SR>(sG, rg, okg, a + SR + 1, false, a4, b4, 0);
-      put<SR>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
+      put<SR, false>(sG, rg, okg, a + SR + 1, false, a4, b4, 0);
+      put<SR, false>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
     }
     __syncthreads();
   }
@@ -745,6 +760,429 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
   const int nreps = p.node.reps > 1 ? p.node.reps : 1;
   const size_t nro = (size_t)(blockIdx.x % nreps) * 2 * p.C;
   for (int e = tid; e < (node ? NS : 9) * CT; e += NT) {
+    const int t = e / CT, c = e % CT;
+    const float v = red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] + red[(2 * NS + t) * CT + c] +
+                    red[(3 * NS + t) * CT + c];
+    if (t < 9) red_add(p.dw, dro + t * p.C + cbase + c, v, CFL_FX_G);
+    else red_add(p.node.sums, nro + (t - 9) * p.C + cbase + c, v, CFL_FX_G);
+  }
+}
+
+// ---- fused depthwise backward with an LDS-DMA dy ring (TUNE_DW_BWD_DMA = 1; measured no faster, kept opt-in) ----
+// The register-budget restructure of dw_bwd_stream_kernel (256 VGPRs + 56 KB LDS: 2 blocks, 8 waves per CU) to 3 blocks
+// per CU:
+//   * dy (staged raw, no transform) goes global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, no VGPR staging) into a
+//     14-row ring, issued 1.5 steps ahead (after the step's epilogue stores);
+//   * x (BN-apply + ReLU on the way in) stays register-staged one step ahead in a 6-row ring: its rows are written
+//     between two barriers at the end of the step (10 rows without the second barrier would not fit 3 blocks);
+//   * every global read is a buffer load on a per-image resource with a 32-bit offset: padding pieces take an
+//     out-of-range offset and read 0 (no clamped addresses, no 64-bit address registers);
+//   * rings in the dws swizzled layout (unpadded 64-byte pixels, dws::pxo);
+//   * the dgrad epilogue runs before the wgrad (its 16 accumulators are dead while the 36 tap sums work).
+// 45 KB LDS, 147 / 166 VGPRs, no scratch: 3 blocks per CU. Measured (profiles/r5_dw/): 1-2 us per call SLOWER than the
+// two-ring kernel at 512 or 768 blocks - the step chain (epilogue operands loaded at the top of the step and waited for
+// mid-step, two barriers) is the bound, not the resident wave count. (A first 54 KB version - x ring 10 rows - ran 2
+// blocks per CU at 768 blocks, 25 % slower: the hardware did not fit 3 x 53.9 KB.)
+// Register loads and LDS stores are inline asm (for a compiler-visible load hipcc drains every DMA in flight before
+// the first use, conv3x3_sk.hip); the counted `s_waitcnt vmcnt` below are the only waits. Issue order in step s:
+// [half-res residual / node y of s] [x rows of s + 1] | wait for the first group | epilogue stores, [dy DMAs of
+// s + 2] | wait for all but the DMAs: at any wait the stores are OLDER than everything it leaves in flight.
+namespace dwd {
+using dws::CPT;
+using dws::CT;
+using dws::G;
+using dws::SL;
+using dws::SR;
+using dws::TW;
+constexpr int PXB = CT * 2;                      // bytes per pixel (32 bf16 channels)
+constexpr int ROWB = (TW + 2) * PXB;             // 2176: one ring row
+constexpr int NRG = 3 * SR + 2, NRX = SR + 2;
+constexpr int OFF_X = NRG * ROWB, OFF_W = OFF_X + NRX * ROWB, OFF_N = OFF_W + 9 * CT * 4, SMEM = OFF_N + 4 * CT * 4;
+constexpr uint32_t OOB = 0x80000000u;            // buffer offset past every resource's range: the load returns 0
+static_assert(3 * SMEM <= 160 * 1024, "three blocks per CU");
+static_assert(ROWB > 2048 && ROWB - 2048 == 8 * 16, "a row = 2 full DMA instructions + 8 lanes of a third");
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+using dws::pxo;
+
+// raw buffer resource over [base, base + bytes) (gfx9 dword 3); wave-uniform
+CFL_DEVICE i4v rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i4v r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+template <int N>
+CFL_DEVICE void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+CFL_DEVICE void order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+CFL_DEVICE u2v ld8(const i4v& rs, uint32_t off) {
+  u2v v;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+  return v;
+}
+CFL_DEVICE void st8(unsigned char* p, uint2 v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)p;
+  const u2v d = {v.x, v.y};
+  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(d) : "memory");
+}
+CFL_DEVICE uint2 u2(u2v v) { return make_uint2(v.x, v.y); }
+}  // namespace dwd
+
+namespace dwd {
+// 16 bytes of the buffer at `off` -> LDS at the wave-uniform `lds` + 16 * lane. Inline asm (M0 = the LDS address):
+// with the DMA visible, hipcc orders every later LDS read that may alias it (the tap reads too) behind vmcnt(0).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"        // M0 is reserved; this kernel has no other M0 user (checked ISA)
+CFL_DEVICE void dma16(const i4v& rs, uint32_t off, unsigned char* lds) {
+  const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(a), "v"(off), "s"(rs)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// x rows row0 .. row0 + NR - 1 of the staging map of dws::fetch (thread t: column t / G, the first 2 G NR threads
+// also a right-halo piece - every thread issues that load, so a wave issues NR + 1 loads whatever its index).
+// xcol: this thread's column byte offset in the image (OOB if the column is padding); hcol: its right-halo piece's
+template <int NR>
+CFL_DEVICE void fetchx(const i4v& rs, const DwParams& p, uint32_t xcol, uint32_t hcol, int hrow, int row0, bool on,
+                       u2v (&v)[NR + 1], uint32_t& okm) {
+  okm = 0;
+  const uint32_t rowb = (uint32_t)p.W * p.C * 2;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int iy = row0 + r;                                 // wave-uniform
+    const bool ok = on && (unsigned)iy < (unsigned)p.H && xcol != OOB;
+    v[r] = ld8(rs, ok ? (uint32_t)iy * rowb + xcol : OOB);
+    okm |= (uint32_t)ok << r;
+  }
+  const int iy = row0 + hrow;
+  const bool ok = on && hrow < NR && (unsigned)iy < (unsigned)p.H && hcol != OOB;
+  v[NR] = ld8(rs, ok ? (uint32_t)iy * rowb + hcol : OOB);
+  okm |= (uint32_t)ok << NR;
+}
+
+template <int NR>
+CFL_DEVICE void putx(unsigned char* ring, const u2v (&v)[NR + 1], uint32_t okm, int row0, bool xform, const float* a4,
+                     const float* b4, int relu) {
+  const int tid = threadIdx.x, q = tid % G;
+  const int slot0 = (row0 + NRX) % NRX;                      // row0 >= -1
+  unsigned char* col = ring + pxo(tid / G) * PXB + q * CPT * 2;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int slot = slot0 + r >= NRX ? slot0 + r - NRX : slot0 + r;
+    const bool ok = (okm >> r) & 1u;
+    st8(col + slot * ROWB, dws::xform4(ok ? u2(v[r]) : make_uint2(0, 0), xform && ok, a4, b4, relu));
+  }
+  if (__builtin_amdgcn_readfirstlane(tid) < 2 * G * NR) {   // the waves holding right-halo pieces
+    const int re = tid / (2 * G), hxe = TW + (tid % (2 * G)) / G;
+    if (re < NR) {
+      const int slot = slot0 + re >= NRX ? slot0 + re - NRX : slot0 + re;
+      const bool ok = (okm >> NR) & 1u;
+      st8(ring + slot * ROWB + pxo(hxe) * PXB + q * CPT * 2,
+          dws::xform4(ok ? u2(v[NR]) : make_uint2(0, 0), xform && ok, a4, b4, relu));
+    }
+  }
+}
+}  // namespace dwd
+
+template <bool NODE>
+__global__ __launch_bounds__(NT, 3) void dw_bwd_dma_kernel(DwParams p, int replicas, int seg_rows) {
+  using namespace dws;
+  using dwd::NRG;
+  using dwd::NRX;
+  using dwd::OOB;
+  using dwd::PXB;
+  using dwd::ROWB;
+  using dwd::pxo;
+  // ONE shared object (a second one can make hipcc drain the DMAs before every ds_read): [dy ring][x ring][taps][node]
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[dwd::SMEM];
+  unsigned char* sX = smem + dwd::OFF_X;
+  float* sW = reinterpret_cast<float*>(smem + dwd::OFF_W);
+  float* sNode = reinterpret_cast<float*>(smem + dwd::OFF_N);
+
+  const int tid = threadIdx.x, lane = tid & 63, cg = tid % G, pt = tid / G;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sr = wid, sc = (pt % (TW / SL)) * SL;            // a wave = one output row of the step
+  static_assert(NT / 64 == SR && TW / SL * G == 64, "wave w owns output row w of a step");
+  const int nslices = p.C / CT, tiles_w = (p.W + TW - 1) / TW, nseg = (p.H + seg_rows - 1) / seg_rows;
+  int lin = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int cs = lin % nslices;
+  lin /= nslices;
+  const int tw = lin % tiles_w;
+  lin /= tiles_w;
+  const int sg = lin % nseg;
+  const int b = lin / nseg;
+  const int x0 = tw * TW, cbase = cs * CT, c0 = cbase + cg * CPT;
+  const int ybeg = sg * seg_rows, yend = min(p.H, ybeg + seg_rows);
+  const int nsteps = (yend - ybeg + SR - 1) / SR;
+  const bool has_ab = p.xf.ab != nullptr;
+  const int relu = p.xf.relu;
+  const size_t img = (size_t)b * p.H * p.W * p.C;
+  const uint32_t img_bytes = (uint32_t)p.H * p.W * p.C * 2;
+  const dwd::i4v rs_x = dwd::rsrc(p.x + img, img_bytes);
+  const dwd::i4v rs_g = dwd::rsrc(p.dy + img, img_bytes);
+  const int Hh = (p.H + 1) >> 1, Wh = (p.W + 1) >> 1;
+  const bf16_t* hsrc = p.add_half ? p.add_half : p.dy;
+  const dwd::i4v rs_h = dwd::rsrc(hsrc + (size_t)b * Hh * Wh * p.C, (uint32_t)Hh * Wh * p.C * 2);
+
+  // plain loads first, waited for before the first DMA is issued
+  float a4[4], b4[4];
+  load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
+  load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+  for (int e = tid; e < 9 * CT; e += NT) {
+    const int t = e / CT, c = e - t * CT;
+    sW[e] = p.w[(8 - t) * p.C + cbase + c];
+  }
+  if (NODE && tid < 4 * CT) sNode[tid] = p.node.ab[(tid / CT) * p.C + cbase + tid % CT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(a4[j]), "+v"(b4[j]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // dy DMA: lane l of instruction j of a row fills bytes 1024 j + 16 l of the row = pixel position 16 j + l / 4
+  // (pixel pxo(position)), channel quarter l % 4; lanes 8.. of the third instruction are masked off
+  uint32_t gcol[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int px = pxo(16 * j + (lane >> 2)), ix = x0 - 1 + px;
+    const bool ok = (unsigned)ix < (unsigned)p.W && px < TW + 2;
+    gcol[j] = ok ? (uint32_t)(ix * p.C + cbase + (lane & 3) * 8) * 2 : OOB;
+  }
+  const uint32_t rowb = (uint32_t)p.W * p.C * 2;
+  // (issued unconditionally - a fixed count per step keeps the waits single constants: a row with on == false
+  // reads zeros from an out-of-range offset into a ring slot no later step reads, no memory traffic)
+  auto dma_row = [&](int r, bool on) {                       // wave-uniform image row r (>= -1)
+    unsigned char* dst = smem + ((r + NRG) % NRG) * ROWB;
+    const bool rok = on && (unsigned)r < (unsigned)p.H;
+    const uint32_t ro = rok ? (uint32_t)r * rowb : 0u;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const uint32_t off = rok && gcol[j] != OOB ? ro + gcol[j] : OOB;
+      if (j < 2) dwd::dma16(rs_g, off, dst + 1024 * j);
+      else if (lane < 8) dwd::dma16(rs_g, off, dst + 2048);
+    }
+  };
+  // x staging offsets (dws::fetch's map): column tid / G, right-halo piece (row tid / 2G, column 32 + (tid % 2G) / G)
+  const int xix = x0 + tid / G - 1, hix = x0 + TW - 1 + (tid % (2 * G)) / G;
+  const uint32_t xcol = (unsigned)xix < (unsigned)p.W ? (uint32_t)(xix * p.C + c0) * 2 : OOB;
+  const uint32_t hcol = (unsigned)hix < (unsigned)p.W ? (uint32_t)(hix * p.C + c0) * 2 : OOB;
+  const int hrow = tid / (2 * G);
+
+  // prologue: dy rows of steps 0 (ybeg - 1 .. ybeg + SR) and 1, x rows of step 0
+  {
+    dma_row(ybeg - 1 + wid, true);
+    dma_row(ybeg + SR - 1 + (wid & 1), true);                      // rows ybeg + 3, ybeg + 4 (twice: identical bytes)
+    dwd::order();
+    dwd::u2v u[SR + 3];
+    uint32_t oku;
+    dwd::fetchx<SR + 2>(rs_x, p, xcol, hcol, hrow, ybeg - 1, true, u, oku);
+    dwd::order();
+    dma_row(ybeg + SR + 1 + wid, nsteps > 1);
+    dwd::order();
+    dwd::wait_vm<3>();
+#pragma unroll
+    for (int i = 0; i < SR + 3; ++i) asm volatile("" : "+v"(u[i]));
+    dwd::putx<SR + 2>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  float accw[9][4], s0[4], s1[4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accw[t][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s0[j] = s1[j] = 0.f;
+  for (int s = 0; s < nsteps; ++s) {
+    const int a = ybeg + s * SR;
+    const bool more = s + 1 < nsteps, dma2 = s + 2 < nsteps;
+    const int oy = a + sr;                                   // wave-uniform
+    // [residual half-resolution gradient (even pixels) / node y of this step] (unconditional: fixed counts)
+    dwd::u2v hr[SL / 2];
+    {
+      const uint32_t hrowo = (uint32_t)(min(oy, p.H - 1) >> 1) * Wh;
+#pragma unroll
+      for (int i = 0; i < SL / 2; ++i) {
+        const int hx = min(x0 + sc + 2 * i, p.W - 1) >> 1;
+        hr[i] = dwd::ld8(rs_h, ((hrowo + hx) * p.C + c0) * 2);
+      }
+    }
+    dwd::u2v yr[NODE ? SL : 1];
+    if constexpr (NODE) {
+      const uint32_t yro = (uint32_t)min(oy, p.H - 1) * rowb;
+#pragma unroll
+      for (int i = 0; i < SL; ++i) yr[i] = dwd::ld8(rs_x, yro + (uint32_t)(min(x0 + sc + i, p.W - 1) * p.C + c0) * 2);
+    }
+    // [x rows of step s + 1] (the dy DMAs of step s + 2 follow the epilogue's stores)
+    dwd::u2v rx[SR + 1];
+    uint32_t okx;
+    dwd::fetchx<SR>(rs_x, p, xcol, hcol, hrow, a + SR + 1, more, rx, okx);
+    dwd::order();
+
+    const float live = oy < yend ? 1.f : 0.f;               // rows past the segment belong to the next block
+    float acc[SL][4], g[SL][4];
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = g[i][j] = 0.f;
+    // dgrad: flipped taps over the dy halo; the centre row's columns 1..SL are this strip's own dy (wgrad operand)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const unsigned char* hrow_p = smem + ((oy - 1 + ky + NRG) % NRG) * ROWB + cg * CPT * 2;
+      float wt[3][4];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) load_f4(&sW[(ky * 3 + kx) * CT + cg * CPT], wt[kx]);
+#pragma unroll
+      for (int cx = 0; cx < SL + 2; ++cx) {
+        float f[4];
+        unpack4(*reinterpret_cast<const uint2*>(hrow_p + pxo(sc + cx) * PXB), f);
+        if (ky == 1 && cx >= 1 && cx <= SL) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[cx - 1][j] = f[j] * live;
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SL) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[o][j] = fmaf(f[j], wt[kx][j], acc[o][j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // (materialise the dgrad sums and the dy strip here: otherwise hipcc sinks the FMAs into their uses behind the
+    // wait and the epilogue branch, keeping all 18 row reads + 9 tap vectors live across them)
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]), "+v"(g[i][j]));
+    // the epilogue operands have landed (the x rows of step s + 1 stay in flight)
+    dwd::wait_vm<SR + 1>();
+#pragma unroll
+    for (int i = 0; i < SL / 2; ++i) asm volatile("" : "+v"(hr[i]));
+#pragma unroll
+    for (int i = 0; i < (NODE ? SL : 1); ++i) asm volatile("" : "+v"(yr[i]));
+    if (oy < yend) {
+      const size_t off0 = (((size_t)b * p.H + oy) * p.W + x0 + sc) * p.C + c0;
+#pragma unroll
+      for (int i = 0; i < SL; ++i)
+        if (x0 + sc + i < p.W) {
+          uint2 v = pack4(acc[i]);
+          if (p.add_half || p.mask_x) {                      // residual join (node_bwd semantics, one rounding)
+            float o[4];
+            unpack4(v, o);
+            if (p.mask_x) {                                  // transformed x at this pixel: the x ring's centre row
+              float xv[4];
+              unpack4(*reinterpret_cast<const uint2*>(sX + (oy % NRX) * ROWB + pxo(sc + i + 1) * PXB + cg * CPT * 2),
+                      xv);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] = xv[j] > 0.f ? o[j] : 0.f;
+            }
+            if (p.add_half && (i & 1) == 0 && (oy & 1) == 0) {   // (oy < yend, x < W hold here)
+              float r[4];
+              unpack4(dwd::u2(hr[i / 2]), r);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] += r[j];
+            }
+            v = pack4(o);
+          }
+          if constexpr (NODE) {                              // g = mask * o (o already bf16) + BN-backward sums
+            float o[4], y[4], nmean[4], nrstd[4];
+            const float* nc = &sNode[cg * CPT];
+            load_f4(nc + 2 * CT, nmean);
+            load_f4(nc + 3 * CT, nrstd);
+            unpack4(v, o);
+            unpack4(dwd::u2(yr[NODE ? i : 0]), y);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float gg = (!relu || fmaf(a4[j], y[j], b4[j]) > 0.f) ? o[j] : 0.f;
+              o[j] = gg;
+              s0[j] += gg;
+              s1[j] += gg * (y[j] - nmean[j]) * nrstd[j];
+            }
+            v = pack4(o);
+          }
+          *reinterpret_cast<uint2*>(p.y + off0 + (size_t)i * p.C) = v;
+        }
+    }
+    // [dy rows of step s + 2] - after the stores, so the end-of-step wait counts only these DMAs as younger than
+    // the x rows
+    dwd::order();
+    dma_row(a + 2 * SR + 1 + wid, dma2);
+    dwd::order();
+    // wgrad: dW[tap] += x[p + tap - 1] * dy[p] over the x halo
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const unsigned char* hrow_p = sX + ((oy - 1 + ky + NRX) % NRX) * ROWB + cg * CPT * 2;
+#pragma unroll
+      for (int cx = 0; cx < SL + 2; ++cx) {
+        float f[4];
+        unpack4(*reinterpret_cast<const uint2*>(hrow_p + pxo(sc + cx) * PXB), f);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int o = cx - kx;
+          if (o < 0 || o >= SL) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) accw[ky * 3 + kx][j] = fmaf(f[j], g[o][j], accw[ky * 3 + kx][j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // everything but this step's dy DMAs (rows of step s + 2) has landed - the x rows of step s + 1, the epilogue's
+    // stores and the DMAs of step s + 1
+    dwd::wait_vm<3>();
+#pragma unroll
+    for (int i = 0; i < SR + 1; ++i) asm volatile("" : "+v"(rx[i]));
+    // x rows of step s + 1 -> the slots of rows a - 1 .. a + 2, once every wave is done with step s (a 6-row x ring:
+    // 8.7 KB less LDS than staging them beside the rows in use; past the last step: zeros into slots no step reads)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    dwd::putx<SR>(sX, rx, okx, a + SR + 1, has_ab || relu, a4, b4, relu);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this thread's x ring stores
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // block reduction of the 9 tap sums (+ the 2 node sums), one atomic per (row, channel) into replica rows
+  dwd::wait_vm<0>();                                         // the last step's (zero) DMAs land in the dy ring
+  __builtin_amdgcn_s_barrier();
+  constexpr int NS = 11;
+  float* red = reinterpret_cast<float*>(smem);               // dy ring no longer needed
+  float part[NS][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[t][j] = accw[t][j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    part[9][j] = s0[j];
+    part[10][j] = s1[j];
+  }
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = part[t][j];
+      for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      part[t][j] = v;
+    }
+  if (lane < G) {
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[(wid * NS + t) * CT + cg * CPT + j] = part[t][j];
+  }
+  __syncthreads();
+  const size_t dro = (size_t)(blockIdx.x % replicas) * 9 * p.C;
+  const int nreps = p.node.reps > 1 ? p.node.reps : 1;
+  const size_t nro = (size_t)(blockIdx.x % nreps) * 2 * p.C;
+  for (int e = tid; e < (NODE ? NS : 9) * CT; e += NT) {
     const int t = e / CT, c = e % CT;
     const float v = red[(0 * NS + t) * CT + c] + red[(1 * NS + t) * CT + c] + red[(2 * NS + t) * CT + c] +
                     red[(3 * NS + t) * CT + c];
@@ -821,6 +1259,14 @@ int dw_bwd(const DwParams& p, hipStream_t st) {
   // two rings (56 KB LDS): 2 blocks per CU, so one round of resident blocks is 512 (the single-pass kernels' 768
   // left a half-empty second round)
   int blocks, seg_rows;
+  if (cfl_tune(TUNE_DW_BWD_DMA) == 1) {                     // 3 blocks per CU: one round is 768
+    stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 768);
+    if (p.node.y) hipLaunchKernelGGL(dw_bwd_dma_kernel<true>, dim3(blocks), dim3(NT), 0, st, p,
+                                     p.replicas > 1 ? p.replicas : 1, seg_rows);
+    else hipLaunchKernelGGL(dw_bwd_dma_kernel<false>, dim3(blocks), dim3(NT), 0, st, p,
+                            p.replicas > 1 ? p.replicas : 1, seg_rows);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 512);
   if (p.node.y) hipLaunchKernelGGL(dw_bwd_stream_kernel<true>, dim3(blocks), dim3(NT), 0, st, p,
                                    p.replicas > 1 ? p.replicas : 1, seg_rows);

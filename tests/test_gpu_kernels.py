@@ -2090,6 +2090,48 @@ def test_dw_bwd_residual_join_matches_node_bwd(B, H, W, C, bn):
         assert torch.allclose(sums.view(4, -1).sum(0), s_ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("B,H,W,C,mode", [(2, 64, 64, 64, "node"), (1, 50, 70, 32, "join"), (3, 9, 33, 32, "plain"),
+                                          (2, 128, 96, 32, "node"), (4, 32, 32, 128, "join")])
+def test_dw_bwd_dma_ring_equals_register_staged(B, H, W, C, mode):
+    """The LDS-DMA fused depthwise backward (dw_bwd_dma_kernel, TUNE_DW_BWD_DMA = 1: dy ring two steps ahead, buffer
+    loads with out-of-range zero padding, 3 blocks / CU) equals the default register-staged two-ring kernel bit for bit in dx (same arithmetic per pixel) and up to float atomic order in dW / node sums,
+    over many-step segments, ragged maps (odd H, W not a multiple of the 32-pixel strip) and the three epilogues."""
+    torch.manual_seed(61)
+    C_ = hip()
+    xb, _ = bf(torch.randn(B, H, W, C))
+    gb, _ = bf(torch.randn(B, H, W, C))
+    rb, _ = bf(torch.randn(B, (H + 1) // 2, (W + 1) // 2, C))
+    w = (torch.randn(9 * C) * 0.2).to(DEV)
+    nab = ab_for(C, 62)[0]
+    nab[2 * C:3 * C], nab[3 * C:] = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    nab = nab.to(DEV)
+    reps = 16
+
+    def run(tune):
+        C_.set_tune(C_.TUNE_DW_BWD_DMA, tune)
+        out = torch.zeros_like(gb)
+        dw = torch.zeros(reps * 9 * C, device=DEV)
+        sums = torch.zeros(4 * 2 * C, device=DEV)
+        if mode == "node":
+            C_.dw_bwd(xb, nab, 1, gb, w, out, dw, reps, B, H, W, C, node_y=xb, node_ab=nab, node_sums=sums,
+                      node_reps=4, node_relu=1)
+        elif mode == "join":
+            C_.dw_bwd(xb, nab, 1, gb, w, out, dw, reps, B, H, W, C, add_half=rb, mask_x=1)
+        else:
+            C_.dw_bwd(xb, nab, 1, gb, w, out, dw, reps, B, H, W, C)
+        torch.cuda.synchronize()
+        return out, dw.view(reps, -1).sum(0), sums.view(4, -1).sum(0)
+
+    try:
+        ref = run(0)
+        got = run(1)
+    finally:
+        C_.set_tune(C_.TUNE_DW_BWD_DMA, 0)
+    assert torch.equal(got[0], ref[0]), int((got[0] != ref[0]).sum())
+    assert torch.allclose(got[1], ref[1], rtol=1e-4, atol=1e-3)
+    assert torch.allclose(got[2], ref[2], rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("B,H,Cin,N,tune", [(2, 32, 64, 128, ""), (2, 16, 128, 256, ""), (2, 24, 32, 64, "ws"),
                                             (2, 16, 64, 64, "small"), (2, 20, 64, 64, ""), (2, 32, 128, 64, "sk"),
                                             (2, 32, 256, 256, "sk")])

@@ -12,7 +12,7 @@ while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
   timeout -s KILL ${PMC_T:-150} rocprofv3 --pmc $counters --output-format csv -d $R/gpurun_out/pmc/p$i -o run -- \
-      python $R/bench.py --profile-steps ${PSTEPS:-6} > $R/gpurun_out/pmc/p$i.log 2>&1
+      python $R/bench.py --profile-steps ${PSTEPS:-6} ${PROF_ARGS} > $R/gpurun_out/pmc/p$i.log 2>&1
   rc=$?
   [ $rc -eq 0 ] || { echo "pass $i ($counters) failed rc=$rc"; tail -5 $R/gpurun_out/pmc/p$i.log; exit $rc; }
   echo "pass $i ok: $counters"
