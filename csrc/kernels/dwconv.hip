@@ -768,7 +768,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
   }
 }
 
-// ---- fused depthwise backward with an LDS-DMA dy ring (TUNE_DW_BWD_DMA = 1; measured no faster, kept opt-in) ----
+// ---- fused depthwise backward with an LDS-DMA dy ring (the long-segment launches: dw_bwd's size rule) ----
 // The register-budget restructure of dw_bwd_stream_kernel (256 VGPRs + 56 KB LDS: 2 blocks, 8 waves per CU) to 3 blocks
 // per CU:
 //   * dy (staged raw, no transform) goes global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, no VGPR staging) into a
@@ -779,10 +779,12 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
 //     out-of-range offset and read 0 (no clamped addresses, no 64-bit address registers);
 //   * rings in the dws swizzled layout (unpadded 64-byte pixels, dws::pxo);
 //   * the dgrad epilogue runs before the wgrad (its 16 accumulators are dead while the 36 tap sums work).
-// 45 KB LDS, 147 / 166 VGPRs, no scratch: 3 blocks per CU. Measured (profiles/r5_dw/): 1-2 us per call SLOWER than the
-// two-ring kernel at 512 or 768 blocks - the step chain (epilogue operands loaded at the top of the step and waited for
-// mid-step, two barriers) is the bound, not the resident wave count. (A first 54 KB version - x ring 10 rows - ran 2
-// blocks per CU at 768 blocks, 25 % slower: the hardware did not fit 3 x 53.9 KB.)
+// 45 KB LDS, 147 / 166 VGPRs, no scratch: 3 blocks per CU. Measured (profiles/r5_dw/): at the 512^2 planned batch
+// (segments of whole maps, many rounds of blocks) 14-15 % faster per call than the two-ring kernel (19.3 vs 22.4 ms
+// per step over the 6 calls); at 256^2 / batch 16 (one round of 6-8-step segments) 1-2 us per call slower - there the
+// step chain (epilogue operands loaded at the top of a step and waited for mid-step, two barriers) and the deeper
+// prologue bound it, not the resident wave count. (A first 54 KB version - x ring 10 rows - ran 2 blocks per CU at
+// 768 blocks, 25 % slower: the hardware did not fit 3 x 53.9 KB.)
 // Register loads and LDS stores are inline asm (for a compiler-visible load hipcc drains every DMA in flight before
 // the first use, conv3x3_sk.hip); the counted `s_waitcnt vmcnt` below are the only waits. Issue order in step s:
 // [half-res residual / node y of s] [x rows of s + 1] | wait for the first group | epilogue stores, [dy DMAs of
@@ -1259,7 +1261,12 @@ int dw_bwd(const DwParams& p, hipStream_t st) {
   // two rings (56 KB LDS): 2 blocks per CU, so one round of resident blocks is 512 (the single-pass kernels' 768
   // left a half-empty second round)
   int blocks, seg_rows;
-  if (cfl_tune(TUNE_DW_BWD_DMA) == 1) {                     // 3 blocks per CU: one round is 768
+  // LDS-DMA kernel (3 blocks per CU, one round is 768) for the launches that stream long segments: at the 512^2
+  // planned batch 14-15 % faster per call than the two-ring kernel, at 256^2 / batch 16 (one round of 6-8-step
+  // segments, prologue-bound) 1-2 us slower (profiles/r5_dw/). Auto: >= 2 rounds of strips at 3 blocks per CU.
+  const int strips = p.B * ((p.W + dws::TW - 1) / dws::TW) * (p.C / dws::CT);
+  const int dma_knob = cfl_tune(TUNE_DW_BWD_DMA);
+  if (dma_knob == 1 || (dma_knob == 0 && strips >= 1536)) {
     stream_shape(p, blocks, seg_rows, cfl_tune(TUNE_DW_BWD_BLOCKS) > 0 ? cfl_tune(TUNE_DW_BWD_BLOCKS) : 768);
     if (p.node.y) hipLaunchKernelGGL(dw_bwd_dma_kernel<true>, dim3(blocks), dim3(NT), 0, st, p,
                                      p.replicas > 1 ? p.replicas : 1, seg_rows);

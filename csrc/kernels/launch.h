@@ -526,8 +526,9 @@ enum TuneKey {
   TUNE_WGRAD3_SK_MINTILES = 49, // ... min 128-pixel tiles per block (default 16)
   TUNE_CONV3_F8 = 50,          // fp8 3x3 routing: 0 = default (fp8 unless the weight-stationary bf16 kernel takes the call),
                                //   1 = never, 2 = every call carrying fp8 operands
-  TUNE_DW_BWD_DMA = 51,        // fused depthwise backward: 0 = default (register-staged two-ring kernel, 2 blocks /
-                               //   CU), 1 = the LDS-DMA dy ring kernel (3 blocks / CU; measured no faster)
+  TUNE_DW_BWD_DMA = 51,        // fused depthwise backward: 0 = default (LDS-DMA dy ring kernel, 3 blocks / CU, when
+                               //   the launch has >= 1,536 strips, else the register-staged two-ring kernel), 1 = always
+                               //   the DMA kernel, 2 = never
   TUNE_N = 52
 };
 int cfl_tune(int key);
