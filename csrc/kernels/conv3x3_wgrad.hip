@@ -26,10 +26,10 @@ namespace {
 
 using namespace wg3;
 
-template <int BNO, bool TR>
+template <int BNO, bool TR, int CBT = CB, bool SB = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int tiles_total, int splits) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad3_lds_bytes<BNO>()];
-  wgrad3_body<BNO, TR>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad3_lds_bytes<BNO, CBT, SB>()];
+  wgrad3_body<BNO, TR, CBT, SB>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // Grouped launch: several independent weight gradients (different layers, same tile config) in ONE grid. Every
@@ -77,6 +77,17 @@ static bool wgrad3_sk_use(const WgradParams& p) {
   return v == 2 || p.Ho * p.Wo <= 64 * 64;
 }
 
+// input channels per block: 64 (wgrad3_body CBT = 64, one LDS buffer) for the large launches - a layer's dy is then
+// re-read Cin / 64 times instead of Cin / 32 and each staged tile feeds twice the MFMAs - else 32
+// (TUNE_WGRAD3_WIDE: 0 = auto, 1 = never, 2 = whenever Cin % 64 == 0)
+int conv3x3_wgrad_cbt(const WgradParams& p) {
+  const int v = cfl_tune(TUNE_WGRAD3_WIDE);
+  if (v == 1 || p.Cin % 64 || wgrad3_sk_use(p)) return CB;
+  if (v == 2) return 64;
+  const int64_t tiles = (int64_t)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
+  return tiles * (p.Cin / CB) >= 65536 ? 64 : CB;
+}
+
 bool conv3x3_wgrad_supported(const WgradParams& p) {
   return p.ks == 3 && p.stride == 1 && p.pad_t == 1 && p.pad_l == 1 && p.Cin % CB == 0 && p.N % 32 == 0 &&
          p.Ho >= 8 && p.Wo >= 8;
@@ -94,7 +105,7 @@ void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits
     return;
   }
   bno = p.N % 64 == 0 ? 64 : 32;
-  const int xy = (p.Cin / CB) * (p.N / bno);
+  const int xy = (p.Cin / conv3x3_wgrad_cbt(p)) * (p.N / bno);
   const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 512;
   // >= 16 pixel tiles per block: the engine launches the decoder's halo wgrads grouped (conv3x3_wgrad_grouped), so
   // long blocks still fill the chip, and every pixel split is one plain-stored slab row that grad_finish must read
@@ -120,12 +131,12 @@ int conv3x3_wgrad_splits(const WgradParams& p) {
 }
 
 // tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>; split-K-in-block
-// body: 4 = TR, 5 = HWIO
+// body: 4 = TR, 5 = HWIO; 64-channel blocks: 6 = <64,TR>, 7 = <64,HWIO>, 8 = <32,TR>, 9 = <32,HWIO>
 int conv3x3_wgrad_config(const WgradParams& p) {
   if (wgrad3_sk_use(p)) return p.dst_mode == 1 ? 4 : 5;
   int bno, tiles, splits;
   conv3x3_wgrad_shape(p, bno, tiles, splits);
-  return (bno == 64 ? 0 : 2) + (p.dst_mode == 1 ? 0 : 1);
+  return (conv3x3_wgrad_cbt(p) == 64 ? 6 : 0) + (bno == 64 ? 0 : 2) + (p.dst_mode == 1 ? 0 : 1);
 }
 
 int conv3x3_wgrad(const WgradParams& p, hipStream_t st);
@@ -142,7 +153,7 @@ int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
       conv3x3_wgrad_shape(p, bno, tiles, splits);
       if (p.slabs > 0 && p.slabs != splits) return 2;
       const int c = conv3x3_wgrad_config(p);
-      if (c >= 4) {                                   // split-K-in-block body: launched on its own
+      if (c >= 4) {                                   // split-K-in-block / 64-channel bodies: launched on their own
         const int rc = conv3x3_wgrad(p, st);
         if (rc) return rc;
         continue;
@@ -175,11 +186,22 @@ int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {
   int bno, tiles, splits;
   conv3x3_wgrad_shape(p, bno, tiles, splits);
   if (p.slabs > 0 && p.slabs != splits) return 2;
-  dim3 grid(p.Cin / CB, p.N / bno, splits);
+  dim3 grid(p.Cin / conv3x3_wgrad_cbt(p), p.N / bno, splits);
   const bool tr = p.dst_mode == 1;
   if (wgrad3_sk_use(p)) {
     if (tr) hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<true>), grid, dim3(NT), 0, st, p, tiles, splits);
     else hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<false>), grid, dim3(NT), 0, st, p, tiles, splits);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
+  if (conv3x3_wgrad_cbt(p) == 64) {
+    if (bno == 64 && tr)
+      hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, true, 64, true>), grid, dim3(NT), 0, st, p, tiles, splits);
+    else if (bno == 64)
+      hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, false, 64, true>), grid, dim3(NT), 0, st, p, tiles, splits);
+    else if (tr)
+      hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, true, 64, true>), grid, dim3(NT), 0, st, p, tiles, splits);
+    else
+      hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, false, 64, true>), grid, dim3(NT), 0, st, p, tiles, splits);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   if (bno == 64 && tr) hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, true>), grid, dim3(NT), 0, st, p, tiles, splits);

@@ -330,7 +330,8 @@ int launch_group(const WgradParams* ps, int n, hipStream_t st) {
 // latency-bound grid that leaves the chip part-idle in its tail; in one grid the blocks of all of them co-run and
 // the four launch boundaries between the groups are gone. One LDS buffer sized for the largest body (the 64-wide
 // halo config, 75.5 KB: 2 blocks per CU, as the halo groups had); the kernel's VGPR count is the largest body's.
-// kind: 0-5 halo config (conv3x3_wgrad_config; 4, 5 = the split-K-in-block body), 10 + c generic config c (wgrad_config; c = 1, the 80 KB
+// kind: 0-9 halo config (conv3x3_wgrad_config; 4, 5 = the split-K-in-block body, 6-9 the 64-channel blocks), 10 + c
+// generic config c (wgrad_config; c = 1, the 80 KB
 // 128-pixel-stage variant, is launched on its own)
 constexpr int MIX_MAX = 24;
 struct MixItem {
@@ -345,7 +346,8 @@ struct MixGroup {
   int xcd;                  // XCD-grouped block order (TUNE_WGRAD_MIX_XCD != 1)
 };
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int MIX_LDS = cmax(cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wg3s::LDS_BYTES), wgrad_lds_bytes<128, 128, 32>()),
+constexpr int MIX_LDS = cmax(cmax(cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wg3::wgrad3_lds_bytes<64, 64, true>()),
+                                            wg3s::LDS_BYTES), wgrad_lds_bytes<128, 128, 32>()),
                                   wgrad_lds_bytes<128, 128, 64>()),
                              cmax(cmax(wgrad_lds_bytes<64, 32, 128>(), wgrad_lds_bytes<32, 64, 128>()),
                                   cmax(wgrad_lds_bytes<32, 32, 128>(), wgrad_lds_bytes<64, 64, 64>())));
@@ -373,6 +375,10 @@ __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
     case 3: wg3::wgrad3_body<32, false>(P, a, b, bx, by, bz, smem); break;
     case 4: wg3s::wgrad3sk_body<true>(P, a, b, bx, by, bz, smem); break;
     case 5: wg3s::wgrad3sk_body<false>(P, a, b, bx, by, bz, smem); break;
+    case 6: wg3::wgrad3_body<64, true, 64, true>(P, a, b, bx, by, bz, smem); break;
+    case 7: wg3::wgrad3_body<64, false, 64, true>(P, a, b, bx, by, bz, smem); break;
+    case 8: wg3::wgrad3_body<32, true, 64, true>(P, a, b, bx, by, bz, smem); break;
+    case 9: wg3::wgrad3_body<32, false, 64, true>(P, a, b, bx, by, bz, smem); break;
     case 10: wgrad_body<128, 128, 32>(P, a, bx, by, bz, smem); break;
     case 16: wgrad_body<128, 128, 64>(P, a, bx, by, bz, smem); break;
     case 12: wgrad_body<64, 32, 128>(P, a, bx, by, bz, smem); break;
@@ -396,6 +402,7 @@ int conv_wgrad_slabs(const WgradParams& p) {
 bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x3_wgrad_supported(p); }
 
 int conv3x3_wgrad_config(const WgradParams& p);
+int conv3x3_wgrad_cbt(const WgradParams& p);
 int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st);
 void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits);
 
@@ -459,7 +466,7 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
         conv3x3_wgrad_shape(p, bno, it.a, it.b);
         if (p.slabs > 0 && p.slabs != it.b) return 2;
         it.kind = conv3x3_wgrad_config(p);
-        it.gx = p.Cin / 32;
+        it.gx = p.Cin / conv3x3_wgrad_cbt(p);
         it.gy = p.N / bno;
         zs = it.b;
       } else {
@@ -489,8 +496,8 @@ static bool mix_ok(const WgradParams& p) {
 
 
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
-  static thread_local WgradParams by_cfg[6][16], gen_cfg[7][32];   // halo configs 0-5 (conv3x3_wgrad_config)
-  int cnt[6] = {0, 0, 0, 0, 0, 0}, gcnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  static thread_local WgradParams by_cfg[10][16], gen_cfg[7][32];  // halo configs 0-9 (conv3x3_wgrad_config)
+  int cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, gcnt[7] = {0, 0, 0, 0, 0, 0, 0};
   const bool group = cfl_tune(TUNE_WGRAD_GROUP) != 1;
   const bool group1 = group && cfl_tune(TUNE_WGRAD_GROUP) != 2;
   if (group1 && cfl_tune(TUNE_WGRAD_MIX) != 1) {            // default: one mixed launch (plus any odd ones out)
@@ -512,7 +519,7 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
     if (p.slabs > 0 && p.slabs != conv_wgrad_slabs(p)) return 2;
     if (p.algo != 1 && conv3x3_wgrad_supported(p) && group) {
       const int c = conv3x3_wgrad_config(p);
-      if (c < 0 || c >= 6 || cnt[c] == 16) return 5;
+      if (c < 0 || c >= 10 || cnt[c] == 16) return 5;
       by_cfg[c][cnt[c]++] = p;
     } else if (!(p.algo != 1 && conv3x3_wgrad_supported(p)) && group1 && generic_ok(p)) {
       int bko, bno, rm;
@@ -538,7 +545,7 @@ int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st) {
     }
     if (rc) return rc;
   }
-  for (int c = 0; c < 6; ++c)
+  for (int c = 0; c < 10; ++c)
     if (cnt[c]) {
       const int rc = conv3x3_wgrad_grouped(by_cfg[c], cnt[c], st);
       if (rc) return rc;

@@ -529,7 +529,9 @@ enum TuneKey {
   TUNE_DW_BWD_DMA = 51,        // fused depthwise backward: 0 = default (LDS-DMA dy ring kernel, 3 blocks / CU, when
                                //   the launch has >= 1,536 strips, else the register-staged two-ring kernel), 1 = always
                                //   the DMA kernel, 2 = never
-  TUNE_N = 52
+  TUNE_WGRAD3_WIDE = 52,       // halo wgrad 64-input-channel blocks (one LDS buffer): 0 = default (launches of >= 64k
+                               //   32-channel tile-blocks: the 512^2 planned batch), 1 = never, 2 = whenever Cin % 64 == 0
+  TUNE_N = 53
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

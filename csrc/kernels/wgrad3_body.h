@@ -8,10 +8,9 @@ namespace {
 namespace wg3 {
 
 constexpr int NT = 256;
-constexpr int CB = 32;            // input channels per block (the A-operand rows)
+constexpr int CB = 32;            // input channels per block (the A-operand rows) of the default configs
 constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;
-constexpr int LDH = CB + 16;     // 96-byte halo rows (see the layout note in conv3x3_wgrad.hip)
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
@@ -19,35 +18,54 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(p));
 }
 
-// LDS bytes of one block of the BNO config: two halo images + two dy tiles (the caller owns the allocation, so a
-// grouped launch of several wgrad kinds can share one buffer: conv_wgrad.hip wgrad_mix_kernel)
-template <int BNO>
-constexpr int wgrad3_lds_bytes() { return 2 * HP * LDH * 2 + 2 * TP * (BNO + 16) * 2; }
+// halo rows: CBT input channels + 16 bf16 of padding (96 / 160 bytes, see the layout note in conv3x3_wgrad.hip)
+template <int CBT>
+constexpr int ldh() { return CBT + 16; }
+
+// LDS bytes of one block of the (BNO, CBT) config: two halo images + two dy tiles, SB (single buffer): one of each
+// (the caller owns the allocation, so a grouped launch of several wgrad kinds can share one buffer: conv_wgrad.hip
+// wgrad_mix_kernel)
+template <int BNO, int CBT = CB, bool SB = false>
+constexpr int wgrad3_lds_bytes() { return (SB ? 1 : 2) * (HP * ldh<CBT>() * 2 + TP * (BNO + 16) * 2); }
 
 // TR: accumulate D[n][c] instead of D[c][n] so that the 16 contiguous accumulator columns land on contiguous
 // addresses of the destination layout (c for the Conv2DTranspose (kh,kw,out,in) layout, n for HWIO): each atomic
 // wave-instruction then adds 4 x 64 B segments instead of 64 scattered dwords.
-template <int BNO, bool TR>
+// CBT: input channels per block (32, or 64 for the large launches: each dy tile then serves twice the channels, so
+// a layer's dy is re-read Cin / 64 instead of Cin / 32 times, and each staged byte feeds twice the MFMAs).
+// SB: one LDS buffer (the 64-channel configs: two would leave one block per CU); the next tile's registers are
+// stored between two barriers instead of into the other buffer.
+template <int BNO, bool TR, int CBT = CB, bool SB = false>
 CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, int bx, int by, int bz,
                             unsigned char* smem) {
   constexpr int NF = BNO / 16;              // n fragments
-  constexpr int COMBOS = 2 * NF;            // (c fragment, n fragment) pairs per tap
+  constexpr int COMBOS = (CBT / 16) * NF;   // (c fragment, n fragment) pairs per tap
   constexpr int CPW = COMBOS / 4;           // combos per wave
+  constexpr int LDH = ldh<CBT>();
   constexpr int LDD = BNO + 16;    // 96 / 160-byte dy rows
-  constexpr int HALO_CH = HP * (CB / 8), H_PER_T = (HALO_CH + NT - 1) / NT;
+  constexpr int QP = CBT / 8;               // 16-byte pieces per halo pixel
+  constexpr int HALO_CH = HP * QP, H_PER_T = (HALO_CH + NT - 1) / NT;
   constexpr int D_CH = TP * (BNO / 8), D_PER_T = (D_CH + NT - 1) / NT;
+  constexpr int NBUF = SB ? 1 : 2;
   static_assert(COMBOS % 4 == 0, "combos must split over 4 waves");
+  static_assert(CPW <= NF && NF % CPW == 0, "a wave's combos share one c fragment (one A read per tap)");
+  static_assert(NT % QP == 0, "a thread's halo channel piece is the same in every staged chunk");
   bf16_t (*sH)[HP][LDH] = reinterpret_cast<bf16_t (*)[HP][LDH]>(smem);
-  bf16_t (*sD)[TP][LDD] = reinterpret_cast<bf16_t (*)[TP][LDD]>(smem + 2 * HP * LDH * 2);
+  bf16_t (*sD)[TP][LDD] = reinterpret_cast<bf16_t (*)[TP][LDD]>(smem + NBUF * HP * LDH * 2);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cbase = bx * CB, nBlock = by * BNO;
+  const int cbase = bx * CBT, nBlock = by * BNO;
   const int tiles_w = (p.Wo + TW - 1) / TW, tiles_h = (p.Ho + TH - 1) / TH;
   const int Hl = p.Hin << p.up_in, Wl = p.Win << p.up_in;
   const bool has_ab = p.xf.ab != nullptr;
+  // producer BN coefficients of this thread's 8 halo channels: held in registers, or (the 144-accumulator config)
+  // re-read at each tile's store (L1 / L2 hits) to leave the registers to the accumulators
+  constexpr bool AB_REG = CPW < 4;
   float a8[8], b8[8];
-  load_f8_or(p.xf.ab + cbase + (tid & 3) * 8, has_ab, 1.f, a8);
-  load_f8_or(p.xf.ab + p.xf.C + cbase + (tid & 3) * 8, has_ab, 0.f, b8);
+  if constexpr (AB_REG) {
+    load_f8_or(p.xf.ab + cbase + (tid % QP) * 8, has_ab, 1.f, a8);
+    load_f8_or(p.xf.ab + p.xf.C + cbase + (tid % QP) * 8, has_ab, 0.f, b8);
+  }
 
   // The next tile's halo / dy chunks are loaded RAW, branch-free (clamped in-image addresses, a validity bit per
   // chunk) and only masked + transformed (producer BN-apply + ReLU) in store(), after the current tile's MFMAs:
@@ -65,7 +83,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
       const int ec = e < HALO_CH ? e : HALO_CH - 1;
-      const int hp = ec >> 2, q = ec & 3;
+      const int hp = ec / QP, q = ec % QP;
       const int hy = hp / HW, hx = hp - hy * HW;
       const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
       const bool ok = e < HALO_CH && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
@@ -87,6 +105,10 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
     }
   };
   auto store = [&](int buf) {
+    if constexpr (!AB_REG) {
+      load_f8_or(p.xf.ab + cbase + (tid % QP) * 8, has_ab, 1.f, a8);
+      load_f8_or(p.xf.ab + p.xf.C + cbase + (tid % QP) * 8, has_ab, 0.f, b8);
+    }
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
@@ -104,7 +126,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
           }
           v = pack8(f);
         }
-        *reinterpret_cast<uint4*>(&sH[buf][e >> 2][(e & 3) * 8]) = v;
+        *reinterpret_cast<uint4*>(&sH[buf][e / QP][(e % QP) * 8]) = v;
       }
     }
 #pragma unroll
@@ -156,19 +178,27 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int sh = (tap / 3) * HW + (tap % 3);
+        // the wave's combos share c fragment cf[0] (static_assert above): one A read per tap
+        const s4v lo = tr_read(&sH[buf][h0 + sh][16 * cf[0] + 4 * pq]);
+        const s4v hi = tr_read(&sH[buf][h1 + sh][16 * cf[0] + 4 * pq]);
+        const s8v aop = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int u = 0; u < CPW; ++u) {
-          const s4v lo = tr_read(&sH[buf][h0 + sh][16 * cf[u] + 4 * pq]);
-          const s4v hi = tr_read(&sH[buf][h1 + sh][16 * cf[u] + 4 * pq]);
-          const s8v aop = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           if (TR) acc[tap][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bop[u], aop, acc[tap][u], 0, 0, 0);
           else acc[tap][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aop, bop[u], acc[tap][u], 0, 0, 0);
         }
+        // 144 accumulators (CBT = BNO = 64): no room to hoist every tap's operand reads
+        if constexpr (CPW == 4) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (more) store(buf ^ 1);
+    if constexpr (SB) {
+      __syncthreads();                               // every wave's reads of this tile done
+      if (more) store(0);
+    } else {
+      if (more) store(buf ^ 1);
+    }
     __syncthreads();
-    buf ^= 1;
+    buf ^= NBUF - 1;
   }
   // D col = lane&15, row = (lane>>4)*4 + r;  TR: D[n][c] -> (8-tap, n, c) layout, else D[c][n] -> (tap, c, n).
   // Slab mode: this split's own row of the slab, plain stores (each element has exactly one writer); otherwise

@@ -722,6 +722,55 @@ def test_conv3x3_halo_wgrad_matches_generic_and_autograd(B, Hs, Cin, N, up, use_
 
 
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,dst_mode", [
+    (2, 8, 64, 32, 0, True, 1),      # 64 x 32 block (one c block: the N = 32 decoder level)
+    (2, 8, 128, 64, 1, True, 1),     # 64 x 64 block (144 accumulators), upsampled input
+    (2, 20, 128, 128, 0, False, 0),  # Keras HWIO layout, ragged rows and columns, 2 c blocks x 2 n blocks
+])
+def test_wgrad3_wide_channel_blocks(B, Hs, Cin, N, up, use_ab, dst_mode):
+    """The 64-input-channel halo weight-gradient blocks (wgrad3_body CBT = 64, one LDS buffer, TUNE_WGRAD3_WIDE = 2)
+    against the 32-channel body and fp32 autograd, and their slab rows summed by grad_finish against the direct
+    (atomic) result."""
+    torch.manual_seed(31)
+    C_ = hip()
+    Ho = Hs * (2 if up else 1)
+    xb, xf = bf(torch.randn(B, Hs, Hs, Cin))
+    dyb, dyf = bf(torch.randn(B, Ho, Ho, N))
+    ab, a, b = ab_for(Cin, 16)
+    abd = ab.to(DEV) if use_ab else None
+    K = 9 * Cin
+    outs = {}
+    try:
+        for wide in (1, 2):
+            C_.set_tune(C_.TUNE_WGRAD3_WIDE, wide)
+            dw = torch.zeros(K * N, device=DEV)
+            C_.conv_wgrad(xb, dyb, dw, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0)
+            outs[wide] = dw.cpu()
+        assert rel(outs[2], outs[1]) < 2e-3
+        rows, plain = C_.conv_wgrad_slabs(B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1)
+        assert plain
+        slab = torch.full((rows * K * N,), float("nan"), device=DEV)       # plain rows overwrite all
+        C_.conv_wgrad(xb, dyb, slab, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0, 0, rows)
+        dst = torch.zeros(K * N, device=DEV)
+        table, work = C_.make_grad_finish_table([(slab, dst, K * N, rows, C_.GF_SUM)])
+        C_.grad_finish(table, 1, work)
+        assert rel(dst.cpu(), outs[2]) < 1e-5
+    finally:
+        C_.set_tune(C_.TUNE_WGRAD3_WIDE, 0)
+    t = (xf * a + b) if use_ab else xf
+    xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    if up:
+        xin = R.upsample2(xin)
+    if dst_mode == 1:
+        w = torch.zeros(3, 3, N, Cin, requires_grad=True)
+        out = R.convt_same(xin, w, None)
+    else:
+        w = torch.zeros(3, 3, Cin, N, requires_grad=True)
+        out = R.conv2d_same(xin, w, None, 1)
+    (out.permute(0, 2, 3, 1) * dyf).sum().backward()
+    assert rel(outs[2].view(w.shape), w.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,dst_mode", [
     (2, 16, 256, 256, 0, True, 1),   # the 16^2 decoder ConvT shape (Cin 256 -> N 256)
     (2, 16, 256, 128, 1, True, 1),   # upsampled 16^2 -> 32^2 (Cin 256 -> N 128)
     (3, 6, 32, 64, 1, True, 1),      # ragged 12x12 output
@@ -1820,15 +1869,17 @@ def test_conv_side_job_matches_separate_passes(kind, B, H, K, N, s2, off):
     assert torch.allclose(f[4], u[4], rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("mix", [0, 1])
-def test_conv_wgrad_batch_grouped_equals_individual(mix):
+@pytest.mark.parametrize("mix,wide", [(0, 0), (1, 0), (0, 2)])
+def test_conv_wgrad_batch_grouped_equals_individual(mix, wide):
     """conv_wgrad_batch (the engine's deferred weight gradients): every wgrad in ONE mixed launch (default, mix=0)
     or 3x3 halo wgrads of different layers grouped into shared launches per tile config (mix=1) - bit-identical
     slabs to one call each - and generic 1x1 wgrads in the same mixed launch or grouped per tile config
-    (replica-row atomics: equal up to float summation order)."""
+    (replica-row atomics: equal up to float summation order). wide=2: the halo items with Cin % 64 == 0 on the
+    64-channel bodies (mixed-launch kinds 6-9)."""
     torch.manual_seed(41)
     C_ = hip()
     C_.set_tune(C_.TUNE_WGRAD_MIX, mix)
+    C_.set_tune(C_.TUNE_WGRAD3_WIDE, wide)
     shapes = [  # (B, Hin, Cin, up, Ho, N, ks, dst_mode)
         (2, 16, 64, 0, 16, 32, 3, 1), (2, 8, 64, 1, 16, 32, 3, 1), (2, 16, 32, 0, 16, 64, 3, 1),
         (2, 16, 64, 0, 16, 64, 3, 1), (2, 16, 32, 0, 16, 64, 1, 0), (3, 8, 32, 0, 8, 32, 3, 0),
@@ -1844,12 +1895,14 @@ def test_conv_wgrad_batch_grouped_equals_individual(mix):
         calls.append((x, dy, slab, ab, 1, B, Hin, Hin, Cin, up, Ho, Ho, N, ks, 1, pad, pad, dm, 0, 0, rows))
     try:
         C_.conv_wgrad_batch(calls)
+        C_.set_tune(C_.TUNE_WGRAD_MIX, 0)
+        batched = [c[2].clone() for c in calls]
+        for c in calls:
+            c[2].zero_()
+            C_.conv_wgrad(*c)
     finally:
         C_.set_tune(C_.TUNE_WGRAD_MIX, 0)
-    batched = [c[2].clone() for c in calls]
-    for c in calls:
-        c[2].zero_()
-        C_.conv_wgrad(*c)
+        C_.set_tune(C_.TUNE_WGRAD3_WIDE, 0)
     for a, c in zip(batched, calls):
         if c[13] == 3:
             assert torch.equal(a, c[2])
