@@ -991,8 +991,8 @@ class UNetEngine:
         reference's batches), so every held-out image is evaluated exactly once. Default cap (CFL_EVAL_CAP): 1024
         images, further bounded to a quarter of the device's free HBM at ~21.7 MB of forward activations per 256^2
         image (scaled by resolution) - several clients may share one device in a rehearsal. Round 4's 2048 cap (the
-        bench's 1,776-image split in ONE launch, 38.5 GB) measured 13,069 vs 13,037 img/s against three 592-image
-        launches: noise, for 2.6x the footprint (profiles/r5_evalcap)."""
+        bench's 1,776-image split in ONE launch) measured 12,754 / 12,688 img/s and 40.6 GB peak HBM per client
+        against 12,859 / 12,812 img/s and 15.5 GB for three 592-image launches (profiles/r5_evalcap, one box)."""
         if cap <= 0:
             cap = int(os.environ.get("CFL_EVAL_CAP", "1024"))
             if self.dev.type == "cuda":
