@@ -894,7 +894,10 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
   if (small_tiles(p)) {
     splits = launch<8, 8, 32, 2, 2, true>(p, 1, st);
   } else if (big_tiles(p)) {
-    splits = launch<16, 16, 64, 2, 2, true>(p, 1, st);
+    // 4 x 1 waves of 64 pixels x 64 channels: 8 fragment reads per 16 MFMAs instead of 10 (128 x 32 per wave) - these
+    // large-M calls are LDS-read bound (measured: profiles/README.md round 5)
+    if (cfl_tune(TUNE_CONV3_BIG_WAVES) == 1) splits = launch<16, 16, 64, 2, 2, true>(p, 1, st);
+    else splits = launch<16, 16, 64, 4, 1, true>(p, 1, st);
   } else if (use_wb(p) && wb_bn(p) == 64) {
     if (w16) splits = launch<8, 16, 64, 2, 2, true>(p, splits, st);
     else splits = launch<16, 8, 64, 2, 2, true>(p, splits, st);

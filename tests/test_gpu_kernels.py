@@ -1337,16 +1337,20 @@ def test_conv3x3_small_tiles_forced(B, Hs, Cin, N, up, use_ab):
         hip().set_tune(hip().TUNE_CONV3_SMALL, 0)
 
 
+@pytest.mark.parametrize("waves", [0, 1])
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab", [(2, 16, 64, 64, 0, True), (2, 16, 128, 128, 1, False),
                                                   (1, 32, 256, 64, 0, True)])
-def test_conv3x3_big_tiles_forced(B, Hs, Cin, N, up, use_ab):
-    """TUNE_CONV3_BIG=2 forces the 16x16-pixel tiles of the large-M layers (several chunks, upsampled input) vs the
-    generic implicit GEMM and the fp32 reference."""
+def test_conv3x3_big_tiles_forced(B, Hs, Cin, N, up, use_ab, waves):
+    """TUNE_CONV3_BIG=2 forces the 16x16-pixel tiles of the large-M layers (several chunks, upsampled input) - with
+    the default 4 x 1 wave grid (waves=0) and the 2 x 2 one (TUNE_CONV3_BIG_WAVES=1) - vs the generic implicit GEMM
+    and the fp32 reference."""
     hip().set_tune(hip().TUNE_CONV3_BIG, 2)
+    hip().set_tune(hip().TUNE_CONV3_BIG_WAVES, waves)
     try:
         test_conv3x3_halo_tile_matches_generic(B, Hs, Cin, N, up, use_ab)
     finally:
         hip().set_tune(hip().TUNE_CONV3_BIG, 0)
+        hip().set_tune(hip().TUNE_CONV3_BIG_WAVES, 0)
 
 
 @pytest.mark.parametrize("B,Hs,Cin,N,up,use_ab,grid", [
