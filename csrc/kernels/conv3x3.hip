@@ -806,14 +806,16 @@ static bool small_tiles(const ConvParams& p) {
   return blocks < 192 && p.Cin / BK >= 2 && small >= 384;
 }
 
-// Large-M layers (the 64^2 / 128^2 decoder levels at the 512^2 planned batch: 4.5-18M pixels, Cin 64-256): 16x16-
+// Large-M layers (the 32^2-128^2 decoder levels at the 512^2 planned batch: 1.1-18M pixels, Cin 64-256): 16x16-
 // pixel tiles. The whole-chunk weight tile (9 taps x 64 x 32, 36 KB) is re-read from L2 for every pixel tile, and at
 // this M the 8x16 tiles ran at ~28 % of the MFMA peak on that L2 stream; 256 pixels per tile halve the weight bytes
 // per MFMA. TUNE_CONV3_BIG: 1 = off, 2 = whenever the shape allows.
 static bool big_tiles(const ConvParams& p) {
   const int v = cfl_tune(TUNE_CONV3_BIG);
   if (v == 1 || p.pj.v || !use_wb(p) || wb_bn(p) != 64 || p.Ho % 16 || p.Wo % 16) return false;
-  return v == 2 || (int64_t)p.B * p.Ho * p.Wo >= (1 << 22);
+  // (>= 1M pixels: the 32^2 level at the 512^2 planned batch, 1.1M, gained 250-430 us per call over the 8x16 tiles
+  // with the 4 x 1 wave grid - profiles/r5_conv/trace_ab_big_tiles_1M_512.txt; the 256^2 bench's largest is 262k)
+  return v == 2 || (int64_t)p.B * p.Ho * p.Wo >= (1 << 20);
 }
 
 bool conv3x3_deep_eligible(const ConvParams& p);
