@@ -852,11 +852,13 @@ int conv3x3_deep(const ConvParams& p, hipStream_t st);
 
 int conv3x3(const ConvParams& p, hipStream_t st) {
   if (p.wt8) {
-    // block-scaled fp8 operands (fp8.hip). TUNE_CONV3_F8: 0 = default - fp8 unless the bf16 weight-stationary kernel
-    // takes the call (Cin <= 64 at the high-resolution levels, where it beat the fp8 per-tile kernel at 512^2:
-    // profiles/r5_fp8), 1 = never, 2 = every call that carries fp8 operands
+    // block-scaled fp8 operands (fp8.hip). TUNE_CONV3_F8: 0 = default - fp8 for the decoder node-join data gradients
+    // (the convT1 dgrads with the pj epilogue) unless the bf16 weight-stationary kernel takes the call; the other
+    // calls measured faster on the bf16 kernels once those moved to 16x16 tiles on a 4 x 1 wave grid (per position
+    // at 512^2: bf16 -77 .. -276 us, the node-join form +217 us - profiles/r5_conv/trace_ab_fp8_routing_512.txt),
+    // 1 = never, 2 = every call that carries fp8 operands, 3 = every call the weight-stationary kernel does not take
     const int v = cfl_tune(TUNE_CONV3_F8);
-    if (v == 2 || (v == 0 && !ws_eligible(p))) return conv3x3_f8(p, st);
+    if (v == 2 || (v == 3 && !ws_eligible(p)) || (v == 0 && p.pj.v && !ws_eligible(p))) return conv3x3_f8(p, st);
     ConvParams q = p;
     q.wt8 = nullptr;
     q.ws8 = nullptr;

@@ -501,9 +501,10 @@ bool conv3x3_f8_supported(const ConvParams& p) {
 int conv3x3_f8(const ConvParams& p, hipStream_t st) {
   if (!conv3x3_f8_supported(p)) return 1;
   const bool bn64 = p.N % 64 == 0;
-  // 16 x 16 pixel tiles at large M (as the bf16 whole-chunk path's TUNE_CONV3_BIG), else 8 x 16 / 16 x 8
-  if ((int64_t)p.B * p.Ho * p.Wo >= (1 << 22) && p.Ho % 16 == 0 && p.Wo % 16 == 0 && !p.pj.v)
-    return bn64 ? launch_f8<16, 16, 64, 2, 2>(p, st) : launch_f8<16, 16, 32, 4, 1>(p, st);
+  // 16 x 16 pixel tiles from 1M output pixels (as the bf16 whole-chunk path's TUNE_CONV3_BIG), on a 4 x 1 wave grid
+  // (64 px x 64 ch per wave: 4 instead of 5 fragment reads per 4 MFMAs), else 8 x 16 / 16 x 8
+  if ((int64_t)p.B * p.Ho * p.Wo >= (1 << 20) && p.Ho % 16 == 0 && p.Wo % 16 == 0 && !p.pj.v)
+    return bn64 ? launch_f8<16, 16, 64, 4, 1>(p, st) : launch_f8<16, 16, 32, 4, 1>(p, st);
   if (p.Wo >= 16) return bn64 ? launch_f8<8, 16, 64, 2, 2>(p, st) : launch_f8<8, 16, 32, 4, 1>(p, st);
   return bn64 ? launch_f8<16, 8, 64, 2, 2>(p, st) : launch_f8<16, 8, 32, 4, 1>(p, st);
 }

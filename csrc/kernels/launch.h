@@ -524,8 +524,9 @@ enum TuneKey {
   TUNE_WGRAD3_SK = 48,         // halo wgrad split-K-in-block body (wgrad3_sk_body.h): 0 / 1 = off (default; measured
                                //   slower in the mixed launch), 2 = every halo wgrad, 3 = maps <= 64^2
   TUNE_WGRAD3_SK_MINTILES = 49, // ... min 128-pixel tiles per block (default 16)
-  TUNE_CONV3_F8 = 50,          // fp8 3x3 routing: 0 = default (fp8 unless the weight-stationary bf16 kernel takes the call),
-                               //   1 = never, 2 = every call carrying fp8 operands
+  TUNE_CONV3_F8 = 50,          // fp8 3x3 routing: 0 = default (fp8 for the node-join dgrads the weight-stationary bf16
+                               //   kernel does not take), 1 = never, 2 = every call carrying fp8 operands, 3 = every
+                               //   call the weight-stationary kernel does not take
   TUNE_DW_BWD_DMA = 51,        // fused depthwise backward: 0 = default (LDS-DMA dy ring kernel, 3 blocks / CU, when
                                //   the launch has >= 1,536 strips, else the register-staged two-ring kernel), 1 = always
                                //   the DMA kernel, 2 = never
