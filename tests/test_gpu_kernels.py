@@ -994,6 +994,56 @@ def test_engine_fp8_step_tracks_bf16(fp8_forced):
             assert c > 0.9, (ly.name, c)
 
 
+@pytest.mark.parametrize("which", ["dw_dma", "wide", "big", "all"])
+def test_engine_large_launch_paths_match_default(which):
+    """The engine with the paths the 512^2 planned batch selects by size forced at a small shape - the LDS-DMA fused
+    depthwise backward (DW_BWD_DMA = 1), the 64-input-channel halo weight-gradient blocks (WGRAD3_WIDE = 2, their slab
+    rows sized at engine build) and the 16x16-pixel 3x3 tiles (CONV3_BIG = 2) - takes the same training step as the
+    default engine. Both run in deterministic mode (int64 fixed-point cross-block reductions), so float-atomic ordering
+    noise is gone: the DMA depthwise backward computes the same sums in the same order, and the wide wgrad's slab rows
+    are summed exactly in fixed point, so both give bit-identical gradients (measured: rel 0.0); the big tiles reorder
+    the MFMA K sums of the forward, which flips bf16 output roundings that the backward of a random-init net
+    amplifies (measured: loss rel 1.2e-4, gradient rel 3.9e-3), so they match to the tolerances below."""
+    from crack_detection_federatedlearning_grpc_amd.data.device import make_synthetic_device
+    from crack_detection_federatedlearning_grpc_amd.models.engine import UNetEngine
+    from crack_detection_federatedlearning_grpc_amd.models.spec import ParamTable
+    C_ = hip()
+    table = ParamTable()
+    data = make_synthetic_device(8, 128, seed=11)
+    flat = table.init_flat(11)
+    all_knobs = {"dw_dma": (C_.TUNE_DW_BWD_DMA, 1), "wide": (C_.TUNE_WGRAD3_WIDE, 2), "big": (C_.TUNE_CONV3_BIG, 2)}
+    knobs = list(all_knobs.values()) if which == "all" else [all_knobs[which]]
+    res = []
+    try:
+        for forced in (False, True):
+            for k, v in all_knobs.values():
+                C_.set_tune(k, 0)
+            if forced:
+                for k, v in knobs:
+                    C_.set_tune(k, v)
+            eng = UNetEngine(table, 4, 128, deterministic=True)
+            eng.bind_data(data.images, data.masks)
+            eng.set_flat(flat)
+            eng.idx.copy_(torch.arange(4, dtype=torch.int32, device=DEV))
+            eng._zero_step()
+            eng.forward(True)
+            eng.backward()
+            torch.cuda.synchronize()
+            res.append((eng.read_metrics("train")["loss"], eng.grad.clone()))
+            del eng
+    finally:
+        for k, _ in all_knobs.values():
+            C_.set_tune(k, 0)
+        C_.set_det(0)
+    (l0, g0), (l1, g1) = res
+    print(which, "loss", l0, l1, "grad rel", rel(g1, g0))
+    if which in ("dw_dma", "wide"):
+        assert abs(l1 - l0) / l0 < 1e-12 and torch.equal(g1, g0), (l0, l1, rel(g1, g0))
+    else:
+        assert abs(l1 - l0) / l0 < 1e-3, (l0, l1)
+        assert rel(g1, g0) < 1e-2, rel(g1, g0)
+
+
 @pytest.mark.parametrize("ks,stride,up,Cin,N,H", [(3, 1, 0, 64, 64, 16), (3, 1, 1, 32, 32, 8), (1, 1, 0, 32, 64, 8),
                                                   (1, 2, 0, 64, 32, 16), (3, 1, 0, 32, 32, 128)])
 def test_conv_wgrad_slab_rows_sum_to_direct(ks, stride, up, Cin, N, H):
