@@ -11,6 +11,14 @@ constexpr int NT = 256;
 constexpr int CB = 32;            // input channels per block (the A-operand rows) of the default configs
 constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;
+// hp / HW for 0 <= hp < HP as (hp * HW_MAGIC) >> 16 (one full-rate 24-bit multiply)
+constexpr unsigned HW_MAGIC = (65536u + HW - 1) / HW;
+constexpr bool hw_magic_ok() {
+  for (int hp = 0; hp < HP; ++hp)
+    if ((int)((hp * HW_MAGIC) >> 16) != hp / HW) return false;
+  return true;
+}
+static_assert(hw_magic_ok(), "halo pixel division by multiply-shift");
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
@@ -73,34 +81,45 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
   // latency (~2.4 us per 128-pixel tile against ~0.5 us of MFMAs).
   uint4 rh[H_PER_T], rd[D_PER_T];
   uint32_t hval = 0, dval = 0;
+  // Chunk addressing: a thread's 16-byte channel piece is the same in every chunk (NT % QP == 0, NT % (BNO/8) == 0)
+  // and its chunk pixels step by a constant, so per tile a chunk costs a few full-rate ops: 24-bit products into a
+  // 32-bit byte offset from the tile image's base pointer (uniform, 64-bit: one layer of the 512^2 planned batch
+  // spans more than 4 GB, one image never does). The generic form (64-bit products and runtime divisions per chunk,
+  // ~150 VALU ops of which ~50 quarter-rate) took ~1,350 of the ~4,900 cycles of a 128-pixel tile step (s_memtime
+  // phase stamps of wave 0: issue 1.35k, MFMAs 1.57k, store 1.63k, barrier 0.13k).
+  const int hq = tid % QP, hp0 = tid / QP;
+  const int dq = tid % (BNO / 8), dp0 = tid / (BNO / 8);
+  const unsigned x_row = (unsigned)p.Win * p.Cin * 2u, x_px = (unsigned)p.Cin * 2u;
+  const unsigned d_row = (unsigned)p.Wo * p.N * 2u, d_px = (unsigned)p.N * 2u;
   auto load = [&](int t) {
     const int b = t / (tiles_w * tiles_h);
     const int r = t - b * tiles_w * tiles_h;
     const int ty0 = (r / tiles_w) * TH, tx0 = (r % tiles_w) * TW;
+    const char* xb = reinterpret_cast<const char*>(p.x + (size_t)b * p.Hin * p.Win * p.Cin + cbase) + hq * 16;
+    const char* db = reinterpret_cast<const char*>(p.dy + (size_t)b * p.Ho * p.Wo * p.N + nBlock) + dq * 16;
     hval = 0;
     dval = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
-      const int e = tid + i * NT;
-      const int ec = e < HALO_CH ? e : HALO_CH - 1;
-      const int hp = ec / QP, q = ec % QP;
-      const int hy = hp / HW, hx = hp - hy * HW;
-      const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
-      const bool ok = e < HALO_CH && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
-      const int iyc = imin(imax(iy, 0), Hl - 1), ixc = imin(imax(ix, 0), Wl - 1);
-      rh[i] = *reinterpret_cast<const uint4*>(
-          p.x + (((size_t)b * p.Hin + (iyc >> p.up_in)) * p.Win + (ixc >> p.up_in)) * p.Cin + cbase + q * 8);
+      const int hp = hp0 + i * (NT / QP);
+      const bool in = (i + 1) * NT <= HALO_CH || hp < HP;
+      const int hpc = (i + 1) * NT <= HALO_CH ? hp : imin(hp, HP - 1);
+      const int hy = (int)__umul24((unsigned)hpc, HW_MAGIC) >> 16, hx = hpc - hy * HW;
+      const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
+      const bool ok = in && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
+      const unsigned iyc = (unsigned)imin(imax(iy, 0), Hl - 1) >> p.up_in;
+      const unsigned ixc = (unsigned)imin(imax(ix, 0), Wl - 1) >> p.up_in;
+      rh[i] = *reinterpret_cast<const uint4*>(xb + (__umul24(iyc, x_row) + __umul24(ixc, x_px)));
       hval |= (uint32_t)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < D_PER_T; ++i) {
-      const int e = tid + i * NT;
-      const int ec = e < D_CH ? e : D_CH - 1;
-      const int pp = ec / (BNO / 8), q = ec % (BNO / 8);
+      const int pp = dp0 + i * (NT / (BNO / 8));
+      const bool in = (i + 1) * NT <= D_CH || pp < TP;
       const int oy = ty0 + pp / TW, ox = tx0 + pp % TW;
-      const bool ok = e < D_CH && oy < p.Ho && ox < p.Wo;
-      rd[i] = *reinterpret_cast<const uint4*>(
-          p.dy + (((size_t)b * p.Ho + imin(oy, p.Ho - 1)) * p.Wo + imin(ox, p.Wo - 1)) * p.N + nBlock + q * 8);
+      const bool ok = in && oy < p.Ho && ox < p.Wo;
+      const unsigned oyc = (unsigned)imin(oy, p.Ho - 1), oxc = (unsigned)imin(ox, p.Wo - 1);
+      rd[i] = *reinterpret_cast<const uint4*>(db + (__umul24(oyc, d_row) + __umul24(oxc, d_px)));
       dval |= (uint32_t)ok << i;
     }
   };
