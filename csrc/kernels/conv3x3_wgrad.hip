@@ -89,9 +89,10 @@ int conv3x3_wgrad_cbt(const WgradParams& p) {
 }
 
 bool conv3x3_wgrad_supported(const WgradParams& p) {
-  // the body addresses one image with 32-bit byte offsets built from 24-bit products (wgrad3_body.h load)
-  const bool fits = (int64_t)p.Hin * p.Win * p.Cin * 2 < (1ll << 32) && (int64_t)p.Win * p.Cin * 2 < (1 << 24) &&
-                    (int64_t)p.Ho * p.Wo * p.N * 2 < (1ll << 32) && (int64_t)p.Wo * p.N * 2 < (1 << 24);
+  // the body reads one image through a buffer resource with 32-bit byte offsets built from 24-bit products, and
+  // 0x80000000 as its out-of-range offset (wgrad3_body.h load)
+  const bool fits = (int64_t)p.Hin * p.Win * p.Cin * 2 < (1ll << 31) && (int64_t)p.Win * p.Cin * 2 < (1 << 24) &&
+                    (int64_t)p.Ho * p.Wo * p.N * 2 < (1ll << 31) && (int64_t)p.Wo * p.N * 2 < (1 << 24);
   return p.ks == 3 && p.stride == 1 && p.pad_t == 1 && p.pad_l == 1 && p.Cin % CB == 0 && p.N % 32 == 0 &&
          p.Ho >= 8 && p.Wo >= 8 && fits;
 }

@@ -22,6 +22,19 @@ static_assert(hw_magic_ok(), "halo pixel division by multiply-shift");
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
+typedef short s2v_ __attribute__((ext_vector_type(2)));
+
+// two bf16 of a halo chunk (one dword) -> max(a * x + b, lo) in bf16, with one packed fp32 FMA, the hardware bf16
+// pack and a packed signed 16-bit max: every negative bf16 is a negative int16, so max with 0 is the exact ReLU and
+// max with 0x8000 (the int16 minimum) the identity
+CFL_DEVICE uint32_t xform2(uint32_t w, f32x2_t a, f32x2_t b, uint32_t lo) {
+  const f32x2_t x = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+  const f32x2_t y = __builtin_elementwise_fma(a, x, b);
+  const s2v_ r = __builtin_elementwise_max(__builtin_bit_cast(s2v_, __builtin_convertvector(y, bf16x2_t)),
+                                           __builtin_bit_cast(s2v_, lo));
+  return __builtin_bit_cast(uint32_t, r);
+}
+
 CFL_DEVICE s4v tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(p));
 }
@@ -80,7 +93,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
   // transformed right after the load, the prefetch was consumed at issue and every tile waited its full load
   // latency (~2.4 us per 128-pixel tile against ~0.5 us of MFMAs).
   uint4 rh[H_PER_T], rd[D_PER_T];
-  uint32_t hval = 0, dval = 0;
+  uint32_t hval = 0;
   // Chunk addressing: a thread's 16-byte channel piece is the same in every chunk (NT % QP == 0, NT % (BNO/8) == 0)
   // and its chunk pixels step by a constant, so per tile a chunk costs a few full-rate ops: 24-bit products into a
   // 32-bit byte offset from the tile image's base pointer (uniform, 64-bit: one layer of the 512^2 planned batch
@@ -91,14 +104,18 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
   const int dq = tid % (BNO / 8), dp0 = tid / (BNO / 8);
   const unsigned x_row = (unsigned)p.Win * p.Cin * 2u, x_px = (unsigned)p.Cin * 2u;
   const unsigned d_row = (unsigned)p.Wo * p.N * 2u, d_px = (unsigned)p.N * 2u;
+  const int x_img = p.Hin * p.Win * p.Cin * 2, d_img = p.Ho * p.Wo * p.N * 2;   // < 2^31 (conv3x3_wgrad_supported)
+  constexpr uint32_t OOB = 0x80000000u;          // past every resource's range: the buffer load returns 0
   auto load = [&](int t) {
     const int b = t / (tiles_w * tiles_h);
     const int r = t - b * tiles_w * tiles_h;
     const int ty0 = (r / tiles_w) * TH, tx0 = (r % tiles_w) * TW;
-    const char* xb = reinterpret_cast<const char*>(p.x + (size_t)b * p.Hin * p.Win * p.Cin + cbase) + hq * 16;
-    const char* db = reinterpret_cast<const char*>(p.dy + (size_t)b * p.Ho * p.Wo * p.N + nBlock) + dq * 16;
+    // raw buffer resources over the tile's image (base in scalar registers: no 64-bit address math per chunk)
+    const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.x + (size_t)b * p.Hin * p.Win * p.Cin + cbase), 0, x_img, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_d = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.dy + (size_t)b * p.Ho * p.Wo * p.N + nBlock), 0, d_img, 0x00020000);
     hval = 0;
-    dval = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int hp = hp0 + i * (NT / QP);
@@ -109,51 +126,47 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
       const bool ok = in && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
       const unsigned iyc = (unsigned)imin(imax(iy, 0), Hl - 1) >> p.up_in;
       const unsigned ixc = (unsigned)imin(imax(ix, 0), Wl - 1) >> p.up_in;
-      rh[i] = *reinterpret_cast<const uint4*>(xb + (__umul24(iyc, x_row) + __umul24(ixc, x_px)));
+      const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs_x, __umul24(iyc, x_row) + __umul24(ixc, x_px) + hq * 16,
+                                                          0, 0);
+      rh[i] = make_uint4(v.x, v.y, v.z, v.w);
       hval |= (uint32_t)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < D_PER_T; ++i) {
+      // dy outside the map (a partial tile) reads as 0 from the out-of-range offset
       const int pp = dp0 + i * (NT / (BNO / 8));
-      const bool in = (i + 1) * NT <= D_CH || pp < TP;
       const int oy = ty0 + pp / TW, ox = tx0 + pp % TW;
-      const bool ok = in && oy < p.Ho && ox < p.Wo;
-      const unsigned oyc = (unsigned)imin(oy, p.Ho - 1), oxc = (unsigned)imin(ox, p.Wo - 1);
-      rd[i] = *reinterpret_cast<const uint4*>(db + (__umul24(oyc, d_row) + __umul24(oxc, d_px)));
-      dval |= (uint32_t)ok << i;
+      const bool ok = ((i + 1) * NT <= D_CH || pp < TP) && oy < p.Ho && ox < p.Wo;
+      const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+          rs_d, ok ? __umul24((unsigned)oy, d_row) + __umul24((unsigned)ox, d_px) + dq * 16 : OOB, 0, 0);
+      rd[i] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
+  const uint32_t relu_lo = p.xf.relu ? 0u : 0x80008000u;
   auto store = [&](int buf) {
     if constexpr (!AB_REG) {
-      load_f8_or(p.xf.ab + cbase + (tid % QP) * 8, has_ab, 1.f, a8);
-      load_f8_or(p.xf.ab + p.xf.C + cbase + (tid % QP) * 8, has_ab, 0.f, b8);
+      load_f8_or(p.xf.ab + cbase + hq * 8, has_ab, 1.f, a8);
+      load_f8_or(p.xf.ab + p.xf.C + cbase + hq * 8, has_ab, 0.f, b8);
     }
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
       if (e < HALO_CH) {
-        uint4 v = rh[i];
-        if (!((hval >> i) & 1u)) {
-          v = make_uint4(0, 0, 0, 0);                 // padding stays exactly 0 (TF SAME pads the transformed input)
-        } else if (has_ab || p.xf.relu) {
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (has_ab) f[j] = fmaf(a8[j], f[j], b8[j]);
-            if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
-          }
-          v = pack8(f);
-        }
-        *reinterpret_cast<uint4*>(&sH[buf][e / QP][(e % QP) * 8]) = v;
+        // producer BN-apply + ReLU, then padding exactly 0 (TF SAME pads the transformed input)
+        const uint32_t m = ((hval >> i) & 1u) ? 0xffffffffu : 0u;
+        const uint4 v = rh[i];
+        uint4 o;
+        o.x = xform2(v.x, f32x2_t{a8[0], a8[1]}, f32x2_t{b8[0], b8[1]}, relu_lo) & m;
+        o.y = xform2(v.y, f32x2_t{a8[2], a8[3]}, f32x2_t{b8[2], b8[3]}, relu_lo) & m;
+        o.z = xform2(v.z, f32x2_t{a8[4], a8[5]}, f32x2_t{b8[4], b8[5]}, relu_lo) & m;
+        o.w = xform2(v.w, f32x2_t{a8[6], a8[7]}, f32x2_t{b8[6], b8[7]}, relu_lo) & m;
+        *reinterpret_cast<uint4*>(&sH[buf][e / QP][(e % QP) * 8]) = o;
       }
     }
 #pragma unroll
     for (int i = 0; i < D_PER_T; ++i) {
       const int e = tid + i * NT;
-      if (e < D_CH)
-        *reinterpret_cast<uint4*>(&sD[buf][e / (BNO / 8)][(e % (BNO / 8)) * 8]) =
-            ((dval >> i) & 1u) ? rd[i] : make_uint4(0, 0, 0, 0);
+      if (e < D_CH) *reinterpret_cast<uint4*>(&sD[buf][e / (BNO / 8)][(e % (BNO / 8)) * 8]) = rd[i];
     }
   };
 
