@@ -969,6 +969,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_DW_BWD_DMA") = (int)TUNE_DW_BWD_DMA;
   m.attr("TUNE_WGRAD3_WIDE") = (int)TUNE_WGRAD3_WIDE;
   m.attr("TUNE_CONV3_BIG_WAVES") = (int)TUNE_CONV3_BIG_WAVES;
+  m.attr("TUNE_WGRAD_DIRECT") = (int)TUNE_WGRAD_DIRECT;
   m.attr("TUNE_HEAD_BLOCKS") = (int)TUNE_HEAD_BLOCKS;
   m.attr("TUNE_IGEMM_CFG") = (int)TUNE_IGEMM_CFG;
   m.attr("TUNE_CONV3_WB") = (int)TUNE_CONV3_WB;

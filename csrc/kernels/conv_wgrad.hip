@@ -33,7 +33,17 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
 template <int BKO, int BNO, int RM>
 constexpr int wgrad_lds_bytes() { return 2 * RM * (BKO + 16) * 2 + 2 * RM * (BNO + 16) * 2; }
 
-template <int BKO, int BNO, int RM>
+// DIRECT: a 1x1 / stride-1 / unpadded / not-upsampled conv (x pixel m = output pixel m): a step's x and dy rows are
+// contiguous, read with raw buffer loads from per-step scalar resources whose range ends at the block's last pixel
+// (past it both read 0 - a dy row of 0 contributes nothing whatever its x row holds), so a chunk costs no address
+// math, no validity bits and no masking; the x transform runs on packed fp32 FMAs (wgrad3_body.h xform2). The
+// general form decodes each chunk row's (b, oh, ow), builds 64-bit addresses and carries per-lane row counters:
+// ~30 VALU ops per chunk against 8 MFMAs per wave per step in the <64, 32, 128> config.
+constexpr bool wgrad_direct(const WgradParams& p) {
+  return p.ks == 1 && p.stride == 1 && p.pad_t == 0 && p.pad_l == 0 && p.up_in == 0 && p.K == p.Cin;
+}
+
+template <int BKO, int BNO, int RM, bool DIRECT = false>
 CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int bz, unsigned char* smem) {
   constexpr int TK = BKO / 2, TN = BNO / 2;
   constexpr int FK = TK / 16, FN = TN / 16;
@@ -74,7 +84,7 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
   // pixel decode (b, oh, ow) of each x chunk row, advanced incrementally by RM per step (no division in the loop)
   int db[XPT], doh[XPT], dow[XPT];
 #pragma unroll
-  for (int i = 0; i < XPT; ++i) {
+  for (int i = 0; i < (DIRECT ? 0 : XPT); ++i) {
     const int m = m_begin + (tid + i * NT) / XW;
     db[i] = m / HWo;
     const int r = m - db[i] * HWo;
@@ -85,7 +95,29 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
   // that the prefetch should overlap (see wgrad3_body.h)
   uint4 rx[XPT], rg[GPT];
   uint32_t xval = 0, gval = 0;
+  const uint32_t relu_lo = p.xf.relu ? 0u : 0x80008000u;
   auto load = [&](int m0) {
+    if constexpr (DIRECT) {
+      // resources from the block's first channel of the step's first pixel (uniform) to the block's last pixel
+      const int rows = m_end - m0;
+      const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.x + (size_t)m0 * p.Cin + kBlock), 0, (rows * p.Cin - kBlock) * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rs_g = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.dy + (size_t)m0 * p.N + nBlock), 0, (rows * p.N - nBlock) * 2, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int ch = tid + i * NT;
+        const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs_x, (ch / XW) * p.Cin * 2 + (ch % XW) * 16, 0, 0);
+        rx[i] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int ch = tid + i * NT;
+        const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs_g, (ch / GW) * p.N * 2 + (ch % GW) * 16, 0, 0);
+        rg[i] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      return;
+    }
     xval = 0;
     gval = 0;
 #pragma unroll
@@ -119,6 +151,27 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
     }
   };
   auto store = [&](int buf) {
+    if constexpr (DIRECT) {
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int ch = tid + i * NT;
+        if (ch < XC) {
+          const uint4 v = rx[i];
+          uint4 o;
+          o.x = wg3::xform2(v.x, f32x2_t{ca[0], ca[1]}, f32x2_t{cb[0], cb[1]}, relu_lo);
+          o.y = wg3::xform2(v.y, f32x2_t{ca[2], ca[3]}, f32x2_t{cb[2], cb[3]}, relu_lo);
+          o.z = wg3::xform2(v.z, f32x2_t{ca[4], ca[5]}, f32x2_t{cb[4], cb[5]}, relu_lo);
+          o.w = wg3::xform2(v.w, f32x2_t{ca[6], ca[7]}, f32x2_t{cb[6], cb[7]}, relu_lo);
+          *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = o;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int ch = tid + i * NT;
+        if (ch < GC) *reinterpret_cast<uint4*>(&sG[buf][ch / GW][(ch % GW) * 8]) = rg[i];
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int ch = tid + i * NT;
@@ -331,7 +384,7 @@ int launch_group(const WgradParams* ps, int n, hipStream_t st) {
 // the four launch boundaries between the groups are gone. One LDS buffer sized for the largest body (the 64-wide
 // halo config, 75.5 KB: 2 blocks per CU, as the halo groups had); the kernel's VGPR count is the largest body's.
 // kind: 0-9 halo config (conv3x3_wgrad_config; 4, 5 = the split-K-in-block body, 6-9 the 64-channel blocks), 10 + c
-// generic config c (wgrad_config; c = 1, the 80 KB
+// generic config c (wgrad_config; 20 + c: its DIRECT form, wgrad_body; c = 1, the 80 KB
 // 128-pixel-stage variant, is launched on its own)
 constexpr int MIX_MAX = 24;
 struct MixItem {
@@ -379,6 +432,12 @@ __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
     case 7: wg3::wgrad3_body<64, false, 64, true>(P, a, b, bx, by, bz, smem); break;
     case 8: wg3::wgrad3_body<32, true, 64, true>(P, a, b, bx, by, bz, smem); break;
     case 9: wg3::wgrad3_body<32, false, 64, true>(P, a, b, bx, by, bz, smem); break;
+    case 20: wgrad_body<128, 128, 32, true>(P, a, bx, by, bz, smem); break;
+    case 26: wgrad_body<128, 128, 64, true>(P, a, bx, by, bz, smem); break;
+    case 22: wgrad_body<64, 32, 128, true>(P, a, bx, by, bz, smem); break;
+    case 23: wgrad_body<32, 64, 128, true>(P, a, bx, by, bz, smem); break;
+    case 24: wgrad_body<32, 32, 128, true>(P, a, bx, by, bz, smem); break;
+    case 25: wgrad_body<64, 64, 64, true>(P, a, bx, by, bz, smem); break;
     case 10: wgrad_body<128, 128, 32>(P, a, bx, by, bz, smem); break;
     case 16: wgrad_body<128, 128, 64>(P, a, bx, by, bz, smem); break;
     case 12: wgrad_body<64, 32, 128>(P, a, bx, by, bz, smem); break;
@@ -471,7 +530,7 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
         zs = it.b;
       } else {
         int bko, bno, rm;
-        it.kind = 10 + wgrad_config(p, bko, bno, rm);
+        it.kind = (wgrad_direct(p) && cfl_tune(TUNE_WGRAD_DIRECT) != 1 ? 20 : 10) + wgrad_config(p, bko, bno, rm);
         wgrad_shape(p, bko, bno, rm, it.a, zs);
         it.b = 0;
         it.gx = p.K / bko;

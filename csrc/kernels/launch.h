@@ -533,7 +533,8 @@ enum TuneKey {
   TUNE_WGRAD3_WIDE = 52,       // halo wgrad 64-input-channel blocks (one LDS buffer): 0 = default (launches of >= 64k
                                //   32-channel tile-blocks: the 512^2 planned batch), 1 = never, 2 = whenever Cin % 64 == 0
   TUNE_CONV3_BIG_WAVES = 53,   // conv3x3 16x16-pixel tiles: wave grid 0 = default (4 x 1: 64 px x 64 ch per wave), 1 = 2 x 2
-  TUNE_N = 54
+  TUNE_WGRAD_DIRECT = 54,      // generic wgrad, 1x1 / stride-1 convs in the mixed launch: 0 = direct-row body, 1 = general
+  TUNE_N = 55
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);

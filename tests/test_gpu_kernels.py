@@ -1941,8 +1941,9 @@ def test_conv_wgrad_batch_grouped_equals_individual(mix, wide):
     """conv_wgrad_batch (the engine's deferred weight gradients): every wgrad in ONE mixed launch (default, mix=0)
     or 3x3 halo wgrads of different layers grouped into shared launches per tile config (mix=1) - bit-identical
     slabs to one call each - and generic 1x1 wgrads in the same mixed launch or grouped per tile config
-    (replica-row atomics: equal up to float summation order). wide=2: the halo items with Cin % 64 == 0 on the
-    64-channel bodies (mixed-launch kinds 6-9)."""
+    (replica-row atomics: equal up to float summation order; in the mixed launch the 1x1 / stride-1 ones run the
+    direct-row body, kinds 20+, against the general body of the single calls). wide=2: the halo items with
+    Cin % 64 == 0 on the 64-channel bodies (mixed-launch kinds 6-9)."""
     torch.manual_seed(41)
     C_ = hip()
     C_.set_tune(C_.TUNE_WGRAD_MIX, mix)
@@ -1950,7 +1951,10 @@ def test_conv_wgrad_batch_grouped_equals_individual(mix, wide):
     shapes = [  # (B, Hin, Cin, up, Ho, N, ks, dst_mode)
         (2, 16, 64, 0, 16, 32, 3, 1), (2, 8, 64, 1, 16, 32, 3, 1), (2, 16, 32, 0, 16, 64, 3, 1),
         (2, 16, 64, 0, 16, 64, 3, 1), (2, 16, 32, 0, 16, 64, 1, 0), (3, 8, 32, 0, 8, 32, 3, 0),
-        (2, 32, 64, 0, 32, 64, 1, 0), (2, 16, 128, 0, 16, 256, 1, 0), (4, 8, 256, 0, 8, 128, 1, 0)]
+        (2, 32, 64, 0, 32, 64, 1, 0), (2, 16, 128, 0, 16, 256, 1, 0), (4, 8, 256, 0, 8, 128, 1, 0),
+        # pixel counts off the 32 / 64 / 128-pixel steps: the direct-row 1x1 body's last step reads past the block's
+        # end as zeros (buffer range)
+        (3, 12, 32, 0, 12, 64, 1, 0), (5, 20, 64, 0, 20, 32, 1, 0), (3, 10, 128, 0, 10, 128, 1, 0)]
     calls = []
     for B, Hin, Cin, up, Ho, N, ks, dm in shapes:
         x, _ = bf(torch.randn(B, Hin, Hin, Cin))
