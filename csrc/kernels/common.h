@@ -52,6 +52,51 @@ CFL_DEVICE uint4 pack8(const float* f) {
 
 CFL_DEVICE void load8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
 
+typedef short s2v_ __attribute__((ext_vector_type(2)));
+
+// two bf16 (one dword of a staged chunk) -> max(a * x + b, lo) in bf16, with one packed fp32 FMA, the hardware bf16
+// pack and a packed signed 16-bit max: every negative bf16 is a negative int16, so max with 0 is the exact ReLU and
+// max with 0x8000 (the int16 minimum) the identity. lo: 0 (ReLU) or 0x80008000u (none), a = 1 / b = 0 without a BN.
+CFL_DEVICE uint32_t xform2(uint32_t w, f32x2_t a, f32x2_t b, uint32_t lo) {
+  const f32x2_t x = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+  const f32x2_t y = __builtin_elementwise_fma(a, x, b);
+  const s2v_ r = __builtin_elementwise_max(__builtin_bit_cast(s2v_, __builtin_convertvector(y, bf16x2_t)),
+                                           __builtin_bit_cast(s2v_, lo));
+  return __builtin_bit_cast(uint32_t, r);
+}
+// 8 channels (a 16-byte chunk) through xform2, then AND-masked (m = 0 zeroes padding exactly)
+CFL_DEVICE uint4 xform8(const uint4& v, const float* a, const float* b, uint32_t lo, uint32_t m) {
+  return make_uint4(xform2(v.x, f32x2_t{a[0], a[1]}, f32x2_t{b[0], b[1]}, lo) & m,
+                    xform2(v.y, f32x2_t{a[2], a[3]}, f32x2_t{b[2], b[3]}, lo) & m,
+                    xform2(v.z, f32x2_t{a[4], a[5]}, f32x2_t{b[4], b[5]}, lo) & m,
+                    xform2(v.w, f32x2_t{a[6], a[7]}, f32x2_t{b[6], b[7]}, lo) & m);
+}
+
+// x / D for small non-negative x as one full-rate 24-bit multiply and a shift; div_small_ok<D, N>() checks it for
+// every x < N at compile time (static_assert at each use)
+template <int D>
+constexpr uint32_t div_magic16() { return (65536u + D - 1) / D; }
+template <int D, int N>
+constexpr bool div_small_ok() {
+  for (int x = 0; x < N; ++x)
+    if ((int)((x * div_magic16<D>()) >> 16) != x / D) return false;
+  return true;
+}
+template <int D>
+CFL_DEVICE int div_small(int x) { return (int)(__umul24((unsigned)x, div_magic16<D>()) >> 16); }
+
+// Raw buffer access: a wave-uniform resource (base, byte range) in scalar registers, 32-bit per-lane byte offsets and
+// a scalar offset; an offset past the range (CFL_OOB) reads 0. The halo / row loaders use these instead of 64-bit
+// per-lane address math.
+constexpr uint32_t CFL_OOB = 0x80000000u;
+CFL_DEVICE __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+CFL_DEVICE uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 CFL_DEVICE void load_f8(const float* p, float* f) {
   const float4 a = *reinterpret_cast<const float4*>(p);
   const float4 b = *reinterpret_cast<const float4*>(p + 4);

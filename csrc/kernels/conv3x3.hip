@@ -103,44 +103,37 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
       load_f8_or(p.xf.ab + p.xf.C + c8, has_ab, 0.f, hb);
     }
   };
-  auto load_halo = [&](int chunk) {
-    const int cbase = chunk * BK;
-    if (!XFIN) load_coefs(chunk);                       // (XFIN: after the prologue, below)
-    uint32_t hv = 0;
+  // The block's halo pieces sit at the same pixels for every chunk: their byte offsets in the tile image (padding:
+  // the out-of-range offset, read as 0) are computed once, and a chunk's loads are buffer loads with the chunk as
+  // the scalar offset - no per-chunk address math and no per-lane branch around a load.
+  static_assert(div_small_ok<HW, H_PER_T * NT / 4>(), "halo pixel division");
+  const __amdgpu_buffer_rsrc_t rs_x =
+      buf_rsrc(p.x + (size_t)b * p.Hin * p.Win * p.Cin, (uint32_t)p.Hin * p.Win * p.Cin * 2u);
+  uint32_t hoff[H_PER_T], hv_tile = 0;
 #pragma unroll
-    for (int i = 0; i < H_PER_T; ++i) {
-      const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < HALO_CHUNKS) {
-        const int hp = e >> 2, q = e & 3;
-        const int hy = hp / HW, hx = hp - hy * HW;
-        const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;      // logical input coords (pad 1)
-        if (iy >= 0 && iy < Hl && ix >= 0 && ix < Wl) {
-          const int c = cbase + q * 8;
-          v = *reinterpret_cast<const uint4*>(
-              p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + c);
-          hv |= 1u << i;
-        }
-      }
-      rh[i] = v;
-    }
-    hvalid = hv;
+  for (int i = 0; i < H_PER_T; ++i) {
+    const int e = tid + i * NT;
+    const int hp = e >> 2;
+    const int hy = div_small<HW>(hp), hx = hp - hy * HW;
+    const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;      // logical input coords (pad 1)
+    const bool ok = e < HALO_CHUNKS && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
+    hoff[i] = ok ? __umul24((unsigned)iy >> p.up_in, (unsigned)p.Win * p.Cin * 2u) +
+                       __umul24((unsigned)ix >> p.up_in, (unsigned)p.Cin * 2u) + (tid & 3) * 16u
+                 : CFL_OOB;
+    hv_tile |= (ok ? 1u : 0u) << i;
+  }
+  auto load_halo = [&](int chunk) {
+    if (!XFIN) load_coefs(chunk);                       // (XFIN: after the prologue, below)
+#pragma unroll
+    for (int i = 0; i < H_PER_T; ++i) rh[i] = buf_load16(rs_x, hoff[i], chunk * BK * 2);
+    hvalid = hv_tile;
   };
-  // producer BN-apply + ReLU of the raw halo in rh; padding stays exactly 0 (it is outside the transform)
+  // producer BN-apply + ReLU of the raw halo in rh (packed, common.h xform8); padding stays exactly 0
+  const uint32_t relu_lo = relu ? 0u : 0x80008000u;
   auto xform_halo = [&]() {
     if (!(has_ab || relu)) return;
 #pragma unroll
-    for (int i = 0; i < H_PER_T; ++i) {
-      if (!((hvalid >> i) & 1u)) continue;
-      float f[8];
-      unpack8(rh[i], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f[j] = fmaf(ha[j], f[j], hb[j]);
-        if (relu) f[j] = fmaxf(f[j], 0.f);
-      }
-      rh[i] = pack8(f);
-    }
+    for (int i = 0; i < H_PER_T; ++i) rh[i] = xform8(rh[i], ha, hb, relu_lo, ((hvalid >> i) & 1u) ? 0xffffffffu : 0u);
   };
   auto store_halo = [&](int buf) {
 #pragma unroll
@@ -153,16 +146,16 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
     }
   };
   // ---- weight tile of K-step (chunk, tap): wt[n][tap*Cin + chunk*32 .. +32) ----
+  // (buffer loads over the weight matrix; a piece's row / quarter is fixed, the tap and chunk are scalar offsets)
+  const __amdgpu_buffer_rsrc_t rs_w = buf_rsrc(p.wt, (uint32_t)p.N * p.K * 2u);
   uint4 rb[B_PER_T];
   auto load_b = [&](int chunk, int tap) {
-    const size_t kofs = (size_t)tap * p.Cin + chunk * BK;
+    const uint32_t kofs = (uint32_t)(tap * p.Cin + chunk * BK) * 2u;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);   // unconditional register write: a conditionally written array goes to scratch
-      if (B_CHUNKS % NT == 0 || e < B_CHUNKS)
-        v = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (e >> 2)) * p.K + kofs + (e & 3) * 8);
-      rb[i] = v;
+      rb[i] = buf_load16(rs_w, (B_CHUNKS % NT == 0 || e < B_CHUNKS)
+                                   ? (uint32_t)((nBlock + (e >> 2)) * p.K + (e & 3) * 8) * 2u : CFL_OOB, kofs);
     }
   };
   auto store_b = [&](int buf) {
@@ -175,17 +168,17 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 
   // ---- whole-chunk weight tiles (WB): piece e -> tap e / B_CHUNKS, row n, 16-byte quarter q ----
   uint4 rbw[BW_PER_T];
+  // NT % B_CHUNKS == 0 (B_CHUNKS = 128 / 256): piece i's tap is i * (NT / B_CHUNKS) + tid / B_CHUNKS and its weight
+  // row / quarter tid % B_CHUNKS - one per-thread offset, the tap and chunk in the scalar offset
+  static_assert(!WB || NT % B_CHUNKS == 0, "whole-chunk weight pieces");
+  const int bw_w = tid % B_CHUNKS;
+  const uint32_t bw_off = (uint32_t)((nBlock + (bw_w >> 2)) * p.K + (tid / B_CHUNKS) * p.Cin + (bw_w & 3) * 8) * 2u;
   auto load_bw = [&](int chunk) {
 #pragma unroll
     for (int i = 0; i < BW_PER_T; ++i) {
       const int e = tid + i * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (BW_CHUNKS % NT == 0 || e < BW_CHUNKS) {
-        const int tap = e / B_CHUNKS, w = e - tap * B_CHUNKS;
-        v = *reinterpret_cast<const uint4*>(p.wt + (size_t)(nBlock + (w >> 2)) * p.K + (size_t)tap * p.Cin +
-                                            chunk * BK + (w & 3) * 8);
-      }
-      rbw[i] = v;
+      rbw[i] = buf_load16(rs_w, (BW_CHUNKS % NT == 0 || e < BW_CHUNKS) ? bw_off : CFL_OOB,
+                          (uint32_t)(i * (NT / B_CHUNKS) * p.Cin + chunk * BK) * 2u);
     }
   };
   auto store_bw = [&]() {
@@ -530,55 +523,46 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
     ty0 = (t / tiles_w) * TH;
     tx0 = (t % tiles_w) * TW;
   };
-  // raw halo of a tile into registers (no use of the values here: the loads stay in flight)
+  // raw halo of a tile into registers (no use of the values here: the loads stay in flight). Buffer loads from the
+  // tile image's resource: a piece costs a few full-rate ops (24-bit products into a 32-bit offset; padding = the
+  // out-of-range offset, read as 0 - no per-lane branch around the load) and the chunk is the scalar offset.
   uint4 rh[CH][H_PER_T];
   uint32_t rvalid = 0;                                  // bit i: piece i lies inside the image
+  const uint32_t x_row = (uint32_t)p.Win * p.Cin * 2u, x_px = (uint32_t)p.Cin * 2u;
+  const uint32_t x_img = (uint32_t)p.Hin * p.Win * p.Cin * 2u;
+  static_assert(div_small_ok<HW, H_PER_T * NT / 4>(), "halo pixel division");
   auto load_halo = [&](int item) {
     int b, ty0, tx0;
     tile_of(item, b, ty0, tx0);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(p.x + (size_t)b * p.Hin * p.Win * p.Cin, x_img);
     rvalid = 0;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
-      const int hp = e >> 2, q = e & 3;
-      const int hy = hp / HW, hx = hp - hy * HW;
+      const int hp = e >> 2;
+      const int hy = div_small<HW>(hp), hx = hp - hy * HW;
       const int iy = ty0 + hy - 1, ix = tx0 + hx - 1;
-      const bool ok = e < HALO_CHUNKS && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+      const bool ok = e < HALO_CHUNKS && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
       rvalid |= (ok ? 1u : 0u) << i;
-      const bf16_t* src = p.x + (((size_t)b * p.Hin + (iy >> p.up_in)) * p.Win + (ix >> p.up_in)) * p.Cin + q * 8;
+      const uint32_t off = ok ? __umul24((unsigned)iy >> p.up_in, x_row) + __umul24((unsigned)ix >> p.up_in, x_px) +
+                                    (tid & 3) * 16u
+                              : CFL_OOB;
 #pragma unroll
-      for (int ch = 0; ch < CH; ++ch) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ok) v = *reinterpret_cast<const uint4*>(src + ch * BK);
-        rh[ch][i] = v;
-      }
+      for (int ch = 0; ch < CH; ++ch) rh[ch][i] = buf_load16(rs, off, ch * BK * 2);
     }
   };
-  // producer BN-apply + ReLU on the way into LDS; padding stays exactly 0 (it is outside the transform)
+  // producer BN-apply + ReLU on the way into LDS (packed, common.h xform8); padding stays exactly 0
+  const uint32_t relu_lo = relu ? 0u : 0x80008000u;
   auto store_halo = [&]() {
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
       const int e = tid + i * NT;
       if (e >= HALO_CHUNKS) continue;
-      const bool ok = (rvalid >> i) & 1u;
+      const uint32_t m = ((rvalid >> i) & 1u) ? 0xffffffffu : 0u;
 #pragma unroll
-      for (int ch = 0; ch < CH; ++ch) {
-        uint4 v = rh[ch][i];
-        if (has_ab || relu) {
-          float f[8];
-          unpack8(v, f);
-          if (has_ab) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaf(a8[ch][j], f[j], b8[ch][j]);
-          }
-          if (relu) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-          }
-          v = ok ? pack8(f) : make_uint4(0, 0, 0, 0);
-        }
-        *reinterpret_cast<uint4*>(sH + ch * HP * LDH + swz_off(e >> 2, e & 3)) = v;
-      }
+      for (int ch = 0; ch < CH; ++ch)
+        *reinterpret_cast<uint4*>(sH + ch * HP * LDH + swz_off(e >> 2, e & 3)) =
+            xform8(rh[ch][i], a8[ch], b8[ch], relu_lo, m);
     }
   };
 
@@ -843,8 +827,10 @@ int conv3x3_split_k(const ConvParams& p) {
 }
 
 bool conv3x3_supported(const ConvParams& p) {
+  // the halo loaders read one image through a buffer resource with 32-bit offsets from 24-bit row / pixel products
+  const bool fits = (int64_t)p.Hin * p.Win * p.Cin * 2 < (1ll << 31) && (int64_t)p.Win * p.Cin * 2 < (1 << 24);
   return p.ks == 3 && p.stride == 1 && p.pad_t == 1 && p.pad_l == 1 && p.Cin % BK == 0 && p.N % 32 == 0 &&
-         p.Wo >= 8 && p.Ho >= 8 && (p.N % 128 == 0 || p.N == 64 || p.N == 32);
+         p.Wo >= 8 && p.Ho >= 8 && (p.N % 128 == 0 || p.N == 64 || p.N == 32) && fits;
 }
 
 bool conv3x3_deep_eligible(const ConvParams& p);

@@ -36,7 +36,7 @@ constexpr int wgrad_lds_bytes() { return 2 * RM * (BKO + 16) * 2 + 2 * RM * (BNO
 // DIRECT: a 1x1 / stride-1 / unpadded / not-upsampled conv (x pixel m = output pixel m): a step's x and dy rows are
 // contiguous, read with raw buffer loads from per-step scalar resources whose range ends at the block's last pixel
 // (past it both read 0 - a dy row of 0 contributes nothing whatever its x row holds), so a chunk costs no address
-// math, no validity bits and no masking; the x transform runs on packed fp32 FMAs (wgrad3_body.h xform2). The
+// math, no validity bits and no masking; the x transform runs on packed fp32 FMAs (common.h xform2). The
 // general form decodes each chunk row's (b, oh, ow), builds 64-bit addresses and carries per-lane row counters:
 // ~30 VALU ops per chunk against 8 MFMAs per wave per step in the <64, 32, 128> config.
 constexpr bool wgrad_direct(const WgradParams& p) {
@@ -158,10 +158,10 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
         if (ch < XC) {
           const uint4 v = rx[i];
           uint4 o;
-          o.x = wg3::xform2(v.x, f32x2_t{ca[0], ca[1]}, f32x2_t{cb[0], cb[1]}, relu_lo);
-          o.y = wg3::xform2(v.y, f32x2_t{ca[2], ca[3]}, f32x2_t{cb[2], cb[3]}, relu_lo);
-          o.z = wg3::xform2(v.z, f32x2_t{ca[4], ca[5]}, f32x2_t{cb[4], cb[5]}, relu_lo);
-          o.w = wg3::xform2(v.w, f32x2_t{ca[6], ca[7]}, f32x2_t{cb[6], cb[7]}, relu_lo);
+          o.x = xform2(v.x, f32x2_t{ca[0], ca[1]}, f32x2_t{cb[0], cb[1]}, relu_lo);
+          o.y = xform2(v.y, f32x2_t{ca[2], ca[3]}, f32x2_t{cb[2], cb[3]}, relu_lo);
+          o.z = xform2(v.z, f32x2_t{ca[4], ca[5]}, f32x2_t{cb[4], cb[5]}, relu_lo);
+          o.w = xform2(v.w, f32x2_t{ca[6], ca[7]}, f32x2_t{cb[6], cb[7]}, relu_lo);
           *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = o;
         }
       }

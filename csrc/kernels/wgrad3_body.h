@@ -22,19 +22,6 @@ static_assert(hw_magic_ok(), "halo pixel division by multiply-shift");
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
-typedef short s2v_ __attribute__((ext_vector_type(2)));
-
-// two bf16 of a halo chunk (one dword) -> max(a * x + b, lo) in bf16, with one packed fp32 FMA, the hardware bf16
-// pack and a packed signed 16-bit max: every negative bf16 is a negative int16, so max with 0 is the exact ReLU and
-// max with 0x8000 (the int16 minimum) the identity
-CFL_DEVICE uint32_t xform2(uint32_t w, f32x2_t a, f32x2_t b, uint32_t lo) {
-  const f32x2_t x = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-  const f32x2_t y = __builtin_elementwise_fma(a, x, b);
-  const s2v_ r = __builtin_elementwise_max(__builtin_bit_cast(s2v_, __builtin_convertvector(y, bf16x2_t)),
-                                           __builtin_bit_cast(s2v_, lo));
-  return __builtin_bit_cast(uint32_t, r);
-}
-
 CFL_DEVICE s4v tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s4v_lds __attribute__((address_space(3)))*)(p));
 }
