@@ -195,18 +195,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
     bf16_t* st = hring + (ch % HSTAGES) * S::HST;
     // branch-free (divergent branches here made hipcc fall back to draining every DMA in flight): pieces past the
     // halo go to an unused pad row, out-of-image pieces keep their zero
+    // (packed BN-apply + ReLU, common.h xform8; the mask zeroes out-of-image pieces)
+    const uint32_t relu_lo = relu ? 0u : 0x80008000u;
 #pragma unroll
     for (int i = 0; i < H_PER_T; ++i) {
-      const bool ok = (hvalid >> i) & 1u;
-      float f[8];
-      unpack8(make_uint4(rh[i][0], rh[i][1], rh[i][2], rh[i][3]), f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float t = fmaf(ha[j], f[j], hb[j]);
-        const float r = relu ? fmaxf(t, 0.f) : t;
-        f[j] = ok ? r : 0.f;
-      }
-      sk_store16(st + sk_off(hrow[i], (tid + i * NT) & 3), pack8(f));
+      const uint32_t m = ((hvalid >> i) & 1u) ? 0xffffffffu : 0u;
+      sk_store16(st + sk_off(hrow[i], (tid + i * NT) & 3),
+                 xform8(make_uint4(rh[i][0], rh[i][1], rh[i][2], rh[i][3]), ha, hb, relu_lo, m));
     }
   };
 

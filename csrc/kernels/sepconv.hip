@@ -49,15 +49,16 @@ CFL_DEVICE void sep_fetch(const SepParams& p, const bf16_t* img, int x0, int row
   constexpr int PPT = (R * S::PIECES + NT - 1) / NT;
   const int tid = threadIdx.x, cq = tid % S::CQ;
   okm = 0;
+  // buffer loads from the image's resource, padding / rows past the segment at the out-of-range offset (read as 0):
+  // no per-lane branch around a load, no 64-bit address math
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img, (uint32_t)p.H * p.W * K * 2u);
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
     const int e = tid + i * NT;
     const int r = e / S::PIECES, px = (e - r * S::PIECES) / S::CQ;
     const int iy = row0 + r, ix = x0 - 1 + px;
     const bool ok = on && e < R * S::PIECES && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-    uint4 t = make_uint4(0, 0, 0, 0);
-    if (ok) t = *reinterpret_cast<const uint4*>(img + ((size_t)iy * p.W + ix) * K + cq * 8);
-    v[i] = t;
+    v[i] = buf_load16(rs, ok ? ((uint32_t)iy * p.W + ix) * (K * 2u) + cq * 16u : CFL_OOB, 0);
     okm |= (uint32_t)ok << i;
   }
 }
@@ -83,16 +84,7 @@ CFL_DEVICE void sep_put(bf16_t* ring, const uint4 (&v)[(R * Sep<K, N, TW>::PIECE
     if (e >= R * S::PIECES) continue;
     const int r = e / S::PIECES, px = (e - r * S::PIECES) / S::CQ;
     uint4 t = v[i];
-    if (xform && ((okm >> i) & 1u)) {
-      float f[8];
-      unpack8(t, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f[j] = fmaf(a8[j], f[j], b8[j]);
-        if (relu) f[j] = fmaxf(f[j], 0.f);
-      }
-      t = pack8(f);
-    }
+    if (xform) t = xform8(t, a8, b8, relu ? 0u : 0x80008000u, ((okm >> i) & 1u) ? 0xffffffffu : 0u);   // common.h
     const int slot = (row0 + r + S::NRING) % S::NRING;      // row0 >= -1
     *reinterpret_cast<uint4*>(ring + sep_off(slot * S::KS + (cq >> 2), S::HWp, px, cq & 3)) = t;
   }
@@ -304,6 +296,7 @@ int launch(const SepParams& p, hipStream_t st) {
 
 bool sep_fwd_supported(const SepParams& p) {
   if (cfl_tune(TUNE_SEP) == 1 || p.W % 32 || p.H < 1 || p.B < 1) return false;
+  if ((int64_t)p.H * p.W * p.K * 2 >= (1ll << 31)) return false;   // one image per buffer resource (sep_fetch)
   return (p.K == 32 && p.N == 64) || (p.K == 64 && (p.N == 64 || p.N == 128));
 }
 
