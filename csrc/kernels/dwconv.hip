@@ -242,14 +242,9 @@ CFL_DEVICE void fetch(const bf16_t* src_b, const DwParams& p, int x0, int row0, 
 
 CFL_DEVICE uint2 xform4(uint2 t, bool on, const float* a4, const float* b4, int relu) {
   if (!on) return t;                                         // padding stays zero (TF SAME pads the input)
-  float f[4];
-  unpack4(t, f);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f[j] = fmaf(a4[j], f[j], b4[j]);
-    if (relu) f[j] = fmaxf(f[j], 0.f);
-  }
-  return pack4(f);
+  const uint32_t lo = relu ? 0u : 0x80008000u;               // packed BN-apply + ReLU (common.h xform2)
+  return make_uint2(xform2(t.x, f32x2_t{a4[0], a4[1]}, f32x2_t{b4[0], b4[1]}, lo),
+                    xform2(t.y, f32x2_t{a4[2], a4[3]}, f32x2_t{b4[2], b4[3]}, lo));
 }
 
 template <int NR, bool SWZ>
