@@ -203,16 +203,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
       load_f8_or(p.xf.ab + c_ld, has_ab, 1.f, ca);
       load_f8_or(p.xf.ab + p.xf.C + c_ld, has_ab, 0.f, cb);
 #pragma unroll
-      for (int i = 0; i < A_PER_T; ++i) {
-        float f[8];
-        unpack8(ra[i], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f[j] = fmaf(ca[j], f[j], cb[j]);
-          if (relu) f[j] = fmaxf(f[j], 0.f);
-        }
-        ra[i] = ((avalid >> i) & 1u) ? pack8(f) : make_uint4(0, 0, 0, 0);   // padding stays exactly 0
-      }
+      for (int i = 0; i < A_PER_T; ++i)         // packed (common.h xform8); padding stays exactly 0
+        ra[i] = xform8(ra[i], ca, cb, relu ? 0u : 0x80008000u, ((avalid >> i) & 1u) ? 0xffffffffu : 0u);
     }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i)

@@ -176,20 +176,9 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
     for (int i = 0; i < XPT; ++i) {
       const int ch = tid + i * NT;
       if (ch < XC) {
-        uint4 v = rx[i];
-        if (!((xval >> i) & 1u)) {
-          v = make_uint4(0, 0, 0, 0);
-        } else if (has_ab || p.xf.relu) {
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            f[j] = fmaf(ca[j], f[j], cb[j]);
-            if (p.xf.relu) f[j] = fmaxf(f[j], 0.f);
-          }
-          v = pack8(f);
-        }
-        *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) = v;
+        // packed transform (common.h xform8), padding / rows past the block exactly 0
+        *reinterpret_cast<uint4*>(&sX[buf][ch / XW][(ch % XW) * 8]) =
+            xform8(rx[i], ca, cb, relu_lo, ((xval >> i) & 1u) ? 0xffffffffu : 0u);
       }
     }
 #pragma unroll
