@@ -519,8 +519,12 @@ static int launch_mix(const WgradParams* ps, int n, hipStream_t st) {
         zs = it.b;
       } else {
         int bko, bno, rm;
-        it.kind = (wgrad_direct(p) && cfl_tune(TUNE_WGRAD_DIRECT) != 1 ? 20 : 10) + wgrad_config(p, bko, bno, rm);
+        const int cfg = wgrad_config(p, bko, bno, rm);
         wgrad_shape(p, bko, bno, rm, it.a, zs);
+        // the direct body's per-step buffer ranges (a block's remaining rows x channels) must fit 31 bits
+        const bool direct = wgrad_direct(p) && cfl_tune(TUNE_WGRAD_DIRECT) != 1 &&
+                            (int64_t)it.a * (p.Cin > p.N ? p.Cin : p.N) * 2 < (1ll << 31);
+        it.kind = (direct ? 20 : 10) + cfg;
         it.b = 0;
         it.gx = p.K / bko;
         it.gy = p.N / bno;
