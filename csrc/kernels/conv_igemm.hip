@@ -60,23 +60,27 @@ CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv, const fl
       mx[j] = -INFINITY;
       am[j] = 0;
     }
+    // all nine window loads issued before any use, from clamped in-image addresses (a per-lane branch around each
+    // load - the clipped bottom / right edge - made every load wait for itself: nine latencies in a row)
+    uint4 wv[9];
+    bool wok[9];
+    const bf16_t* jy = J.y + (size_t)b * J.H * J.W * p.N + c;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int ih = 2 * oh + ky;
-      if (ih >= J.H) continue;
+    for (int k = 0; k < 9; ++k) {
+      const int ih = 2 * oh + k / 3, iw = 2 * ow + k % 3;
+      wok[k] = ih < J.H && iw < J.W;
+      wv[k] = *reinterpret_cast<const uint4*>(jy + ((size_t)imin(ih, J.H - 1) * J.W + imin(iw, J.W - 1)) * p.N);
+    }
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iw = 2 * ow + kx;
-        if (iw >= J.W) continue;
-        float f[8];
-        load8(J.y + ((size_t)(b * J.H + ih) * J.W + iw) * p.N + c, f);
+    for (int k = 0; k < 9; ++k) {
+      float f[8];
+      unpack8(wv[k], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = fmaf(a[j], f[j], bb[j]);
-          if (v > mx[j]) {
-            mx[j] = v;
-            am[j] = ky * 3 + kx;
-          }
+      for (int j = 0; j < 8; ++j) {
+        const float v = fmaf(a[j], f[j], bb[j]);
+        if (wok[k] && v > mx[j]) {
+          mx[j] = v;
+          am[j] = k;
         }
       }
     }
