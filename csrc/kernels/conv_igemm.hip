@@ -171,14 +171,14 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
     avalid = 0;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
+      // unconditional load from the clamped in-image pixel (padding / rows past M are masked in store_tiles): a
+      // per-lane branch around the load made it wait for itself right there
       const int ih = a_ih[i] + ky, iw = a_iw[i] + kx;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ih >= 0 && ih < Hl && iw >= 0 && iw < Wl) {
-        const size_t off = ((size_t)a_off[i] + (size_t)(ih >> p.up_in) * p.Win + (iw >> p.up_in)) * p.Cin + c;
-        v = *reinterpret_cast<const uint4*>(p.x + off);
-        avalid |= 1u << i;
-      }
-      ra[i] = v;
+      const bool ok = ih >= 0 && ih < Hl && iw >= 0 && iw < Wl;
+      const int ihc = imin(imax(ih, 0), Hl - 1), iwc = imin(imax(iw, 0), Wl - 1);
+      const size_t off = ((size_t)a_off[i] + (size_t)(ihc >> p.up_in) * p.Win + (iwc >> p.up_in)) * p.Cin + c;
+      ra[i] = *reinterpret_cast<const uint4*>(p.x + off);
+      avalid |= (ok ? 1u : 0u) << i;
     }
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
@@ -209,6 +209,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 #pragma unroll
       for (int i = 0; i < A_PER_T; ++i)         // packed (common.h xform8); padding stays exactly 0
         ra[i] = xform8(ra[i], ca, cb, relu ? 0u : 0x80008000u, ((avalid >> i) & 1u) ? 0xffffffffu : 0u);
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i)         // padding / rows past M: the clamped loads' data zeroed
+        if (!((avalid >> i) & 1u)) ra[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i)
