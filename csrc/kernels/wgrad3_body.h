@@ -11,14 +11,7 @@ constexpr int NT = 256;
 constexpr int CB = 32;            // input channels per block (the A-operand rows) of the default configs
 constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;
-// hp / HW for 0 <= hp < HP as (hp * HW_MAGIC) >> 16 (one full-rate 24-bit multiply)
-constexpr unsigned HW_MAGIC = (65536u + HW - 1) / HW;
-constexpr bool hw_magic_ok() {
-  for (int hp = 0; hp < HP; ++hp)
-    if ((int)((hp * HW_MAGIC) >> 16) != hp / HW) return false;
-  return true;
-}
-static_assert(hw_magic_ok(), "halo pixel division by multiply-shift");
+static_assert(div_small_ok<HW, HP>(), "halo pixel division by multiply-shift (common.h div_small)");
 
 typedef short s4v_lds __attribute__((ext_vector_type(4)));
 
@@ -118,7 +111,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
       const int hp = hp0 + i * (NT / QP);
       const bool in = (i + 1) * NT <= HALO_CH || hp < HP;
       const int hpc = (i + 1) * NT <= HALO_CH ? hp : imin(hp, HP - 1);
-      const int hy = (int)__umul24((unsigned)hpc, HW_MAGIC) >> 16, hx = hpc - hy * HW;
+      const int hy = div_small<HW>(hpc), hx = hpc - hy * HW;
       const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
       const bool ok = in && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
       const unsigned iyc = (unsigned)imin(imax(iy, 0), Hl - 1) >> p.up_in;
