@@ -108,15 +108,17 @@ def main() -> int:
                          f"ranks on one GPU; --dist-backend gloo rehearses N ranks on fewer)")
     torch.cuda.set_device(local % ndev)               # local % ndev: a gloo rehearsal may share one GPU
     dev = torch.device("cuda", local % ndev)
+    from crack_detection_federatedlearning_grpc_amd.parallel.rccl import group_stream_info, init_rccl_group
     if world == 1 and args.fedavg_1rank:
         import socket
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
             fport = so.getsockname()[1]
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{fport}", rank=0, world_size=1, device_id=dev)
+        init_rccl_group(dev, init_method=f"tcp://127.0.0.1:{fport}", rank=0, world_size=1)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # RCCL group owning its collective: high-priority stream, PreMulSum pre-scale, channel cap
+            init_rccl_group(dev)
         else:
             dist.init_process_group(args.dist_backend)
         print(f"[bench] rank {rank}/{world} local_rank {local} -> {dev} ({torch.cuda.get_device_name(dev)}, "
@@ -261,18 +263,18 @@ def main() -> int:
         timed = agg.timings[n_ar0:]
         agg.timings = timed
         fedavg_stats = agg.timing_summary()
-        # exposed FedAvg time per consumed all-reduce: from the compute stream's end of round r (the FedAvg issue
-        # event) to the first kernel of round r+1's encoder graph (the event after its bucket-0 wait) - pre-scale,
-        # host-side collective launches and any wait included - plus the stall before the rest of that step. The
-        # first timed step consumes the warm-up's all-reduce across the host barrier (not counted); the timed
-        # region's last all-reduce is waited by the closing synchronize.
+        # exposed FedAvg time per consumed all-reduce: how long round r+1's first step stalled on the compute stream
+        # for round r's buckets - its wait before the encoder graph (bucket 0) plus its wait before the rest of the
+        # step (every bucket). The first timed step consumes the warm-up's all-reduce across the host barrier (not
+        # counted); the timed region's last all-reduce is waited by the closing synchronize.
         st = eng.stall_log
         per = []
         for j in range(1, len(st) // 2):
             if j - 1 < len(timed):
-                pre_after = st[2 * j][1]
-                post_before, post_after = st[2 * j + 1]
-                per.append(timed[j - 1][0].elapsed_time(pre_after) + post_before.elapsed_time(post_after))
+                # the two stall brackets only (advisor r5: issue -> end of the first wait also counted the compute
+                # stream's own work queued between the FedAvg issue and that wait)
+                (b0, a0), (b1, a1) = st[2 * j], st[2 * j + 1]
+                per.append(b0.elapsed_time(a0) + b1.elapsed_time(a1))
         if per and fedavg_stats:
             exp = float(np.mean(per))
             fedavg_stats["allreduce_exposed_ms"] = exp
@@ -322,6 +324,7 @@ def main() -> int:
                "train_loss": round(m["loss"], 5), "train_accuracy": round(m["accuracy"], 5),
                "dist_backend": (dist.get_backend() if world > 1 else None),
                "deterministic": det, "conv_dtype": conv_dtype,
+               **({"rccl": group_stream_info()} if dist.is_initialized() and dist.get_backend() == "nccl" else {}),
                **({"fedavg_max_abs_err": fedavg_err} if fedavg_err is not None else {}),
                **fedavg_stats,
                "config": {"model": "Keras U-Net crack segmentation (client_fit_model.py:92-150, 2,058,145 params)",

@@ -52,7 +52,11 @@ class FLConfig:
                                          # communicator and falls back to the gRPC data plane
     dist_backend: str = "nccl"           # rccl data plane backend: nccl (= RCCL over xGMI) | gloo (CPU clients, or
                                          # a rehearsal of N clients sharing one GPU, which RCCL refuses)
-    async_upload: bool = True            # rccl data plane: after a successful collective the client starts the next
+    rccl_max_channels: int = -1          # RCCL channel cap (= workgroups an all-reduce occupies): -1 = env
+                                         # CFL_RCCL_MAX_CHANNELS or 16 (parallel/rccl.py), 0 = RCCL's own choice
+    dist_addr: str = "127.0.0.1"         # rendezvous address the server hands the clients in its READY reply (the
+                                         # rank-0 client's TCPStore host; 127.0.0.1 = every client on this node)
+    async_upload: bool = True           # rccl data plane: after a successful collective the client starts the next
                                          # round at once and reports TRAIN_DONE (rank 0: + the average) from a
                                          # background thread; its reply is checked before the next report
     codec: str = "flat"                  # client upload / advertised reply format: flat (safe) | pickle (reference

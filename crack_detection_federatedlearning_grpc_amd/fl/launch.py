@@ -26,15 +26,25 @@ def main(argv: Optional[List[str]] = None) -> int:
     cfg = _config.parse(argv)
     n = cfg.num_clients or 1
     cfg.num_clients = n
+    if cfg.data_plane == "rccl":
+        from ..parallel.rccl import rccl_placement_error
+        err = rccl_placement_error(n, cfg.device, cfg.dist_backend)
+        if err:
+            print(f"[launch] refused: {err}", file=sys.stderr, flush=True)
+            return 2
     from .server import FLServer
     srv = FLServer(cfg)
     port = srv.start()
     print(f"[launch] server on :{port}, starting {n} client process(es) (data plane {cfg.data_plane})", flush=True)
-    env = dict(os.environ)
     # the client processes share GPU memory over RCCL: the host driver only supports dmabuf IPC, and HSA reads
     # this at its initialisation, so each child gets it in its environment from the start (fl_client.py also
-    # sets it before its first GPU call)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # sets it before its first GPU call); plus the RCCL channel cap (parallel/rccl.py rccl_env)
+    if cfg.data_plane == "rccl":
+        from ..parallel.rccl import rccl_env
+        env = rccl_env(os.environ, cfg.rccl_max_channels)
+    else:
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     procs = []
     for r in range(n):

@@ -265,7 +265,7 @@ class FLServer(TransportServiceServicer):
             if self.cfg.data_plane == "rccl":
                 conf["world_size"] = self.state.wait_window_closed(timeout=self.cfg.register_window_s + 5)
                 conf["dist_port"] = self.dist_port
-                conf["dist_addr"] = "127.0.0.1"
+                conf["dist_addr"] = self.cfg.dist_addr
         return P.transportResponse(ready_rep=P.ReadyRep(config=_cfg(conf)))
 
     def _train_done(self, u, context):

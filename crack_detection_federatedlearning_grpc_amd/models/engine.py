@@ -123,6 +123,7 @@ class UNetEngine:
         self.eval_graph: Optional[torch.cuda.CUDAGraph] = None
         self._retired: List[torch.Tensor] = []   # replaced workspaces a captured graph may still reference
         self._evaluators: Dict[int, "UNetEngine"] = {}
+        self._eval_batch_memo: Dict[Tuple[int, int], int] = {}   # eval_batch_for's choices
         self.images: Optional[torch.Tensor] = None
         self.masks: Optional[torch.Tensor] = None
 
@@ -525,6 +526,14 @@ class UNetEngine:
             x = Lazy(A[f"e{k}_x"], None, 0, H // 2, F)
         if self._mid_hook is not None:                       # split-graph capture: the encoder graph ends here
             self._mid_hook()
+        if train and self._q8:
+            # fp8 mode: quantise the ConvT views of this step's weights HERE, in the decoder part of the step - after
+            # a FedAvg the encoder graph replays once only the encoder bucket landed, while the decoder buckets may
+            # still be reducing / repacking on the side stream; the post graph runs after every bucket, and an eager
+            # step waits for all of them first (the quantisation reads the whole packed buffer, not one layer)
+            if self._pending:
+                self._await_all()
+            self._quant_fp8()
         prev = x                                             # x3 at r[3]
         for k, F in enumerate(DEC_FILTERS):
             t1, b1, t2, b2, rc = (next(n) for _ in range(5))
@@ -809,8 +818,7 @@ class UNetEngine:
     def train_step_eager(self) -> None:
         self._check_det()
         self._zero_step()
-        self._quant_fp8()                    # fp8 mode: the ConvT views of this step's weights
-        self.forward(True)
+        self.forward(True)                   # (fp8 mode: quantises the ConvT views at the decoder's start)
         self.backward()
         self.optimizer_step(advanced=True)
 
@@ -992,7 +1000,15 @@ class UNetEngine:
         images, further bounded to a quarter of the device's free HBM at ~21.7 MB of forward activations per 256^2
         image (scaled by resolution) - several clients may share one device in a rehearsal. Round 4's 2048 cap (the
         bench's 1,776-image split in ONE launch) measured 12,754 / 12,688 img/s and 40.6 GB peak HBM per client
-        against 12,859 / 12,812 img/s and 15.5 GB for three 592-image launches (profiles/r5_evalcap, one box)."""
+        against 12,859 / 12,812 img/s and 15.5 GB for three 592-image launches (profiles/r5_evalcap, one box).
+
+        The choice is made ONCE per (n_images, cap) and remembered: free HBM shrinks once the first evaluator and its
+        graph exist, and re-deciding every pass would pick a smaller batch and build (and capture) another evaluator
+        each round (advisor r5)."""
+        key = (n_images, cap)
+        memo = self._eval_batch_memo
+        if key in memo:
+            return memo[key]
         if cap <= 0:
             cap = int(os.environ.get("CFL_EVAL_CAP", "1024"))
             if self.dev.type == "cuda":
@@ -1004,7 +1020,8 @@ class UNetEngine:
         for k in range(1, nb + 1):
             if nb % k == 0 and k * self.B <= cap:
                 best = k
-        return best * self.B
+        memo[key] = best * self.B
+        return memo[key]
 
     def predict_probs(self) -> torch.Tensor:
         """Sigmoid probabilities at full resolution for the current ``idx`` batch (eval-mode BN)."""

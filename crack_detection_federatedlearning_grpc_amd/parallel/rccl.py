@@ -15,6 +15,22 @@ against seconds of local training per round.
 ``RcclAggregator`` is the FL-client data plane (rendezvous parameters come from the server's READY reply);
 ``FedAvgAllReduce`` is the same reduction bound to an engine's device buffer (bench / in-process trainers).
 On CPU-only hosts the same code runs over gloo (tests).
+
+The RCCL group is built to OWN its collective (``init_rccl_group``):
+
+* the collectives run on c10d's per-device RCCL stream, created HIGH priority (``ProcessGroupNCCL.Options
+  .is_high_priority_stream``): under the next round's forward they get their own hardware queue ahead of the
+  compute queue instead of sharing its priority;
+* the FedAvg pre-scale n_k / sum n is fused into the reduction - ``ncclRedOpCreatePreMulSum`` with a DEVICE scalar
+  (``dist._make_nccl_premul_sum``): RCCL multiplies each rank's input by that rank's weight inside the all-reduce
+  kernel, so there is no per-bucket scaling kernel on the compute stream (gloo keeps the separate ``mul_``);
+* the channel count is capped (``ncclConfig_t.maxCTAs`` via ``Options.config.max_ctas``, and ``NCCL_MAX_NCHANNELS``
+  in the rank environment before the communicator exists): each RCCL channel is one resident workgroup, so the
+  cap bounds the CUs an in-flight all-reduce takes from the next round's kernels. Default 16
+  (``RCCL_MAX_CHANNELS_DEFAULT``; ``CFL_RCCL_MAX_CHANNELS`` / config ``rccl_max_channels``, 0 = RCCL's own choice):
+  an 8-GPU MI355X node is fully connected (7 xGMI links per GPU), so 16 rings still drive every link in both
+  directions while 240 of the 256 CUs keep computing; the 8.2 MB model moves in ~2 MB buckets, far below the
+  message size at which more channels pay.
 """
 from __future__ import annotations
 
@@ -26,6 +42,92 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+RCCL_MAX_CHANNELS_DEFAULT = 16
+
+
+def rccl_channel_cap(explicit: Optional[int] = None) -> int:
+    """The RCCL channel cap of this process: ``explicit`` (config ``rccl_max_channels``) if given, else
+    ``CFL_RCCL_MAX_CHANNELS``, else ``RCCL_MAX_CHANNELS_DEFAULT``; 0 = no cap."""
+    if explicit is not None and int(explicit) >= 0:
+        return int(explicit)
+    v = os.environ.get("CFL_RCCL_MAX_CHANNELS", "")
+    return int(v) if v.strip() else RCCL_MAX_CHANNELS_DEFAULT
+
+
+def rccl_env(env: Dict[str, str], cap: Optional[int] = None) -> Dict[str, str]:
+    """A rank's environment for RCCL (launchers set it before the child starts): dmabuf IPC (the host driver has no
+    legacy IPC) and the channel cap as ``NCCL_MAX_NCHANNELS`` unless the caller already chose one."""
+    env = dict(env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    c = rccl_channel_cap(cap)
+    if c > 0:
+        env.setdefault("NCCL_MAX_NCHANNELS", str(c))
+    return env
+
+
+def rccl_pg_options(cap: Optional[int] = None):
+    """``ProcessGroupNCCL.Options`` of the FedAvg group: high-priority collective stream + channel cap."""
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    c = rccl_channel_cap(cap)
+    if c > 0:
+        opts.config.max_ctas = c
+    return opts
+
+
+def init_rccl_group(device: torch.device, *, init_method: Optional[str] = None, rank: Optional[int] = None,
+                    world_size: Optional[int] = None, timeout: Optional[timedelta] = None,
+                    cap: Optional[int] = None) -> None:
+    """``dist.init_process_group("nccl")`` for one GPU client: eager communicator bound to ``device``, collectives
+    on a high-priority stream, channel cap in the options and (for the communicator's own env read) in
+    ``NCCL_MAX_NCHANNELS`` before RCCL initialises. ``init_method`` None = the env:// rendezvous (torchrun /
+    ``parallel/spawn.py``)."""
+    c = rccl_channel_cap(cap)
+    if c > 0:
+        os.environ.setdefault("NCCL_MAX_NCHANNELS", str(c))
+    kw = {}
+    if init_method is not None:
+        kw.update(init_method=init_method, rank=int(rank), world_size=int(world_size))
+    if timeout is not None:
+        kw["timeout"] = timeout
+    dist.init_process_group("nccl", pg_options=rccl_pg_options(c), device_id=device, **kw)
+
+
+def group_stream_info(group=None) -> Dict[str, object]:
+    """What the RCCL backend of ``group`` was built with (tests / bench JSON): high-priority stream, channel cap."""
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    be = pg._get_backend(torch.device("cuda"))
+    o = be.options
+    return {"high_priority_stream": bool(o.is_high_priority_stream), "max_ctas": int(o.config.max_ctas),
+            "nccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS")}
+
+
+def rccl_placement_error(n_ranks: int, device: str = "auto", backend: str = "nccl",
+                         rank: Optional[int] = None) -> Optional[str]:
+    """Why ``n_ranks`` RCCL clients (or client ``rank`` of them) cannot run here, or None. RCCL refuses two ranks
+    of one communicator on one GPU ("duplicate GPU"), but only at its first collective - after a whole round of
+    training - so the launchers check up front instead of mapping ``rank % device_count`` onto a shared card.
+    gloo (``backend``) and CPU clients are not constrained. ``torch.cuda.device_count()`` does not initialise HIP
+    on this image, so a launcher may call this before it starts its GPU children."""
+    if backend != "nccl" or device == "cpu":
+        return None
+    ndev = torch.cuda.device_count()
+    if ndev == 0 and device != "cuda":
+        return None                                   # auto on a CPU host: the clients fall back to gloo
+    need = n_ranks if rank is None else rank + 1
+    if need > ndev:
+        who = f"{n_ranks} RCCL clients need" if rank is None else f"RCCL client rank {rank} needs"
+        return (f"{who} {need} visible GPUs (one per client), found {ndev}: RCCL refuses two ranks on one GPU - "
+                f"use --dist-backend gloo to rehearse N clients on fewer GPUs")
+    return None
+
+
+def premul_enabled(group=None) -> bool:
+    """Fuse the FedAvg pre-scale into the all-reduce (PreMulSum with a device scalar): RCCL groups only;
+    ``CFL_RCCL_PREMUL=0`` restores the separate scaling kernel."""
+    return dist.get_backend(group) == "nccl" and os.environ.get("CFL_RCCL_PREMUL", "1") != "0"
 
 
 def _buckets(n: int, bucket_elems: int, first: int = 0) -> List[slice]:
@@ -47,6 +149,7 @@ class FedAvgAllReduce:
         self.world = world or dist.get_world_size(group)
         self.buckets = _buckets(flat.numel(), max(1024, int(bucket_mb * (1 << 20)) // 4), first_bucket)
         self._side = None
+        self.premul = premul_enabled(group)   # pre-scale fused into the all-reduce (RCCL PreMulSum)
         self.timing = False               # record hipEvents around each call's collectives (bench.py)
         self.timings: List[tuple] = []    # per call: (issue, last all-reduce done, last bucket repacked) events
 
@@ -66,13 +169,22 @@ class FedAvgAllReduce:
         dist.all_reduce(t, group=self.group)
         return float(t.item())
 
+    def _reduce_op(self, w):
+        """(op, scale-first) of one FedAvg call: RCCL -> PreMulSum with this rank's weight (a device tensor or a
+        float), fused into the all-reduce; otherwise SUM after a separate in-place scale."""
+        if self.premul:
+            return dist._make_nccl_premul_sum(w), False
+        return dist.ReduceOp.SUM, True
+
     def average(self, n_local: float, weighted: bool = True) -> None:
         w = self._weight(n_local, weighted)
+        op, scale = self._reduce_op(w)
         works = []
         for sl in self.buckets:
             b = self.flat[sl]
-            b.mul_(w)
-            works.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            if scale:
+                b.mul_(w)
+            works.append(dist.all_reduce(b, op=op, group=self.group, async_op=True))
         for wk in works:
             wk.wait()
 
@@ -101,10 +213,14 @@ class FedAvgAllReduce:
             self._side = torch.cuda.Stream(device=self.flat.device, priority=-1)
         out = []
         t_ar = None
+        op, scale = self._reduce_op(w)
         for i, sl in enumerate(self.buckets):
             b = self.flat[sl]
-            b.mul_(w)
-            work = dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if scale:
+                b.mul_(w)
+            # RCCL: enqueued on the group's high-priority stream behind the compute stream's work so far; with
+            # PreMulSum the kernel scales each rank's input by its weight on the fly (nothing on the compute stream)
+            work = dist.all_reduce(b, op=op, group=self.group, async_op=True)
             with torch.cuda.stream(self._side):
                 work.wait()                                   # side stream <- this bucket's collective
                 if self.timing and i == len(self.buckets) - 1:
@@ -144,7 +260,7 @@ class RcclAggregator:
     communicator first and the client can fall back to gRPC."""
 
     def __init__(self, rank: int, world: int, addr: str, port: int, device: Optional[torch.device] = None,
-                 timeout_s: float = 300.0, backend: Optional[str] = None):
+                 timeout_s: float = 300.0, backend: Optional[str] = None, max_channels: Optional[int] = None):
         self.rank, self.world = rank, world
         cuda = device is not None and device.type == "cuda"
         backend = backend or ("nccl" if cuda else "gloo")
@@ -155,9 +271,12 @@ class RcclAggregator:
             # gloo raises on its own timeout (the host waits in work.wait()); under RCCL the group timeout only
             # arms the watchdog, so it is set past the host-side deadline of wait_complete
             pg_timeout = self.timeout_s if backend == "gloo" else self.timeout_s + 60.0
-            dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world,
-                                    timeout=timedelta(seconds=pg_timeout),
-                                    **({"device_id": device} if backend == "nccl" else {}))
+            if backend == "nccl":
+                init_rccl_group(device, init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world,
+                                timeout=timedelta(seconds=pg_timeout), cap=max_channels)
+            else:
+                dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world,
+                                        timeout=timedelta(seconds=pg_timeout))
         self.device = device if cuda else torch.device("cpu")
         self._cached = None
         self._backup: Optional[torch.Tensor] = None
@@ -172,7 +291,8 @@ class RcclAggregator:
             dev = torch.device("cuda", torch.cuda.current_device())
         return cls(int(info.get("rank", 0)), int(info["world_size"]), str(info.get("dist_addr") or "127.0.0.1"),
                    int(info["dist_port"]), dev, timeout_s=float(getattr(cfg, "rccl_timeout_s", 300.0)),
-                   backend=getattr(cfg, "dist_backend", None) or None)
+                   backend=getattr(cfg, "dist_backend", None) or None,
+                   max_channels=getattr(cfg, "rccl_max_channels", None))
 
     def _reducer(self, flat: torch.Tensor, first_bucket: int = 0) -> FedAvgAllReduce:
         key = (flat.data_ptr(), flat.numel(), first_bucket)
@@ -394,6 +514,8 @@ class PendingFedAvg:
         out["allreduce_ms"] = float(t_issue.elapsed_time(t_ar))
         st = getattr(self.engine, "stall_log", None) if self.engine is not None else None
         if st and len(st) >= 2:
-            (_b0, a0), (b1, a1) = st[0], st[1]
-            out["allreduce_exposed_ms"] = float(t_issue.elapsed_time(a0) + b1.elapsed_time(a1))
+            # the compute stream's two stall brackets (before / after each wait on the buckets): only the time the
+            # next round's first step actually waited, not the work queued between the issue and the first wait
+            (b0, a0), (b1, a1) = st[0], st[1]
+            out["allreduce_exposed_ms"] = float(b0.elapsed_time(a0) + b1.elapsed_time(a1))
         return out

@@ -60,6 +60,13 @@ def spawn_local_ranks(script: str, argv: Sequence[str], nproc: int, *, timeout: 
     t0 = time.monotonic()
     rc = 0
     failed = None
+    completed = False                       # every rank exited 0: nothing to stop
+    prev_term = None
+
+    def _on_term(signum, _frame):           # a SIGTERM to the launcher stops the ranks through the finally below
+        raise SystemExit(128 + signum)
+    if threading.current_thread() is threading.main_thread():
+        prev_term = signal.signal(signal.SIGTERM, _on_term)
     try:
         while True:
             codes = [p.poll() for p in procs]
@@ -69,6 +76,7 @@ def spawn_local_ranks(script: str, argv: Sequence[str], nproc: int, *, timeout: 
                 rc = 1
                 break
             if all(c == 0 for c in codes):
+                completed = True
                 break
             if timeout is not None and time.monotonic() - t0 > timeout:
                 failed = (-1, "timeout")
@@ -76,7 +84,11 @@ def spawn_local_ranks(script: str, argv: Sequence[str], nproc: int, *, timeout: 
                 break
             time.sleep(poll_s)
     finally:
-        if rc != 0:
+        if prev_term is not None:
+            signal.signal(signal.SIGTERM, prev_term)
+        if not completed:
+            # a failed rank, the timeout, Ctrl-C or a SIGTERM / any exception in the loop above: the children run in
+            # their own sessions (no terminal signal reaches them), so stop every live rank's process group here
             for p in procs:
                 if p.poll() is None:
                     try:

@@ -94,6 +94,13 @@ def run(cfg=None):
     """fl_client.py:178-183."""
     cfg = cfg or _config.FLConfig()
     rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if cfg.data_plane == "rccl":
+        # one GPU per RCCL client: refused here, before any GPU call, instead of rank % device_count putting two
+        # ranks on one card (RCCL would fail only at the first collective, after a round of training)
+        from crack_detection_federatedlearning_grpc_amd.parallel.rccl import rccl_placement_error
+        err = rccl_placement_error(0, cfg.device, cfg.dist_backend, rank=rank)
+        if err:
+            raise SystemExit(f"fl_client: {err}")
     if cfg.device in ("cuda", "auto"):
         try:
             import torch

@@ -61,6 +61,8 @@ elif mode == "fail":
         sys.exit(3)
     time.sleep(600)
 else:
+    if os.environ.get("CHILD_PID_DIR"):
+        open(os.path.join(os.environ["CHILD_PID_DIR"], f"rank{r}.pid"), "w").write(str(os.getpid()))
     time.sleep(600)
 """
 
@@ -84,3 +86,33 @@ def test_spawn_local_ranks_env_relay_failure_and_timeout(tmp_path, capfd):
     assert spawn_local_ranks(str(script), ["hang"], 2, timeout=3) == 124
     assert time.monotonic() - t0 < 30
     assert "timed out" in capfd.readouterr().err
+
+
+def test_spawn_stops_ranks_when_the_launcher_is_terminated(tmp_path):
+    """The ranks run in their own sessions (no terminal signal reaches them): a SIGTERM to the launcher must still
+    stop every rank it started (advisor r5: only a failed rank / the timeout used to)."""
+    import signal
+    import time
+    script = tmp_path / "child.py"
+    script.write_text(_CHILD)
+    launcher = (f"import sys; sys.path.insert(0, {ROOT!r}); "
+                f"from crack_detection_federatedlearning_grpc_amd.parallel.spawn import spawn_local_ranks; "
+                f"sys.exit(spawn_local_ranks({str(script)!r}, ['hang'], 2))")
+    p = subprocess.Popen([sys.executable, "-c", launcher], env=dict(os.environ, CHILD_PID_DIR=str(tmp_path)))
+    pids = []
+    t0 = time.monotonic()
+    while len(pids) < 2 and time.monotonic() - t0 < 60:
+        time.sleep(0.1)
+        pids = [int(f.read_text()) for f in tmp_path.glob("rank*.pid") if f.read_text()]
+    assert len(pids) == 2, "ranks did not start"
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) != 0
+    for pid in pids:
+        t0 = time.monotonic()
+        while True:
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            assert time.monotonic() - t0 < 15, f"rank pid {pid} survived the launcher"
+            time.sleep(0.1)
