@@ -963,8 +963,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_LIST") = (int)TUNE_WGRAD_MIX_LIST;
   m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
   m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
-  m.attr("TUNE_WGRAD3_SK") = (int)TUNE_WGRAD3_SK;
-  m.attr("TUNE_WGRAD3_SK_MINTILES") = (int)TUNE_WGRAD3_SK_MINTILES;
   m.attr("TUNE_CONV3_F8") = (int)TUNE_CONV3_F8;
   m.attr("TUNE_DW_BWD_DMA") = (int)TUNE_DW_BWD_DMA;
   m.attr("TUNE_WGRAD3_WIDE") = (int)TUNE_WGRAD3_WIDE;

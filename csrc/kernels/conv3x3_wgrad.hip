@@ -20,7 +20,6 @@
 #include "launch.h"
 
 #include "wgrad3_body.h"
-#include "wgrad3_sk_body.h"
 
 namespace {
 
@@ -56,33 +55,14 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_group_kernel(const Wgrad3
   wgrad3_body<BNO, TR>(I.p, I.tiles, I.splits, bx, r % I.gy, r / I.gy, smem);
 }
 
-template <bool TR>
-__global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_sk_kernel(WgradParams p, int tiles_total, int splits) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[wg3s::LDS_BYTES];
-  wg3s::wgrad3sk_body<TR>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-}
-
 }  // namespace
-
-// the split-K-in-block body (wgrad3_sk_body.h) for this halo wgrad? TUNE_WGRAD3_SK: 0 / 1 = never (default), 2 =
-// every halo wgrad, 3 = maps <= 64^2 (the levels whose combo-split blocks walk 32 serial tiles).
-// Measured (profiles/r5_wgrad/wgrad_ab.txt, tools/mix_probe.py at 256^2 / b16): each <= 64^2 halo item alone 30-32 us
-// instead of 68-70, but the whole mixed launch 196.6 us (16 tiles per block), 208.1 (8), 185.2 (32) against 164.6 us
-// with the combo-split body: a block's 128-pixel tile step costs ~2 us either way (36 or 72 MFMAs per wave per
-// tile), so halving the block tile doubles the block-slot time the slot-bound mixed launch pays. Kept as an option.
-static bool wgrad3_sk_use(const WgradParams& p) {
-  const int v = cfl_tune(TUNE_WGRAD3_SK);
-  if (v <= 1) return false;
-  if (p.Cin % wg3s::CB || p.N % wg3s::NB) return false;
-  return v == 2 || p.Ho * p.Wo <= 64 * 64;
-}
 
 // input channels per block: 64 (wgrad3_body CBT = 64, one LDS buffer) for the large launches - a layer's dy is then
 // re-read Cin / 64 times instead of Cin / 32 and each staged tile feeds twice the MFMAs - else 32
 // (TUNE_WGRAD3_WIDE: 0 = auto, 1 = never, 2 = whenever Cin % 64 == 0)
 int conv3x3_wgrad_cbt(const WgradParams& p) {
   const int v = cfl_tune(TUNE_WGRAD3_WIDE);
-  if (v == 1 || p.Cin % 64 || wgrad3_sk_use(p)) return CB;
+  if (v == 1 || p.Cin % 64) return CB;
   if (v == 2) return 64;
   const int64_t tiles = (int64_t)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   return tiles * (p.Cin / CB) >= 65536 ? 64 : CB;
@@ -99,15 +79,6 @@ bool conv3x3_wgrad_supported(const WgradParams& p) {
 
 void conv3x3_wgrad_shape(const WgradParams& p, int& bno, int& tiles, int& splits) {
   tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
-  if (wgrad3_sk_use(p)) {
-    // split-K-in-block body: 32 x 32 x 9-tap block tiles; pixel splits for ~16 tiles per block (each split is one
-    // plain-stored slab row that grad_finish reads)
-    bno = wg3s::NB;
-    const int mt = cfl_tune(TUNE_WGRAD3_SK_MINTILES) > 0 ? cfl_tune(TUNE_WGRAD3_SK_MINTILES) : 16;
-    splits = (tiles + mt - 1) / mt;
-    if (splits < 1) splits = 1;
-    return;
-  }
   bno = p.N % 64 == 0 ? 64 : 32;
   const int xy = (p.Cin / conv3x3_wgrad_cbt(p)) * (p.N / bno);
   const int target = cfl_tune(TUNE_WGRAD3_BLOCKS) > 0 ? cfl_tune(TUNE_WGRAD3_BLOCKS) : 512;
@@ -134,10 +105,9 @@ int conv3x3_wgrad_splits(const WgradParams& p) {
   return splits;
 }
 
-// tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>; split-K-in-block
-// body: 4 = TR, 5 = HWIO; 64-channel blocks: 6 = <64,TR>, 7 = <64,HWIO>, 8 = <32,TR>, 9 = <32,HWIO>
+// tile config of a (supported) 3x3 wgrad: 0 = <64,TR>, 1 = <64,HWIO>, 2 = <32,TR>, 3 = <32,HWIO>; 64-channel
+// blocks: 6 = <64,TR>, 7 = <64,HWIO>, 8 = <32,TR>, 9 = <32,HWIO> (4, 5: retired split-K-in-block body, round 6)
 int conv3x3_wgrad_config(const WgradParams& p) {
-  if (wgrad3_sk_use(p)) return p.dst_mode == 1 ? 4 : 5;
   int bno, tiles, splits;
   conv3x3_wgrad_shape(p, bno, tiles, splits);
   return (conv3x3_wgrad_cbt(p) == 64 ? 6 : 0) + (bno == 64 ? 0 : 2) + (p.dst_mode == 1 ? 0 : 1);
@@ -157,7 +127,7 @@ int conv3x3_wgrad_grouped(const WgradParams* ps, int n, hipStream_t st) {
       conv3x3_wgrad_shape(p, bno, tiles, splits);
       if (p.slabs > 0 && p.slabs != splits) return 2;
       const int c = conv3x3_wgrad_config(p);
-      if (c >= 4) {                                   // split-K-in-block / 64-channel bodies: launched on their own
+      if (c >= 4) {                                   // 64-channel bodies: launched on their own
         const int rc = conv3x3_wgrad(p, st);
         if (rc) return rc;
         continue;
@@ -192,11 +162,6 @@ int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {
   if (p.slabs > 0 && p.slabs != splits) return 2;
   dim3 grid(p.Cin / conv3x3_wgrad_cbt(p), p.N / bno, splits);
   const bool tr = p.dst_mode == 1;
-  if (wgrad3_sk_use(p)) {
-    if (tr) hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<true>), grid, dim3(NT), 0, st, p, tiles, splits);
-    else hipLaunchKernelGGL((conv3x3_wgrad_sk_kernel<false>), grid, dim3(NT), 0, st, p, tiles, splits);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-  }
   if (conv3x3_wgrad_cbt(p) == 64) {
     if (bno == 64 && tr)
       hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, true, 64, true>), grid, dim3(NT), 0, st, p, tiles, splits);

@@ -16,7 +16,6 @@
 #include "common.h"
 #include "launch.h"
 #include "wgrad3_body.h"
-#include "wgrad3_sk_body.h"
 
 namespace {
 
@@ -372,7 +371,7 @@ int launch_group(const WgradParams* ps, int n, hipStream_t st) {
 // latency-bound grid that leaves the chip part-idle in its tail; in one grid the blocks of all of them co-run and
 // the four launch boundaries between the groups are gone. One LDS buffer sized for the largest body (the 64-wide
 // halo config, 75.5 KB: 2 blocks per CU, as the halo groups had); the kernel's VGPR count is the largest body's.
-// kind: 0-9 halo config (conv3x3_wgrad_config; 4, 5 = the split-K-in-block body, 6-9 the 64-channel blocks), 10 + c
+// kind: 0-9 halo config (conv3x3_wgrad_config; 6-9 the 64-channel blocks), 10 + c
 // generic config c (wgrad_config; 20 + c: its DIRECT form, wgrad_body; c = 1, the 80 KB
 // 128-pixel-stage variant, is launched on its own)
 constexpr int MIX_MAX = 24;
@@ -388,8 +387,8 @@ struct MixGroup {
   int xcd;                  // XCD-grouped block order (TUNE_WGRAD_MIX_XCD != 1)
 };
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int MIX_LDS = cmax(cmax(cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wg3::wgrad3_lds_bytes<64, 64, true>()),
-                                            wg3s::LDS_BYTES), wgrad_lds_bytes<128, 128, 32>()),
+constexpr int MIX_LDS = cmax(cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wg3::wgrad3_lds_bytes<64, 64, true>()),
+                                       wgrad_lds_bytes<128, 128, 32>()),
                                   wgrad_lds_bytes<128, 128, 64>()),
                              cmax(cmax(wgrad_lds_bytes<64, 32, 128>(), wgrad_lds_bytes<32, 64, 128>()),
                                   cmax(wgrad_lds_bytes<32, 32, 128>(), wgrad_lds_bytes<64, 64, 64>())));
@@ -415,8 +414,6 @@ __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
     case 1: wg3::wgrad3_body<64, false>(P, a, b, bx, by, bz, smem); break;
     case 2: wg3::wgrad3_body<32, true>(P, a, b, bx, by, bz, smem); break;
     case 3: wg3::wgrad3_body<32, false>(P, a, b, bx, by, bz, smem); break;
-    case 4: wg3s::wgrad3sk_body<true>(P, a, b, bx, by, bz, smem); break;
-    case 5: wg3s::wgrad3sk_body<false>(P, a, b, bx, by, bz, smem); break;
     case 6: wg3::wgrad3_body<64, true, 64, true>(P, a, b, bx, by, bz, smem); break;
     case 7: wg3::wgrad3_body<64, false, 64, true>(P, a, b, bx, by, bz, smem); break;
     case 8: wg3::wgrad3_body<32, true, 64, true>(P, a, b, bx, by, bz, smem); break;

@@ -518,12 +518,10 @@ enum TuneKey {
   TUNE_WGRAD_MIX_SKIP = 43,    // TIMING ONLY: mixed wgrad launch drops the items of this bit mask (bit k = item k)
   TUNE_WGRAD_MIX_LIST = 44,    // 1: print the mixed launch's items (index, kind, shape, blocks) to stderr once
   TUNE_WGRAD_MIX_ORDER = 45,   // mixed wgrad launch item order: 0 = default (2), 1 = generic first, 2 = alternating,
-                               //   3 = halo items first
+                               //   3 = halo items first (round 6: longest-block-first orders measured +4 / +8.5 us)
   TUNE_OPT_SCALAR = 46,        // opt_step: 1 = per-column tile form for every tile (default: 16-byte form where aligned)
   // 47: retired (opt_step timing knob without its ticket; the training step no longer uses the ticket)
-  TUNE_WGRAD3_SK = 48,         // halo wgrad split-K-in-block body (wgrad3_sk_body.h): 0 / 1 = off (default; measured
-                               //   slower in the mixed launch), 2 = every halo wgrad, 3 = maps <= 64^2
-  TUNE_WGRAD3_SK_MINTILES = 49, // ... min 128-pixel tiles per block (default 16)
+  // 48, 49: retired (split-K-in-block halo wgrad body: slower in the slot-bound mixed launch, deleted in round 6)
   TUNE_CONV3_F8 = 50,          // fp8 3x3 routing: 0 = default (fp8 for the node-join dgrads the weight-stationary bf16
                                //   kernel does not take), 1 = never, 2 = every call carrying fp8 operands, 3 = every
                                //   call the weight-stationary kernel does not take

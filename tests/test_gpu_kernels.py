@@ -776,10 +776,11 @@ def test_wgrad3_wide_channel_blocks(B, Hs, Cin, N, up, use_ab, dst_mode):
     (3, 6, 32, 64, 1, True, 1),      # ragged 12x12 output
     (2, 20, 96, 96, 0, False, 0),    # Keras HWIO layout, ragged rows and columns, 3 channel chunks
 ])
-def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
-    """The split-K-in-block halo weight gradient (wgrad3_sk_body.h, TUNE_WGRAD3_SK = 2) against the combo-split
-    body (TUNE_WGRAD3_SK = 1) and fp32 autograd; its slab rows (one per pixel split, plain stores) summed by
-    grad_finish equal the direct (atomic) result, and in the deterministic mode two runs are bit-identical."""
+def test_wgrad3_halo_body_slabs_and_det(B, Hs, Cin, N, up, use_ab, dst_mode):
+    """The halo weight gradient (wgrad3_body.h) at the decoder's low-resolution shapes against fp32 autograd; its
+    slab rows (one per pixel split, plain stores) summed by grad_finish equal the direct (atomic) result, and in the
+    deterministic mode two runs are bit-identical. (Round 6: the split-K-in-block variant this test also covered was
+    deleted - slower in the slot-bound mixed launch.)"""
     torch.manual_seed(29)
     C_ = hip()
     Ho = Hs * (2 if up else 1)
@@ -790,25 +791,17 @@ def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
     K = 9 * Cin
     outs = {}
     try:
-        for sk in (1, 2):
-            C_.set_tune(C_.TUNE_WGRAD3_SK, sk)
-            dw = torch.zeros(K * N, device=DEV)
-            C_.conv_wgrad(xb, dyb, dw, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0)
-            outs[sk] = dw.cpu()
-        assert rel(outs[2], outs[1]) < 2e-3
-        # slab rows of the sk body (TUNE_WGRAD3_SK_MINTILES = 1: one pixel tile per split, the most rows)
-        C_.set_tune(C_.TUNE_WGRAD3_SK, 2)
-        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 1)
+        dw = torch.zeros(K * N, device=DEV)
+        C_.conv_wgrad(xb, dyb, dw, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0)
+        outs[2] = dw.cpu()
         rows, plain = C_.conv_wgrad_slabs(B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1)
-        assert plain and rows == B * ((Ho + 7) // 8) * ((Ho + 15) // 16)
+        assert plain and rows >= 1
         slab = torch.full((rows * K * N,), float("nan"), device=DEV)       # plain rows overwrite all
         C_.conv_wgrad(xb, dyb, slab, abd, 1, B, Hs, Hs, Cin, up, Ho, Ho, N, 3, 1, 1, 1, dst_mode, 0, 0, rows)
         dst = torch.zeros(K * N, device=DEV)
         table, work = C_.make_grad_finish_table([(slab, dst, K * N, rows, C_.GF_SUM)])
         C_.grad_finish(table, 1, work)
         assert rel(dst.cpu(), outs[2]) < 1e-5
-        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 0)
-        C_.set_tune(C_.TUNE_WGRAD3_SK, 2)
         # deterministic mode: int64 fixed-point atomics, bitwise reproducible
         C_.set_det(1)
         det = []
@@ -820,8 +813,6 @@ def test_wgrad3_split_k_in_block_body(B, Hs, Cin, N, up, use_ab, dst_mode):
         assert rel(det[0].double() / 2.0 ** 40, outs[2].double()) < 1e-5
     finally:
         C_.set_det(0)
-        C_.set_tune(C_.TUNE_WGRAD3_SK, 0)
-        C_.set_tune(C_.TUNE_WGRAD3_SK_MINTILES, 0)
     t = (xf * a + b) if use_ab else xf
     xin = t.relu().to(torch.bfloat16).float().permute(0, 3, 1, 2)
     if up:

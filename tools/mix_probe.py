@@ -6,7 +6,7 @@ restricted launches leave the other items' slabs stale.
     python tools/mix_probe.py [img] [batch]
 
 Env: CFL_MIX_TUNE="KEY=V,..." sets launch knobs (launch.h TuneKey names without TUNE_) before the engine is built (e.g.
-WGRAD3_SK=1 for the combo-split halo body); MIX_ORDER_ONLY=1 stops after the whole-launch timings; MIX_ALONE_ONLY=1
+WGRAD3_WIDE=2 for the 64-channel halo blocks); MIX_ORDER_ONLY=1 stops after the whole-launch timings; MIX_ALONE_ONLY=1
 times each item alone but skips the "mix without it" runs.
 """
 import os
