@@ -939,6 +939,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("batches") = py::none(), py::arg("cursor") = py::none(), py::arg("idx") = py::none(),
         py::arg("step") = py::none(), py::arg("lr_buf") = py::none(), py::arg("lr") = 0.0, py::arg("b1") = 0.0,
         py::arg("b2") = 0.0);
+  m.def("set_ts", [](py::object buf) {
+    if (buf.is_none()) {
+      ok(cfl_ts_set(nullptr, 0), "set_ts");
+      return;
+    }
+    torch::Tensor t = buf.cast<torch::Tensor>();
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kInt64 && t.is_contiguous() && t.numel() % 2 == 0,
+                "set_ts: contiguous int64 device tensor of [blocks][2]");
+    ok(cfl_ts_set(t.data_ptr(), (int)(t.numel() / 2)), "set_ts");
+  }, "block timeline buffer ([blocks][2] int64 s_memrealtime stamps per kernel launch) or None = off");
   m.def("set_tune", &cfl_set_tune);
   m.def("get_tune", &cfl_tune);
   m.attr("GF_REDUCE") = (int)GF_REDUCE;

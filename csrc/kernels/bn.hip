@@ -57,6 +57,7 @@ __device__ __forceinline__ void replica_sums(const float* stats, int C, float (*
 __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, const float* gamma, const float* beta,
                                                          const float* mmean, const float* mvar, float* ab, int C,
                                                          float count, float eps, int train) {
+  CFL_TS_GUARD;
   // one thread per channel, all of its 2 * STAT_REPLICAS loads in one round (bn_coef_from_stats: the same
   // arithmetic as the consumer-side finalize)
   const int c = threadIdx.x;
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(FT) void bn_finalize_kernel(const float* stats, con
 }
 
 __global__ __launch_bounds__(256) void bn_eval_kernel(const BnEval* layers) {
+  CFL_TS_GUARD;
   const BnEval L = layers[blockIdx.x];
   for (int c = threadIdx.x; c < L.C; c += blockDim.x) {
     const float rstd = rsqrtf(L.mvar[c] + L.eps);
@@ -89,6 +91,7 @@ __global__ __launch_bounds__(256) void bn_eval_kernel(const BnEval* layers) {
 }
 
 __global__ __launch_bounds__(FT) void bn_moving_kernel(const BnMoving* layers, float momentum) {
+  CFL_TS_GUARD;
   __shared__ float part[2][FT];
   const BnMoving L = layers[blockIdx.x];
   float s, s2;
@@ -174,6 +177,7 @@ CFL_DEVICE void node_gather(const NodeBwdParams& p, int b, int h, int w, int c0,
 // must be in flight together
 template <int M0, int M1, int IPT>
 __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
+  CFL_TS_GUARD;
   __shared__ float red[2][4][256];
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
@@ -237,10 +241,12 @@ __global__ __launch_bounds__(NT) void node_bwd_kernel(NodeBwdParams p) {
 
 template <int IPT>
 __global__ __launch_bounds__(NT) void node_pool_bwd_kernel(NodeBwdParams p) {
+  CFL_TS_GUARD;
   side::node_pool_body<IPT>(p, blockIdx.x, gridDim.x);
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdApplyParams p) {
+  CFL_TS_GUARD;
   side::bba_body(p, blockIdx.x, gridDim.x);
 }
 
@@ -340,3 +346,5 @@ int bn_bwd_apply(const BnBwdApplyParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_bn(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_bn(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

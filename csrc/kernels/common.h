@@ -216,6 +216,37 @@ static inline int cfl_det_upload(int v) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_det), &v, sizeof(int)) == hipSuccess ? 0 : 3;
 }
 
+// Block timeline instrumentation (tools/block_timeline.py): with a buffer installed (cfl_ts_set, launch.h), every
+// instrumented kernel's blocks record [dispatch, retire] s_memrealtime stamps (100 MHz, chip-wide) at
+// buf[2 * linear block id]; off (null buffer) it costs one constant load and a branch per block.
+struct CflTs {
+  unsigned long long* buf;
+  int cap;                 // blocks
+};
+namespace {
+__constant__ CflTs g_cfl_ts;
+}
+CFL_DEVICE unsigned long long cfl_ts_now() { return __builtin_amdgcn_s_memrealtime(); }
+// RAII: the retire stamp is taken when thread 0 leaves the kernel by any path (no barrier: an early return of part of
+// a block must not deadlock); wave 0's exit stands for the block's
+struct CflTsGuard {
+  unsigned long long t0;
+  __device__ CflTsGuard() : t0(cfl_ts_now()) {}
+  __device__ ~CflTsGuard() {
+    if (g_cfl_ts.buf == nullptr || threadIdx.x != 0) return;
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (b < g_cfl_ts.cap) {
+      g_cfl_ts.buf[2 * b] = t0;
+      g_cfl_ts.buf[2 * b + 1] = cfl_ts_now();
+    }
+  }
+};
+#define CFL_TS_GUARD CflTsGuard cfl_ts_guard_
+static inline int cfl_ts_upload(void* buf, int cap) {
+  const CflTs t{reinterpret_cast<unsigned long long*>(buf), cap};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_ts), &t, sizeof(t)) == hipSuccess ? 0 : 3;
+}
+
 // log2 of a power of two (host or device)
 __host__ __device__ inline int ilog2(int x) {
   int l = 0;

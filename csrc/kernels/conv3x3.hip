@@ -40,6 +40,7 @@ __device__ __forceinline__ int swz_off(int r, int q) { return r * BK + ((q ^ ((r
 // rows for the layer's later consumers.
 template <int TH, int TW, int BN_, int WM, int WN, bool WB, bool PJ = false, bool XFIN = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks_per_split, float* __restrict__ ws) {
+  CFL_TS_GUARD;
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;          // halo pixels
   // LDS pitch of a halo line: TW + 2, except 16 for the 8-wide tiles - there a 16-row A fragment spans two pixel rows,
@@ -450,6 +451,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
 // LDS: weights CH*9*32 rows + halo CH*HP rows (64 B each, swizzled as above) + a bf16 C staging tile.
 template <int TH, int TW, int CH, bool PJ = false, bool XFIN = false>
 __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(ConvParams p, int n_items) {
+  CFL_TS_GUARD;
   constexpr int BN_ = 32, WM = 4;
   constexpr int BM = TH * TW;
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
@@ -910,3 +912,5 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv3x3(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv3x3(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -47,6 +47,7 @@ constexpr int MAX_CIN = 512;              // producer BN coefficients staged in 
 
 template <int TH, int TW, int WM, int WN>
 __global__ __launch_bounds__(NT, 2) void conv3x3_deep_kernel(ConvParams p) {
+  CFL_TS_GUARD;
   constexpr int BM = TH * TW;
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
   constexpr int TM = BM / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
@@ -290,3 +291,5 @@ int conv3x3_deep(const ConvParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv3x3_deep(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv3x3_deep(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

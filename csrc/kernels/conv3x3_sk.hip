@@ -85,6 +85,7 @@ struct SkCfg {
 
 template <int TH, int TW, int BN, int NCH, bool PJ, bool XFIN>
 __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
+  CFL_TS_GUARD;
   using S = SkCfg<TH, TW, BN>;
   constexpr int BM = S::BM, HWL = S::HWL, HWR = S::HWR, FM = S::FM, FN = S::FN;
   constexpr int W_PER = S::W_PER, W_REM = S::W_REM, H_PER_T = S::H_PER_T, HPIECES = S::HPIECES;
@@ -512,3 +513,5 @@ int conv3x3_sk(const ConvParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv3x3_sk(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv3x3_sk(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

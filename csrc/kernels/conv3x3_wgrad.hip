@@ -27,6 +27,7 @@ using namespace wg3;
 
 template <int BNO, bool TR, int CBT = CB, bool SB = false>
 __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_kernel(WgradParams p, int tiles_total, int splits) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad3_lds_bytes<BNO, CBT, SB>()];
   wgrad3_body<BNO, TR, CBT, SB>(p, tiles_total, splits, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
@@ -46,6 +47,7 @@ struct Wgrad3Group {
 
 template <int BNO, bool TR>
 __global__ __launch_bounds__(NT, 2) void conv3x3_wgrad_group_kernel(const Wgrad3Group g) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad3_lds_bytes<BNO>()];
   int k = 0;
   while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
@@ -182,3 +184,5 @@ int conv3x3_wgrad(const WgradParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv3x3_wgrad(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv3x3_wgrad(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -110,6 +110,7 @@ CFL_DEVICE void join_store(const ConvParams& p, int m, int c, uint4 rv, const fl
 
 template <int BM_, int BN_, int WM, int WN, bool JN = false>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_per_split, float* __restrict__ ws) {
+  CFL_TS_GUARD;
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM_ / WM, TN = BN_ / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -370,6 +371,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
 
 // sum split-K partials + bias -> bf16, with the BN statistics epilogue
 __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const float* __restrict__ ws, int splits) {
+  CFL_TS_GUARD;
   __shared__ float red[2][NT / 64][256];
   const int G = p.N >> 3, lanes = NT / G;
   const int cg = threadIdx.x % G, c0 = cg * 8;
@@ -575,3 +577,5 @@ int conv_igemm(const ConvParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv_igemm(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv_igemm(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -258,6 +258,7 @@ CFL_DEVICE void wgrad_body(const WgradParams& p, int chunk, int bx, int by, int 
 
 template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradParams p, int chunk) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad_lds_bytes<BKO, BNO, RM>()];
   wgrad_body<BKO, BNO, RM>(p, chunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
@@ -307,6 +308,7 @@ struct WgradGroup {
 
 template <int BKO, int BNO, int RM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_group_kernel(const WgradGroup g) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) unsigned char smem[wgrad_lds_bytes<BKO, BNO, RM>()];
   int k = 0;
   while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
@@ -395,6 +397,7 @@ constexpr int MIX_LDS = cmax(cmax(cmax(cmax(wg3::wgrad3_lds_bytes<64>(), wg3::wg
 static_assert(MIX_LDS <= 80 * 1024, "two mixed blocks per CU");
 
 __global__ __launch_bounds__(NT, 2) void wgrad_mix_kernel(const MixGroup g) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) unsigned char smem[MIX_LDS];
   // XCD grouping: within every 64 dispatch slots, each XCD runs 8 consecutive logical blocks - the (up to 8) input-
   // channel blocks of one pixel split, which read the same dy tile, share an XCD's L2 and run at the same time (round-
@@ -621,3 +624,5 @@ int conv_wgrad(const WgradParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_conv_wgrad(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_conv_wgrad(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

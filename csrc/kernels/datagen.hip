@@ -15,6 +15,7 @@ CFL_DEVICE uint32_t hash3(uint32_t x, uint32_t y, uint32_t seed) {
 
 __global__ void render_kernel(const float* segs, const float* params, uint8_t* images, uint8_t* masks, int img,
                               int max_seg) {
+  CFL_TS_GUARD;
   const int n = blockIdx.y;
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   const int y = blockIdx.z;
@@ -74,6 +75,7 @@ namespace {
 __global__ void resize_batch_kernel(const uint8_t* __restrict__ src, const int64_t* __restrict__ offs,
                                     const int* __restrict__ dims, uint8_t* __restrict__ dst, int dh, int dw, int c,
                                     int binarize) {
+  CFL_TS_GUARD;
   const int img = blockIdx.y;
   const int pix = blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= dh * dw) return;
@@ -118,3 +120,5 @@ int resize_batch(const uint8_t* src, const int64_t* offs, const int* dims, uint8
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_datagen(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_datagen(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -46,6 +46,7 @@ template <int SW>
 __global__ __launch_bounds__(NT) void dw_conv_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
                                                      bf16_t* __restrict__ y, InXform xf, int B, int H, int W, int C,
                                                      int flip) {
+  CFL_TS_GUARD;
   const int G = C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
   const bool has_ab = xf.ab != nullptr;
@@ -92,6 +93,7 @@ __global__ __launch_bounds__(NT) void dw_conv_kernel(const bf16_t* __restrict__ 
 
 template <int SW>
 __global__ __launch_bounds__(NT) void dw_wgrad_kernel(DwParams p, int replicas) {
+  CFL_TS_GUARD;
   __shared__ float red[4][9][256];
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
@@ -506,6 +508,7 @@ CFL_DEVICE void dw_stream_body(const DwParams& p, int replicas, int seg_rows, in
 
 template <int MODE>
 __global__ __launch_bounds__(NT, 3) void dw_stream_kernel(DwParams p, int replicas, int seg_rows) {
+  CFL_TS_GUARD;
   dw_stream_body<MODE>(p, replicas, seg_rows, blockIdx.x, gridDim.x);
 }
 
@@ -522,6 +525,7 @@ struct DwGroup {
 };
 
 __global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) {
+  CFL_TS_GUARD;
   int k = 0;
   while (k + 1 < g.n && g.it[k + 1].block0 <= (int)blockIdx.x) ++k;
   const DwItem& I = g.it[k];
@@ -542,6 +546,7 @@ __global__ __launch_bounds__(NT, 3) void dw_wgrad_group_kernel(const DwGroup g) 
 // L2 hits).
 template <bool NODE>
 __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int replicas, int seg_rows) {
+  CFL_TS_GUARD;
   using namespace dws;
   constexpr int LDP = ldp<false>();
   __shared__ __attribute__((aligned(16))) bf16_t sG[NRING * HWp * LDP];   // dy rows
@@ -891,6 +896,7 @@ CFL_DEVICE void putx(unsigned char* ring, const u2v (&v)[NR + 1], uint32_t okm, 
 
 template <bool NODE>
 __global__ __launch_bounds__(NT, 3) void dw_bwd_dma_kernel(DwParams p, int replicas, int seg_rows) {
+  CFL_TS_GUARD;
   using namespace dws;
   using dwd::NRG;
   using dwd::NRX;
@@ -1325,3 +1331,5 @@ int dw_wgrad(const DwParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_dwconv(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_dwconv(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -28,6 +28,7 @@ CFL_DEVICE void stage_rows(const uint8_t* img, int S, int ih0, int nr, float* sr
 }
 
 __global__ __launch_bounds__(NT) void entry_fwd_kernel(EntryParams p) {
+  CFL_TS_GUARD;
   extern __shared__ float srow[];            // [3][S*3] normalised input rows of this output row
   __shared__ float sw[27 * 64];
   __shared__ float red[2][4][256];
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(NT) void entry_fwd_kernel(EntryParams p) {
 // dW[ky][kx][ci][co] = sum_pix x[2oh+ky][2ow+kx][ci] * dy[pix][co]; blockIdx.y = ky, thread = (pixel, 8 outputs).
 // The input row is staged in LDS once per output row; per-block sums go to one of `replicas` copies of dW.
 __global__ __launch_bounds__(NT) void entry_wgrad_kernel(EntryParams p, int replicas) {
+  CFL_TS_GUARD;
   extern __shared__ float srow[];            // [S*3] normalised input row 2*oh + ky
   __shared__ float red[4][9][64];
   const int G = p.Cout >> 3, lg = ilog2(G);
@@ -204,6 +206,7 @@ CFL_DEVICE s8v bytes_frag(const uint8_t* sR, const int (&off)[8], const int (&st
 }
 
 __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int nch, int steps) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sY[ECH][ELD];
   __shared__ float red[2][4][256];
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(NT) void entry_fwd_mfma_kernel(EntryParams p, int n
 // thread's 8 channels' coefficients held in registers; block 0 writes dgamma / dbeta. dx itself is never stored.
 template <bool BWD>
 __global__ __launch_bounds__(NT) void entry_wgrad_mfma_kernel(EntryParams p, int nch, int steps, int replicas) {
+  CFL_TS_GUARD;
   __shared__ __attribute__((aligned(16))) uint8_t sR[2][3 * ERB];
   __shared__ __attribute__((aligned(16))) bf16_t sG[2][ECH][ELD];
   __shared__ float red[4][32 * 32];
@@ -462,3 +466,5 @@ int entry_wgrad(const EntryParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_entry(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_entry(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

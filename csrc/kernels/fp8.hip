@@ -37,6 +37,7 @@ typedef int i8v __attribute__((ext_vector_type(8)));
 __global__ __launch_bounds__(64) void mfma_scale_probe_kernel(const int* __restrict__ a, const int* __restrict__ b,
                                                               const int* __restrict__ sa, const int* __restrict__ sb,
                                                               float* __restrict__ d, int shape) {
+  CFL_TS_GUARD;
   const int l = threadIdx.x;
   i8v av, bv;
 #pragma unroll
@@ -91,6 +92,7 @@ struct Q8Table {
 };
 
 __global__ __launch_bounds__(256) void quant_w8_kernel(const Q8Table t) {
+  CFL_TS_GUARD;
   for (int g = blockIdx.x * 256 + threadIdx.x; g < t.total; g += gridDim.x * 256) {
     int k = 0;
     while (k + 1 < t.n && t.it[k + 1].blk0 <= g) ++k;
@@ -127,6 +129,7 @@ CFL_DEVICE int f8_perm(int rho) {
 
 template <int TH, int TW, int BN_, int WM, int WN, bool PJ, bool XFIN>
 __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
+  CFL_TS_GUARD;
   constexpr int NT = F8_NT, BK = F8_BK;
   constexpr int BM = TH * TW;
   constexpr int HH = TH + 2, HW = TW + 2, HP = HH * HW;
@@ -533,3 +536,5 @@ int mfma_scale_probe(const int* a, const int* b, const int* sa, const int* sb, f
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_fp8(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_fp8(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -37,6 +37,7 @@ CFL_DEVICE float mask_at(const HeadParams& p, int pix, int S, int q) {
 
 template <int CIN>
 __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
+  CFL_TS_GUARD;
   static_assert(CIN == 32, "4 lanes x 8 channels per pixel");
   __shared__ double red[7][NT / 64];
   const int npix = p.B * p.R * p.R;
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
 // of twice (one launch and a 16.8 MB read fewer at the bench shape)
 template <int CIN, bool NODE, bool FWD>
 __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
+  CFL_TS_GUARD;
   static_assert(CIN == 32, "4 lanes x 8 channels per pixel");
   __shared__ float red[CIN + 1][NT / 64];
   __shared__ float nred[NODE ? 2 * CIN : 1][NT / 64];
@@ -289,3 +291,5 @@ int head_bwd(const HeadParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_head(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_head(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

@@ -562,6 +562,26 @@ int cfl_det_upload_pool_add(int v);
 int cfl_det_upload_pw(int v);
 int cfl_det_upload_sepconv(int v);
 
+// block timeline (common.h CflTsGuard): buf = [cap][2] u64 (dispatch, retire) s_memrealtime stamps per linear block id
+// of every instrumented kernel launched while set; nullptr = off. 0 on success.
+int cfl_ts_set(void* buf, int cap);
+int cfl_ts_upload_bn(void* buf, int cap);
+int cfl_ts_upload_conv3x3(void* buf, int cap);
+int cfl_ts_upload_conv3x3_deep(void* buf, int cap);
+int cfl_ts_upload_conv3x3_sk(void* buf, int cap);
+int cfl_ts_upload_conv3x3_wgrad(void* buf, int cap);
+int cfl_ts_upload_conv_igemm(void* buf, int cap);
+int cfl_ts_upload_conv_wgrad(void* buf, int cap);
+int cfl_ts_upload_datagen(void* buf, int cap);
+int cfl_ts_upload_dwconv(void* buf, int cap);
+int cfl_ts_upload_entry(void* buf, int cap);
+int cfl_ts_upload_fp8(void* buf, int cap);
+int cfl_ts_upload_head(void* buf, int cap);
+int cfl_ts_upload_optim(void* buf, int cap);
+int cfl_ts_upload_pool_add(void* buf, int cap);
+int cfl_ts_upload_pw(void* buf, int cap);
+int cfl_ts_upload_sepconv(void* buf, int cap);
+
 // ---------------------------------------------------------------- misc (optim.hip / datagen.hip)
 int fill_f32(float* p, float v, int64_t n, hipStream_t st);
 int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int rows, int64_t row_bytes,

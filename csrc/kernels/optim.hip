@@ -32,6 +32,7 @@ CFL_DEVICE float step_lr(const OptParams& p) {
 }
 
 __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
+  CFL_TS_GUARD;
   const float lr_t = adam_lr(p.step, p.lr, p.b1, p.b2);
   const int64_t n4 = p.n / 4;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
@@ -56,10 +57,14 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamParams p) {
   }
 }
 
-__global__ void step_done_kernel(int* step) { *step += 1; }
+__global__ void step_done_kernel(int* step) {
+  CFL_TS_GUARD;
+  *step += 1;
+}
 
 __global__ __launch_bounds__(NT) void pack_kernel(const float* flat, bf16_t* packed, const PackView* views,
                                                   int* step, int* cursor) {
+  CFL_TS_GUARD;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     if (step != nullptr) *step += 1;                  // adam_step_done
     if (cursor != nullptr) *cursor += 1;              // next step's batch (BatchSelect)
@@ -143,6 +148,7 @@ CFL_DEVICE int opt_swz(int R, int C) { return (C & 32) | ((C + (((R ^ C) >> 5) <
 
 template <bool VEC>
 __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
+  CFL_TS_GUARD;
   const OptItem it = p.items[blockIdx.x];
   const int tid = threadIdx.x;
   __shared__ float tl[64][65];
@@ -296,10 +302,12 @@ __global__ __launch_bounds__(NT) void opt_step_kernel(const OptParams p) {
 }
 
 __global__ void fill_kernel(float* p, float v, int64_t n) {
+  CFL_TS_GUARD;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) p[i] = v;
 }
 
 __global__ void gather_rows_kernel(const uint8_t* src, const int32_t* idx, uint8_t* dst, int rows, int64_t row_bytes) {
+  CFL_TS_GUARD;
   const int r = blockIdx.y;
   const uint8_t* s = src + (int64_t)idx[r] * row_bytes;
   uint8_t* d = dst + (int64_t)r * row_bytes;
@@ -318,6 +326,7 @@ constexpr int GF_ROWS = 16;
 // default kernel 72 -> 246 VGPRs (occupancy 7 -> 2)
 template <bool DET>
 __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __restrict__ e, int n_entries) {
+  CFL_TS_GUARD;
   // entry of this block: entries are sorted by work_begin; count how many begin at or before blockIdx.x
   const int wb = threadIdx.x < n_entries ? e[threadIdx.x].work_begin : 0x7fffffff;
   const int k = __syncthreads_count(wb <= (int)blockIdx.x) - 1;
@@ -461,6 +470,7 @@ __global__ __launch_bounds__(NT) void grad_finish_kernel(const GradFinish* __res
 constexpr int ZS_CHUNK = 4 * NT;   // zero_spans: 16-byte stores per block per chunk
 
 __global__ void zero_spans_kernel(const ZeroSpan* __restrict__ spans, BatchSelect bs, StepAdvance adv) {
+  CFL_TS_GUARD;
   if (blockIdx.x == 0 && blockIdx.y == 0) {            // block-uniform: the barrier is safe
     if (bs.table != nullptr) {                         // any batch size (the 512^2 plan: ~1,100)
       const size_t row = (size_t)(*bs.cursor % bs.nb) * bs.B;
@@ -523,6 +533,12 @@ int cfl_det_set(int v) {
   for (auto f : up)
     if (f(v)) return 3;
   g_det_host = v;
+  return 0;
+}
+int cfl_ts_set(void* buf, int cap) {
+  int (*const up[])(void*, int) = {cfl_ts_upload_bn, cfl_ts_upload_conv3x3, cfl_ts_upload_conv3x3_deep, cfl_ts_upload_conv3x3_sk, cfl_ts_upload_conv3x3_wgrad, cfl_ts_upload_conv_igemm, cfl_ts_upload_conv_wgrad, cfl_ts_upload_datagen, cfl_ts_upload_dwconv, cfl_ts_upload_entry, cfl_ts_upload_fp8, cfl_ts_upload_head, cfl_ts_upload_optim, cfl_ts_upload_pool_add, cfl_ts_upload_pw, cfl_ts_upload_sepconv};
+  for (auto f : up)
+    if (f(buf, cap)) return 3;
   return 0;
 }
 void cfl_set_tune(int key, int value) {
@@ -605,3 +621,5 @@ int gather_rows_u8(const uint8_t* src, const int32_t* idx, uint8_t* dst, int row
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_optim(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_optim(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

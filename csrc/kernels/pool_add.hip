@@ -14,6 +14,7 @@ namespace {
 constexpr int NT = 256;
 
 __global__ __launch_bounds__(NT) void pool_res_kernel(PoolResParams p) {
+  CFL_TS_GUARD;
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
   float a[8], bb[8];
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(NT) void pool_res_kernel(PoolResParams p) {
 }
 
 __global__ __launch_bounds__(NT) void bn_add_kernel(BnAddParams p) {
+  CFL_TS_GUARD;
   const int G = p.C >> 3, lg = ilog2(G);
   const int c0 = (threadIdx.x & (G - 1)) * 8;
   float a[8], bb[8];
@@ -109,3 +111,5 @@ int bn_add_fwd(const BnAddParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_pool_add(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_pool_add(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

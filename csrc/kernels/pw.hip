@@ -54,6 +54,7 @@ constexpr int pw_rows() { return K >= 128 ? 4096 / K : (S2 ? 32 : 64); }
 // entry: 182 -> 256 VGPRs and spills in the BN-backward form).
 template <int NB, int K, int D, bool BWD, bool S2 = false, int SIDE = SIDE_NONE>
 __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslices, int conv_blocks) {
+  CFL_TS_GUARD;
   int bid = blockIdx.x;
   const int nblocks = conv_blocks;
   if constexpr (SIDE != SIDE_NONE) {
@@ -375,3 +376,5 @@ int pw_conv(const ConvParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_pw(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_pw(void* buf, int cap) { return cfl_ts_upload(buf, cap); }

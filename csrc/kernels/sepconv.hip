@@ -92,6 +92,7 @@ CFL_DEVICE void sep_put(bf16_t* ring, const uint4 (&v)[(R * Sep<K, N, TW>::PIECE
 
 template <int K, int N, int TW, bool XFIN>
 __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int seg_rows) {
+  CFL_TS_GUARD;
   using S = Sep<K, N, TW>;
   constexpr int KS = S::KS, NF = S::NF, RS = S::RS;
   constexpr int P0 = (RS + 2) * S::PIECES, PPT0 = (P0 + NT - 1) / NT;
@@ -310,3 +311,5 @@ int sep_fwd(const SepParams& p, hipStream_t st) {
 
 // deterministic reduction mode flag of this translation unit (common.h g_cfl_det; set by cfl_det_set)
 int cfl_det_upload_sepconv(int v) { return cfl_det_upload(v); }
+// block timeline buffer of this translation unit (common.h g_cfl_ts; set by cfl_ts_set)
+int cfl_ts_upload_sepconv(void* buf, int cap) { return cfl_ts_upload(buf, cap); }
