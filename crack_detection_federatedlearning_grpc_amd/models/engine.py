@@ -738,17 +738,18 @@ class UNetEngine:
         self.C.opt_step(self.opt_table, self.n_opt, self.flat, self.grad, self.m, self.v, self.trainable, self.packed,
                         self.lr, self.b1, self.b2, self.adam_eps, self.momentum, self.step_t, cursor, self.opt_ticket)
 
-    def bind_batches(self, batches: torch.Tensor) -> None:
+    def bind_batches(self, batches: torch.Tensor, checked: bool = False) -> None:
         """Device batch table [nb, B] (int32 dataset indices): every training step takes its batch from row
         ``cursor % nb`` (selected and the cursor advanced by the step's zero_spans launch) instead of
         a host copy into ``idx``. After graph capture the table buffer is fixed (the graph holds its address and
         row count): a table of the same row count is copied in; a smaller one whose row count divides the bound
         one is tiled into it, so ``cursor % nb`` still wraps onto the NEW rows; anything else is refused.
-        Every index is checked against the bound dataset (the kernels read images / masks through them)."""
+        Every index is checked against the bound dataset (the kernels read images / masks through them) - on the
+        device (two host syncs), unless the caller already ``checked`` the host copy it uploaded."""
         batches = batches.to(device=self.dev, dtype=torch.int32).contiguous()
         if batches.dim() != 2 or batches.shape[1] != self.B:
             raise ValueError(f"bind_batches: expected [nb, {self.B}], got {tuple(batches.shape)}")
-        if self.images is not None and batches.numel():
+        if self.images is not None and batches.numel() and not checked:
             lo, hi = int(batches.min()), int(batches.max())
             if lo < 0 or hi >= self.n_data:
                 raise ValueError(f"bind_batches: indices [{lo}, {hi}] outside the bound dataset of {self.n_data}")
@@ -940,6 +941,11 @@ class UNetEngine:
         v = mt.cpu().numpy()
         if reset:
             mt.zero_()
+        return self.metrics_dict(v, which)
+
+    @staticmethod
+    def metrics_dict(v: np.ndarray, which: str = "train") -> Dict[str, float]:
+        """The metric record of a metrics vector (``metrics`` / ``eval_metrics`` layout) read to the host."""
         n = max(v[2], 1.0)
         out = {"loss": float(v[0] / n) * 1.0, "bce_sum": float(v[0]), "accuracy": float(v[1] / n),
                "pixels": float(v[2]), "dice_sum": float(v[3])}
@@ -1049,6 +1055,24 @@ class ParamSnapshot:
         pass
 
 
+class DeferredMetrics:
+    """An epoch's metrics snapshot on the device plus the HIP events around its launches; ``result()`` reads it (the
+    first call synchronises on the snapshot), ``seconds()`` is the GPU time between the events."""
+
+    def __init__(self, snap: torch.Tensor, t0, t1, finish):
+        self.snap, self.t0, self.t1, self.finish = snap, t0, t1, finish
+        self._res: Optional[Dict[str, float]] = None
+
+    def result(self) -> Dict[str, float]:
+        if self._res is None:
+            self._res = self.finish(self.snap.cpu().numpy())
+        return self._res
+
+    def seconds(self) -> float:
+        self.t1.synchronize()
+        return self.t0.elapsed_time(self.t1) / 1e3
+
+
 class HipBackend:
     """``train.local.StepBackend`` on the MI355X engine."""
 
@@ -1078,34 +1102,71 @@ class HipBackend:
         e = self.eng
         return int(e.step_t.item()), e.m.cpu().numpy().copy(), e.v.cpu().numpy().copy()
 
-    def train_batches(self, batches: np.ndarray) -> Dict[str, float]:
+    def _upload_indices(self, idx: np.ndarray) -> torch.Tensor:
+        """Dataset indices to the device without a host sync: range-checked here on the host (the kernels gather
+        images / masks through them), then an asynchronous copy from pinned memory (a pageable copy would wait for
+        the stream to drain)."""
         e = self.eng
-        dev_b = torch.as_tensor(np.asarray(batches, np.int32)).to(e.dev)
+        idx = np.ascontiguousarray(idx, np.int32)
+        if idx.size and (int(idx.min()) < 0 or int(idx.max()) >= e.n_data):
+            raise ValueError(f"indices [{int(idx.min())}, {int(idx.max())}] outside the bound dataset of {e.n_data}")
+        h = torch.from_numpy(idx)
+        if e.dev.type == "cuda":
+            h = h.pin_memory()
+        return h.to(e.dev, non_blocking=True)
+
+    def train_batches_deferred(self, batches: np.ndarray) -> "DeferredMetrics":
+        """One epoch of training steps, issued without any host sync: the batch table goes up asynchronously
+        (range-checked on the host), and the epoch's metrics are snapshotted on the device (stream-ordered clone)
+        between two timing events. ``DeferredMetrics.result()`` reads them later - the FL client resolves a whole
+        round's epochs at once, so the GPU never idles at an epoch boundary waiting for the host (train.local)."""
+        e = self.eng
+        dev_b = self._upload_indices(np.asarray(batches, np.int32))
         e.metrics.zero_()
-        e.bind_batches(dev_b)                  # the steps select their batches on the device (no per-step copy)
+        e.bind_batches(dev_b, checked=True)    # the steps select their batches on the device (no per-step copy)
         e.set_batch_cursor(0)
+        t0 = torch.cuda.Event(enable_timing=True)
+        t0.record()
         for _ in range(dev_b.shape[0]):
             e.train_step(self.use_graph)
-        m = e.read_metrics("train")
-        e.check_fixed_point()
-        if e.dice:
-            m["loss"] = m["loss"] + m["dice_sum"] / max(1, len(batches))
-        return m
+        snap = e.metrics.clone()
+        t1 = torch.cuda.Event(enable_timing=True)
+        t1.record()
+        nb = max(1, len(batches))
 
-    def eval_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        def finish(v: np.ndarray) -> Dict[str, float]:
+            e.check_fixed_point()
+            m = UNetEngine.metrics_dict(v, "train")
+            if e.dice:
+                m["loss"] = m["loss"] + m["dice_sum"] / nb
+            return m
+        return DeferredMetrics(snap, t0, t1, finish)
+
+    def eval_batches_deferred(self, batches: np.ndarray) -> "DeferredMetrics":
         """Validation over the images of ``batches`` (the reference's 16-image batches), evaluated in the largest
         multiple of them up to the eval cap per launch (eval_batch_for / evaluator: same per-pixel means, fewer and
-        fuller launches)."""
+        fuller launches); issued without a host sync, like ``train_batches_deferred``."""
         e = self.eng
         idx = np.asarray(batches, np.int32).reshape(-1)
         ev = e.evaluator(e.eval_batch_for(len(idx)))
         e._await_all()
-        dev_b = torch.as_tensor(idx.reshape(-1, ev.B)).to(e.dev)
+        dev_b = self._upload_indices(idx.reshape(-1, ev.B))
         ev.eval_metrics.zero_()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t0.record()
         for s in range(dev_b.shape[0]):
             ev.idx.copy_(dev_b[s])
             ev.eval_step(self.use_graph)
-        return ev.read_metrics("eval")
+        snap = ev.eval_metrics.clone()
+        t1 = torch.cuda.Event(enable_timing=True)
+        t1.record()
+        return DeferredMetrics(snap, t0, t1, lambda v: UNetEngine.metrics_dict(v, "eval"))
+
+    def train_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        return self.train_batches_deferred(batches).result()
+
+    def eval_batches(self, batches: np.ndarray) -> Dict[str, float]:
+        return self.eval_batches_deferred(batches).result()
 
     def predict(self, idx: np.ndarray) -> np.ndarray:
         e = self.eng

@@ -199,23 +199,34 @@ class LocalFit:
         if cfg.tensorboard:
             from ..utils.tfevents import KerasTensorBoard
             tb = KerasTensorBoard(cfg.log_dir, current_round, cfg.histogram_freq)
+        # a device backend issues every epoch without a host sync and the records are read after the loop (one sync
+        # per round instead of several per epoch: an epoch boundary left the GPU idle while the host read metrics and
+        # uploaded the next batch table); TensorBoard histograms need the weights per epoch, so they keep the
+        # per-epoch reads
+        deferred = tb is None and hasattr(self.backend, "train_batches_deferred")
+        issued = []
         for ep in range(cfg.epochs):
             seed = (cfg.data_seed * 1000003 + current_round * 1009 + ep) & 0x7FFFFFFF
             batches = epoch_batches(self.data.train_idx, cfg.batch_size, self.steps, seed)
+            vbs = None
+            if cfg.validate and len(self.data.val_idx) >= cfg.batch_size:
+                vb = epoch_batches(self.data.val_idx, cfg.batch_size, 0, 0)
+                vbs = vb[:max(1, min(len(vb), self.steps))]
+            if deferred:
+                with phase("fl/train_epoch"):
+                    hm = self.backend.train_batches_deferred(batches)
+                with phase("fl/validate"):
+                    hv = self.backend.eval_batches_deferred(vbs) if vbs is not None else None
+                issued.append((ep, int(batches.size), hm, hv))
+                continue
             t0 = time.perf_counter()
             with phase("fl/train_epoch"):
                 m = self.backend.train_batches(batches)
             dt = time.perf_counter() - t0
-            rec = {"client": self.client, "round": current_round, "epoch": ep + 1, "loss": m["loss"],
-                   "accuracy": m["accuracy"], "images": int(batches.size), "train_s": dt,
-                   "images_per_s": batches.size / max(dt, 1e-9)}
-            if cfg.validate and len(self.data.val_idx) >= cfg.batch_size:
-                vb = epoch_batches(self.data.val_idx, cfg.batch_size, 0, 0)
+            rec = self._epoch_record(current_round, ep, int(batches.size), m, dt)
+            if vbs is not None:
                 with phase("fl/validate"):
-                    v = self.backend.eval_batches(vb[:max(1, min(len(vb), self.steps))])
-                rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
-                if "iou" in v:
-                    rec["val_iou"], rec["val_dice"] = v["iou"], v["dice"]
+                    self._val_record(rec, self.backend.eval_batches(vbs))
             self._log(rec)
             if tb is not None:
                 ws = None
@@ -224,12 +235,28 @@ class LocalFit:
                     ws = [(e.keras_name, flat[e.offset:e.offset + e.size]) for e in self.table.entries]
                 tb.on_epoch_end(ep, rec, ws)
             out = rec
+        for ep, n_img, hm, hv in issued:                      # one sync: the round's records, in epoch order
+            rec = self._epoch_record(current_round, ep, n_img, hm.result(), hm.seconds())
+            if hv is not None:
+                self._val_record(rec, hv.result())
+            self._log(rec)
+            out = rec
         if tb is not None:
             tb.close()
         if current_round == cfg.predict_round and len(self.data.val_idx):
             out["predict"] = self.predict_and_analyze(self.data.val_idx[:min(4, len(self.data.val_idx))])
         self.last = out
         return out
+
+    def _epoch_record(self, current_round: int, ep: int, n_img: int, m: Dict[str, float], dt: float) -> Dict:
+        return {"client": self.client, "round": current_round, "epoch": ep + 1, "loss": m["loss"],
+                "accuracy": m["accuracy"], "images": n_img, "train_s": dt, "images_per_s": n_img / max(dt, 1e-9)}
+
+    @staticmethod
+    def _val_record(rec: Dict, v: Dict[str, float]) -> None:
+        rec["val_loss"], rec["val_accuracy"] = v["loss"], v["accuracy"]
+        if "iou" in v:
+            rec["val_iou"], rec["val_dice"] = v["iou"], v["dice"]
 
     def predict_and_analyze(self, idx: np.ndarray) -> List[Dict[str, float]]:
         """client_fit_model.py:176-223 + test/Segmentation2.py:114-141: predict, threshold, crack contours."""
