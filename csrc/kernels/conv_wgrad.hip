@@ -327,8 +327,12 @@ int wgrad_config(const WgradParams& p, int& bko, int& bno, int& rm) {
   // 32-pixel k-step instead of 4. tools/kbench.py at 512^2 / batch 256: 64x64 / 128x128 (32-px stages) / 128x128
   // (64-px stages) = 890.7 / 454.8 / 382.4 us (64^2, 256->256), 902.8 / 492.0 / 388.2 us (128^2, 128->128),
   // 224.9 / 120.0 / 115.1 us (32^2, 256->256). TUNE_WGRAD1_BIG: 1 = 64x64 tiles, 2 = 32-pixel stages.
-  const int big = cfl_tune(TUNE_WGRAD1_BIG);
-  if (big != 1 && k128 && n128 && p.M >= 65536) {
+  // Round 6: at every M (was M >= 64k): the low-resolution 256-channel layers at 256^2 / batch 16 (32^2 256 -> 256,
+  // 128 -> 256, 16^2 256 -> 256 / 128) re-read x and dy K/64 resp. N/64 times on 64x64 tiles and were the mixed
+  // launch's least efficient items (~3x the block time per MB of a streaming item, tools/mix_timeline.py); 128x128
+  // tiles: their slot time 8.2k -> 3.9k block-us, the mixed launch 136.8 -> 127.9 us in the step
+  // (profiles/r6_wgrad/trace_ab_big3.txt)
+  if (big != 1 && k128 && n128) {
     bko = 128; bno = 128;
     rm = big == 2 ? 32 : 64;
     return big == 2 ? 0 : 6;

@@ -505,7 +505,7 @@ enum TuneKey {
   TUNE_SEP_BLOCKS = 34,        // fused SeparableConv forward: target grid size (default 512)
   TUNE_WGRAD_MIX_XCD = 35,     // mixed wgrad launch: 0 = XCD-grouped block order, 1 = dispatch order
   TUNE_SIDE = 36,              // streaming 1x1 dgrads: 0 = co-launch their side job (SideJob), 1 = run it alone first
-  TUNE_WGRAD1_BIG = 37,        // generic wgrad, K and N % 128 == 0 at M >= 64k: 0 = 128x128 tiles, 64-pixel stages;
+  TUNE_WGRAD1_BIG = 37,        // generic wgrad, K and N % 128 == 0 (any M since round 6): 0 = 128x128 tiles, 64-pixel stages;
                                // 1 = 64x64 tiles; 2 = 128x128 tiles, 32-pixel stages
   TUNE_CONV3_BIG = 38,         // conv3x3 whole-chunk path at M >= 1M pixels: 0 = 16x16-pixel tiles, 1 = off, 2 = force
   TUNE_PW_NB = 39,             // streaming 1x1 kernel, N % 128 == 0 and K >= 128: 0 = 128-channel output slices at
