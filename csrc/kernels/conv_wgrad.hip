@@ -332,6 +332,7 @@ int wgrad_config(const WgradParams& p, int& bko, int& bno, int& rm) {
   // launch's least efficient items (~3x the block time per MB of a streaming item, tools/mix_timeline.py); 128x128
   // tiles: their slot time 8.2k -> 3.9k block-us, the mixed launch 136.8 -> 127.9 us in the step
   // (profiles/r6_wgrad/trace_ab_big3.txt)
+  const int big = cfl_tune(TUNE_WGRAD1_BIG);
   if (big != 1 && k128 && n128) {
     bko = 128; bno = 128;
     rm = big == 2 ? 32 : 64;
