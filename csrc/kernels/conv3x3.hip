@@ -844,9 +844,11 @@ int conv3x3(const ConvParams& p, hipStream_t st) {
     // (the convT1 dgrads with the pj epilogue) unless the bf16 weight-stationary kernel takes the call; the other
     // calls measured faster on the bf16 kernels once those moved to 16x16 tiles on a 4 x 1 wave grid (per position
     // at 512^2: bf16 -77 .. -276 us, the node-join form +217 us - profiles/r5_conv/trace_ab_fp8_routing_512.txt),
-    // 1 = never, 2 = every call that carries fp8 operands, 3 = every call the weight-stationary kernel does not take
+    // 1 = never. Round 6 closed the whole-network fp8 modes (profiles/r6_fp8: every routed kernel 23-150 % slower,
+    // VALU / MFMA 56-168 against 3-9 in bf16 - the per-32 amax / scale / convert of every staged halo chunk); 2 stays
+    // only as a TEST hook (kernel coverage of the non-join shapes, tests/test_gpu_kernels.py), never a product mode.
     const int v = cfl_tune(TUNE_CONV3_F8);
-    if (v == 2 || (v == 3 && !ws_eligible(p)) || (v == 0 && p.pj.v && !ws_eligible(p))) return conv3x3_f8(p, st);
+    if (v == 2 || (v == 0 && p.pj.v && !ws_eligible(p))) return conv3x3_f8(p, st);
     ConvParams q = p;
     q.wt8 = nullptr;
     q.ws8 = nullptr;

@@ -523,8 +523,8 @@ enum TuneKey {
   // 47: retired (opt_step timing knob without its ticket; the training step no longer uses the ticket)
   // 48, 49: retired (split-K-in-block halo wgrad body: slower in the slot-bound mixed launch, deleted in round 6)
   TUNE_CONV3_F8 = 50,          // fp8 3x3 routing: 0 = default (fp8 for the node-join dgrads the weight-stationary bf16
-                               //   kernel does not take), 1 = never, 2 = every call carrying fp8 operands, 3 = every
-                               //   call the weight-stationary kernel does not take
+                               //   kernel does not take), 1 = never; 2 = TEST hook only (every call carrying fp8
+                               //   operands: kernel coverage; the whole-network modes were closed in round 6)
   TUNE_DW_BWD_DMA = 51,        // fused depthwise backward: 0 = default (LDS-DMA dy ring kernel, 3 blocks / CU, when
                                //   the launch has >= 1,536 strips, else the register-staged two-ring kernel), 1 = always
                                //   the DMA kernel, 2 = never

@@ -874,8 +874,8 @@ def test_quant_w8_roundtrip():
 
 @pytest.fixture
 def fp8_forced():
-    """Route every call that carries fp8 operands to the fp8 kernels (TUNE_CONV3_F8 = 2; the default sends only the
-    node-join data gradients there)."""
+    """Route every call that carries fp8 operands to the fp8 kernels (TUNE_CONV3_F8 = 2, a test hook for kernel
+    coverage: the product routes only the node-join data gradients there)."""
     hip().set_tune(hip().TUNE_CONV3_F8, 2)
     yield
     hip().set_tune(hip().TUNE_CONV3_F8, 0)
