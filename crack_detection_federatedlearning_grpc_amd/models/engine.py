@@ -382,7 +382,17 @@ class UNetEngine:
         before graph capture."""
         key = layer if isinstance(layer, tuple) else (layer, "kernel")
         rows, plain = self.C.conv_wgrad_slabs(B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l)
-        n = ks * ks * Cin * N
+        slab = self._wslab(key, rows, plain, ks * ks * Cin * N)
+        args = (x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l, dst_mode, 0, 0,
+                rows)
+        if self._wq is not None:
+            self._wq.append(args)          # deferred: issued as one batch at the end of backward
+        else:
+            self.C.conv_wgrad(*args)
+
+    def _wslab(self, key, rows: int, plain: bool, n: int) -> torch.Tensor:
+        """The partial-row slab of weight ``key`` (``rows`` rows of ``n``; int64 pairs for atomic rows in the
+        deterministic mode) registered with grad_finish; (re)allocated on the eager warm-up pass only."""
         slab = self._wslabs.get(key)
         if slab is None or slab.numel() != rows * n * (1 if plain else self._w):
             if self.dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
@@ -399,12 +409,24 @@ class UNetEngine:
                 self._finish_dyn.append((slab, dst, n, rows, self.C.GF_SUM if plain else self.C.GF_REDUCE))
             self._wslabs[key] = slab
             self._finish_dirty = True
-        args = (x, dy, slab, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride, pad_t, pad_l, dst_mode, 0, 0,
-                rows)
-        if self._wq is not None:
-            self._wq.append(args)          # deferred: issued as one batch at the end of backward
-        else:
-            self.C.conv_wgrad(*args)
+        return slab
+
+    def _pw_bwd(self, g, y, bname, d, dd, dy, layer, B, H, K, N) -> None:
+        """Backward of an encoder pointwise conv (K = its output channels, N = its input channels) whose output
+        feeds BN ``bname``: dd = W^T BN_bwd(g, y) and the pointwise weight gradient. One fused streaming pass
+        (pw_bwd.hip) where it supports the shape and TUNE_PWB is 0; otherwise pw.hip's dgrad with the BN backward
+        folded into its operand load (it also stores dy) and the weight gradient from (d, dy)."""
+        C = self.C
+        if C.get_tune(C.TUNE_PWB) == 0 and C.pw_bwd_supported(B, H, H, K, N):
+            rows = C.conv_wgrad_slabs(B, H, H, N, 0, H, H, K, 1, 1, 0, 0)[0]
+            slab = self._wslab((layer, "pointwise_kernel"), rows, False, N * K)
+            bb = self.bn[bname]
+            C.pw_bwd(g, y, bb["ab"], bb["sums"], self.RS, self.W(layer, PK_PW_DGRAD), d, dd, slab, rows,
+                     self.G(bname, "gamma"), self.G(bname, "beta"), B, H, H, K, N)
+            return
+        self._igemm(g, self.W(layer, PK_PW_DGRAD), None, dd, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0,
+                    bwd=(y, bname, dy))
+        self._wgrad(d, dy, (layer, "pointwise_kernel"), None, 0, B, H, H, N, 0, H, H, K, 1, 1, 0, 0, 0)
 
     def bn_count(self, name: str) -> int:
         """Pixels per channel in the batch statistics of a BN layer."""
@@ -685,22 +707,18 @@ class UNetEngine:
             # bias grad: sum(dx_out) == sum(g_b) == dbeta_b (max-pool routing keeps sums) -> grad_finish copy
             self._igemm(dx_out, self.W(rc, PK_CONV_DGRAD1x1), None, D[f"e{k}_dres"], None, None, 0, B, H // 2,
                         H // 2, F, 0, H // 2, H // 2, cin, 1, 1, 0, 0, side_pool=pool_b)
-            # pointwise 2: its dgrad applies BN_b's backward on load and stores dy
-            self._igemm(D[f"e{k}_g"], self.W(s2, PK_PW_DGRAD), None, D[f"e{k}_dd2"], None,
-                        None, 0, B, H, H, F, 0, H, H, F, 1, 1, 0, 0, bwd=(A[f"e{k}_y2"], b2, D[f"e{k}_dy"]))
-            self._wgrad(A[f"e{k}_d2"], D[f"e{k}_dy"], (s2, "pointwise_kernel"), None, 0, B, H, H,
-                        F, 0, H, H, F, 1, 1, 0, 0, 0)
+            # pointwise 2 with BN_b's backward folded in (dgrad + weight gradient)
+            self._pw_bwd(D[f"e{k}_g"], A[f"e{k}_y2"], b2, A[f"e{k}_d2"], D[f"e{k}_dd2"], D[f"e{k}_dy"], s2, B, H, F,
+                         F)
             # depthwise 2 on relu(BN_a(y1)): dgrad with the BN_a node (ReLU mask + sums) fused into its epilogue
             # and the weight gradient from the same dy rows, one pass
             C.dw_bwd(A[f"e{k}_y1"], bna["ab"], 1, D[f"e{k}_dd2"], self.P(s2, "depthwise_kernel"), D[f"e{k}_g"],
                      self.gslab[(s2, "depthwise_kernel")], self.C.STAT_REPLICAS, B, H, H, F,
                      node_y=A[f"e{k}_y1"], node_ab=bna["ab"], node_sums=bna["sums"], node_reps=self.RS,
                      node_relu=1)
-            # pointwise 1 (BN_a's backward applied on load)
-            self._igemm(D[f"e{k}_g"], self.W(s1, PK_PW_DGRAD), None, D[f"e{k}_dd1"],
-                        None, None, 0, B, H, H, F, 0, H, H, cin, 1, 1, 0, 0, bwd=(A[f"e{k}_y1"], b1, D[f"e{k}_dy2"]))
-            self._wgrad(A[f"e{k}_d1"], D[f"e{k}_dy2"], (s1, "pointwise_kernel"), None, 0, B, H,
-                        H, cin, 0, H, H, F, 1, 1, 0, 0, 0)
+            # pointwise 1 with BN_a's backward folded in
+            self._pw_bwd(D[f"e{k}_g"], A[f"e{k}_y1"], b1, A[f"e{k}_d1"], D[f"e{k}_dd1"], D[f"e{k}_dy2"], s1, B, H, F,
+                         cin)
             # residual 1x1 stride-2 conv on x_in (dres = dx_out)
             self._wgrad(xin.t, dx_out, rc, xin.ab, xin.relu, B, H, H, cin, 0, H // 2, H // 2, F,
                         1, 2, 0, 0, 0)

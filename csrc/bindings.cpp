@@ -274,6 +274,47 @@ void conv_wgrad_op(at::Tensor x, at::Tensor dy, at::Tensor dw, OptT ab, int relu
 
 // calls: a list of conv_wgrad argument tuples (x, dy, dw, ab, relu, B, Hin, Win, Cin, up_in, Ho, Wo, N, ks, stride,
 // pad_t, pad_l, dst_mode, m_chunk, algo, slabs) -> one batch (3x3 halo wgrads grouped into shared launches)
+// fused pointwise backward (pw_bwd.hip): g, y [B,H,W,K]; d, dd [B,H,W,N]; w [N*K] packed PK_PW_DGRAD; dw replica
+// rows [replicas][N*K] (x2 int64 in the deterministic mode); the BN rows / sums of the BN that y feeds
+bool pw_bwd_supported_op(int B, int H, int W, int K, int N) {
+  PwBwdParams p{};
+  p.M = B * H * W;
+  p.K = K;
+  p.N = N;
+  p.replicas = 1;
+  p.bwd.reps = 1;
+  return pw_bwd_supported(p);
+}
+
+void pw_bwd_op(torch::Tensor g, torch::Tensor y, torch::Tensor ab, torch::Tensor sums, int reps, torch::Tensor w,
+               torch::Tensor d, torch::Tensor dd, torch::Tensor dw, int replicas, OptT dgamma, OptT dbeta, int B,
+               int H, int W, int K, int N) {
+  const int64_t M = (int64_t)B * H * W;
+  TORCH_CHECK(g.numel() == M * K && y.numel() == M * K && d.numel() == M * N && dd.numel() == M * N &&
+              w.numel() >= (int64_t)N * K && ab.numel() >= 4 * K && sums.numel() >= (int64_t)reps * 2 * K &&
+              dw.numel() >= (int64_t)replicas * N * K * (cfl_det_host() ? 2 : 1), "pw_bwd: tensor sizes");
+  PwBwdParams p{};
+  p.g = ptr<const bf16_t>(g, "g");
+  p.y = ptr<const bf16_t>(y, "y");
+  p.d = ptr<const bf16_t>(d, "d");
+  p.w = ptr<const bf16_t>(w, "w");
+  p.dd = ptr<bf16_t>(dd, "dd");
+  p.dw = ptr<float>(dw, "dw");
+  p.bwd.y = p.y;
+  p.bwd.ab = ptr<const float>(ab, "ab");
+  p.bwd.sums = ptr<const float>(sums, "sums");
+  p.bwd.reps = reps;
+  p.bwd.invM = 1.f / (float)M;
+  p.bwd.dgamma = optr<float>(dgamma, "dgamma");
+  p.bwd.dbeta = optr<float>(dbeta, "dbeta");
+  p.M = (int)M;
+  p.K = K;
+  p.N = N;
+  p.replicas = replicas;
+  TORCH_CHECK(pw_bwd_supported(p), "pw_bwd: unsupported shape");
+  ok(pw_bwd(p, stream()), "pw_bwd");
+}
+
 void conv_wgrad_batch_op(py::list calls) {
   std::vector<WgradParams> ps;
   for (auto h : calls) {
@@ -879,6 +920,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("ks"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("dst_mode"),
         py::arg("m_chunk") = 0, py::arg("algo") = 0, py::arg("slabs") = 0);
   m.def("conv_wgrad_batch", &conv_wgrad_batch_op, py::arg("calls"));
+  m.def("pw_bwd_supported", &pw_bwd_supported_op);
+  m.def("pw_bwd", &pw_bwd_op, py::arg("g"), py::arg("y"), py::arg("ab"), py::arg("sums"), py::arg("reps"),
+        py::arg("w"), py::arg("d"), py::arg("dd"), py::arg("dw"), py::arg("replicas"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("K"), py::arg("N"));
   m.def("conv_wgrad_slabs", &conv_wgrad_slabs_op, py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("Cin"),
         py::arg("up_in"), py::arg("Ho"), py::arg("Wo"), py::arg("N"), py::arg("ks"), py::arg("stride"),
         py::arg("pad_t"), py::arg("pad_l"), py::arg("algo") = 0);
@@ -973,6 +1018,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_WGRAD_MIX_LIST") = (int)TUNE_WGRAD_MIX_LIST;
   m.attr("TUNE_WGRAD_MIX_ORDER") = (int)TUNE_WGRAD_MIX_ORDER;
   m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
+  m.attr("TUNE_PWB") = (int)TUNE_PWB;
+  m.attr("TUNE_PWB_BLOCKS") = (int)TUNE_PWB_BLOCKS;
   m.attr("TUNE_CONV3_F8") = (int)TUNE_CONV3_F8;
   m.attr("TUNE_DW_BWD_DMA") = (int)TUNE_DW_BWD_DMA;
   m.attr("TUNE_WGRAD3_WIDE") = (int)TUNE_WGRAD3_WIDE;

@@ -242,6 +242,13 @@ struct CflTsGuard {
   }
 };
 #define CFL_TS_GUARD CflTsGuard cfl_ts_guard_
+// phase stamp k (0 or 1) of this block, thread 0, at buf[2 * (cap / 2 + linear block id) + k]: the upper half of
+// the buffer holds two in-kernel phase boundaries per block (tools/gpu phase probes; cap must cover twice the grid)
+CFL_DEVICE void cfl_ts_phase(int k) {
+  if (g_cfl_ts.buf == nullptr || threadIdx.x != 0) return;
+  const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (b < g_cfl_ts.cap / 2) g_cfl_ts.buf[2 * (g_cfl_ts.cap / 2 + b) + k] = cfl_ts_now();
+}
 static inline int cfl_ts_upload(void* buf, int cap) {
   const CflTs t{reinterpret_cast<unsigned long long*>(buf), cap};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cfl_ts), &t, sizeof(t)) == hipSuccess ? 0 : 3;
@@ -362,38 +369,61 @@ CFL_DEVICE void bnb_prologue(const BnBwdIn& q, int C, float* co, float* part, bo
   }
   float s_lo = 0.f, s_hi = 0.f;                 // sums of element t (and t + NTH when C2 > NTH)
   const bool det = cfl_det();                   // int64 fixed-point rows: summed as integers, converted once
+  // every replica-row load is unconditional (row index clamped into range, rows past reps weighted 0) so all of
+  // them issue back to back and the block waits ONE memory round trip: guarded per-row loads compiled to a branch
+  // and a full wait per row (16 serial round trips at reps 16, measured as most of a block's fixed cost)
+  const int rlast = reps - 1;
   if (C2 <= NTH) {
     const int per = NTH / C2, e = t % C2, j = t / C2;
     float v = 0.f;
     long long vi = 0;
+    if (det) {
+      long long x[BNB_MAX_REPS];
 #pragma unroll
-    for (int k = 0; k < BNB_MAX_REPS; ++k) {
-      const int r = j + k * per;
-      if (r < reps) {
-        if (det) vi += red_raw(q.sums, (size_t)r * C2 + e);
-        else v += q.sums[(size_t)r * C2 + e];
-      }
+      for (int k = 0; k < BNB_MAX_REPS; ++k) x[k] = red_raw(q.sums, (size_t)imin(j + k * per, rlast) * C2 + e);
+#pragma unroll
+      for (int k = 0; k < BNB_MAX_REPS; ++k) vi += j + k * per < reps ? x[k] : 0ll;
+    } else {
+      float x[BNB_MAX_REPS];
+#pragma unroll
+      for (int k = 0; k < BNB_MAX_REPS; ++k) x[k] = q.sums[(size_t)imin(j + k * per, rlast) * C2 + e];
+#pragma unroll
+      for (int k = 0; k < BNB_MAX_REPS; ++k)
+        if (j + k * per < reps) v += x[k];
     }
     part[t] = det ? red_fx(vi, CFL_FX_G) : v;
     __syncthreads();
     if (t < C2)
       for (int k = 0; k < per; ++k) s_lo += part[k * C2 + t];
   } else {                                      // C2 == 2 * NTH at most (C <= 256, NTH = 256)
-    long long lo = 0, hi = 0;
-#pragma unroll
-    for (int r = 0; r < BNB_MAX_REPS; ++r)
-      if (r < reps) {
-        if (det) {
-          lo += red_raw(q.sums, (size_t)r * C2 + t);
-          hi += red_raw(q.sums, (size_t)r * C2 + t + NTH);
-        } else {
-          s_lo += q.sums[(size_t)r * C2 + t];
-          s_hi += q.sums[(size_t)r * C2 + t + NTH];
-        }
-      }
     if (det) {
+      long long xl[BNB_MAX_REPS], xh[BNB_MAX_REPS], lo = 0, hi = 0;
+#pragma unroll
+      for (int r = 0; r < BNB_MAX_REPS; ++r) {
+        xl[r] = red_raw(q.sums, (size_t)imin(r, rlast) * C2 + t);
+        xh[r] = red_raw(q.sums, (size_t)imin(r, rlast) * C2 + t + NTH);
+      }
+#pragma unroll
+      for (int r = 0; r < BNB_MAX_REPS; ++r)
+        if (r < reps) {
+          lo += xl[r];
+          hi += xh[r];
+        }
       s_lo = red_fx(lo, CFL_FX_G);
       s_hi = red_fx(hi, CFL_FX_G);
+    } else {
+      float xl[BNB_MAX_REPS], xh[BNB_MAX_REPS];
+#pragma unroll
+      for (int r = 0; r < BNB_MAX_REPS; ++r) {
+        xl[r] = q.sums[(size_t)imin(r, rlast) * C2 + t];
+        xh[r] = q.sums[(size_t)imin(r, rlast) * C2 + t + NTH];
+      }
+#pragma unroll
+      for (int r = 0; r < BNB_MAX_REPS; ++r)
+        if (r < reps) {
+          s_lo += xl[r];
+          s_hi += xh[r];
+        }
     }
   }
   // element e < C is s0[e], e >= C is s1[e - C]
@@ -419,18 +449,30 @@ CFL_DEVICE void bnb_prologue(const BnBwdIn& q, int C, float* co, float* part, bo
 // dx of 8 channels c0..c0+7 from 8 g and 8 y values (coefficients from bnb_prologue's LDS block)
 // (co 16-byte aligned, C and c0 multiples of 8: the five coefficient rows are read as 16-byte vectors - 10 LDS reads
 // per call instead of 40 scalar ones)
-CFL_DEVICE uint4 bnb_apply8(const uint4& gv, const uint4& yv, const float* co, int C, int c0) {
-  float g[8], y[8], o[8], a[8], mean[8], rstd[8], k1[8], k2[8];
+// The five coefficient vectors of channels c0..c0+7 in registers, for callers that apply them to many pixels
+// (pw_bwd.hip: a thread's channel group is fixed for the whole launch)
+struct BnbCo8 {
+  float a[8], mean[8], rstd[8], k1[8], k2[8];
+};
+CFL_DEVICE BnbCo8 bnb_co8(const float* co, int C, int c0) {
+  BnbCo8 k;
+  load_f8(co + c0, k.a);
+  load_f8(co + C + c0, k.mean);
+  load_f8(co + 2 * C + c0, k.rstd);
+  load_f8(co + 3 * C + c0, k.k1);
+  load_f8(co + 4 * C + c0, k.k2);
+  return k;
+}
+CFL_DEVICE uint4 bnb_apply8(const uint4& gv, const uint4& yv, const BnbCo8& k) {
+  float g[8], y[8], o[8];
   unpack8(gv, g);
   unpack8(yv, y);
-  load_f8(co + c0, a);
-  load_f8(co + C + c0, mean);
-  load_f8(co + 2 * C + c0, rstd);
-  load_f8(co + 3 * C + c0, k1);
-  load_f8(co + 4 * C + c0, k2);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = bnb_apply(g[j], y[j], a[j], mean[j], rstd[j], k1[j], k2[j]);
+  for (int j = 0; j < 8; ++j) o[j] = bnb_apply(g[j], y[j], k.a[j], k.mean[j], k.rstd[j], k.k1[j], k.k2[j]);
   return pack8(o);
+}
+CFL_DEVICE uint4 bnb_apply8(const uint4& gv, const uint4& yv, const float* co, int C, int c0) {
+  return bnb_apply8(gv, yv, bnb_co8(co, C, c0));
 }
 
 // One half-resolution pixel of a PoolJoinEpi (launch.h) from the four bf16 conv outputs of its 2x2 block and the

@@ -215,6 +215,22 @@ int conv_wgrad_slabs(const WgradParams& p);
 bool conv_wgrad_plain_slabs(const WgradParams& p);   // slab rows are plain-stored (else atomic replica rows)
 #define WGRAD_REPLICAS 16
 
+// ---------------------------------------------------------------- fused pointwise backward (pw_bwd.hip)
+// dgrad + wgrad of a pointwise conv whose output feeds a BatchNorm, the BN backward folded in:
+//   dy = bnb_apply(g, y);  dd = dy * W^T (stored);  dW = d^T dy (added into replica row blockIdx % replicas)
+struct PwBwdParams {
+  const bf16_t* g;         // [M][K] gradient w.r.t. the BN output (K = pw output channels)
+  const bf16_t* y;         // [M][K] BN input (the pw output)  -- bwd.y mirrors it
+  const bf16_t* d;         // [M][N] pw input (N = pw input channels)
+  const bf16_t* w;         // [N][K] dgrad weights (pack PK_PW_DGRAD)
+  bf16_t* dd;              // [M][N] dgrad output
+  float* dw;               // [replicas][N * K] weight-gradient replica rows (Keras (1,1,N,K); int64 in det mode)
+  BnBwdIn bwd;             // BN coefficients / node sums / dgamma, dbeta (dx unused)
+  int M, K, N, replicas;
+};
+bool pw_bwd_supported(const PwBwdParams& p);
+int pw_bwd(const PwBwdParams& p, hipStream_t st);
+
 // ---------------------------------------------------------------- fused SeparableConv forward (sepconv.hip)
 // y = pointwise(depthwise3x3(T(x))) + bias with the BN statistics of y; d = the depthwise output (side-stored for the
 // pointwise weight gradient). T = xf (BN-apply + ReLU; xfin: computed here from the producer's replica sums).
@@ -532,7 +548,10 @@ enum TuneKey {
                                //   32-channel tile-blocks: the 512^2 planned batch), 1 = never, 2 = whenever Cin % 64 == 0
   TUNE_CONV3_BIG_WAVES = 53,   // conv3x3 16x16-pixel tiles: wave grid 0 = default (4 x 1: 64 px x 64 ch per wave), 1 = 2 x 2
   TUNE_WGRAD_DIRECT = 54,      // generic wgrad, 1x1 / stride-1 convs in the mixed launch: 0 = direct-row body, 1 = general
-  TUNE_N = 55
+  TUNE_PWB_BLOCKS = 55,        // fused pointwise backward (pw_bwd.hip): grid (default 384 at N = 32, 256 at N = 64)
+  TUNE_PWB = 56,               // encoder pointwise backward: 0 = fused dgrad + wgrad (pw_bwd.hip), 1 = pw.hip dgrad +
+                               //   deferred wgrad (round 5)
+  TUNE_N = 57
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
@@ -560,6 +579,7 @@ int cfl_det_upload_head(int v);
 int cfl_det_upload_optim(int v);
 int cfl_det_upload_pool_add(int v);
 int cfl_det_upload_pw(int v);
+int cfl_det_upload_pw_bwd(int v);
 int cfl_det_upload_sepconv(int v);
 
 // block timeline (common.h CflTsGuard): buf = [cap][2] u64 (dispatch, retire) s_memrealtime stamps per linear block id
@@ -580,6 +600,7 @@ int cfl_ts_upload_head(void* buf, int cap);
 int cfl_ts_upload_optim(void* buf, int cap);
 int cfl_ts_upload_pool_add(void* buf, int cap);
 int cfl_ts_upload_pw(void* buf, int cap);
+int cfl_ts_upload_pw_bwd(void* buf, int cap);
 int cfl_ts_upload_sepconv(void* buf, int cap);
 
 // ---------------------------------------------------------------- misc (optim.hip / datagen.hip)

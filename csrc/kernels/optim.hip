@@ -512,7 +512,7 @@ static int (*const g_det_up[])(int) = {cfl_det_upload_bn, cfl_det_upload_conv3x3
                             cfl_det_upload_conv3x3_sk, cfl_det_upload_conv3x3_wgrad, cfl_det_upload_conv_igemm,
                             cfl_det_upload_conv_wgrad, cfl_det_upload_datagen, cfl_det_upload_dwconv,
                             cfl_det_upload_entry, cfl_det_upload_fp8, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
-                            cfl_det_upload_pw, cfl_det_upload_sepconv};
+                            cfl_det_upload_pw, cfl_det_upload_pw_bwd, cfl_det_upload_sepconv};
 // 1 if any TU's fixed-point overflow flag is raised (cleared by cfl_det_set), 0 if none, 3 on a copy error
 int cfl_fx_overflow() {
   int any = 0;
@@ -529,14 +529,14 @@ int cfl_det_set(int v) {
                             cfl_det_upload_conv3x3_sk, cfl_det_upload_conv3x3_wgrad, cfl_det_upload_conv_igemm,
                             cfl_det_upload_conv_wgrad, cfl_det_upload_datagen, cfl_det_upload_dwconv,
                             cfl_det_upload_entry, cfl_det_upload_fp8, cfl_det_upload_head, cfl_det_upload_optim, cfl_det_upload_pool_add,
-                            cfl_det_upload_pw, cfl_det_upload_sepconv};
+                            cfl_det_upload_pw, cfl_det_upload_pw_bwd, cfl_det_upload_sepconv};
   for (auto f : up)
     if (f(v)) return 3;
   g_det_host = v;
   return 0;
 }
 int cfl_ts_set(void* buf, int cap) {
-  int (*const up[])(void*, int) = {cfl_ts_upload_bn, cfl_ts_upload_conv3x3, cfl_ts_upload_conv3x3_deep, cfl_ts_upload_conv3x3_sk, cfl_ts_upload_conv3x3_wgrad, cfl_ts_upload_conv_igemm, cfl_ts_upload_conv_wgrad, cfl_ts_upload_datagen, cfl_ts_upload_dwconv, cfl_ts_upload_entry, cfl_ts_upload_fp8, cfl_ts_upload_head, cfl_ts_upload_optim, cfl_ts_upload_pool_add, cfl_ts_upload_pw, cfl_ts_upload_sepconv};
+  int (*const up[])(void*, int) = {cfl_ts_upload_bn, cfl_ts_upload_conv3x3, cfl_ts_upload_conv3x3_deep, cfl_ts_upload_conv3x3_sk, cfl_ts_upload_conv3x3_wgrad, cfl_ts_upload_conv_igemm, cfl_ts_upload_conv_wgrad, cfl_ts_upload_datagen, cfl_ts_upload_dwconv, cfl_ts_upload_entry, cfl_ts_upload_fp8, cfl_ts_upload_head, cfl_ts_upload_optim, cfl_ts_upload_pool_add, cfl_ts_upload_pw, cfl_ts_upload_pw_bwd, cfl_ts_upload_sepconv};
   for (auto f : up)
     if (f(buf, cap)) return 3;
   return 0;

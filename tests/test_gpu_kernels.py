@@ -1034,7 +1034,7 @@ def test_engine_fp8_quantises_after_late_fedavg_buckets(fp8_forced):
         C_.set_det(0)
 
 
-@pytest.mark.parametrize("which", ["dw_dma", "wide", "big", "all"])
+@pytest.mark.parametrize("which", ["dw_dma", "wide", "big", "pwb", "all"])
 def test_engine_large_launch_paths_match_default(which):
     """The engine with the paths the 512^2 planned batch selects by size forced at a small shape - the LDS-DMA fused
     depthwise backward (DW_BWD_DMA = 1), the 64-input-channel halo weight-gradient blocks (WGRAD3_WIDE = 2, their slab
@@ -1051,7 +1051,8 @@ def test_engine_large_launch_paths_match_default(which):
     table = ParamTable()
     data = make_synthetic_device(8, 128, seed=11)
     flat = table.init_flat(11)
-    all_knobs = {"dw_dma": (C_.TUNE_DW_BWD_DMA, 1), "wide": (C_.TUNE_WGRAD3_WIDE, 2), "big": (C_.TUNE_CONV3_BIG, 2)}
+    all_knobs = {"dw_dma": (C_.TUNE_DW_BWD_DMA, 1), "wide": (C_.TUNE_WGRAD3_WIDE, 2), "big": (C_.TUNE_CONV3_BIG, 2),
+                 "pwb": (C_.TUNE_PWB, 1)}
     knobs = list(all_knobs.values()) if which == "all" else [all_knobs[which]]
     res = []
     try:
@@ -1079,6 +1080,10 @@ def test_engine_large_launch_paths_match_default(which):
     print(which, "loss", l0, l1, "grad rel", rel(g1, g0))
     if which in ("dw_dma", "wide"):
         assert abs(l1 - l0) / l0 < 1e-12 and torch.equal(g1, g0), (l0, l1, rel(g1, g0))
+    elif which == "pwb":
+        # the unfused encoder pointwise backward (pw.hip dgrad + mixed-launch wgrad): the same BN grads, dy (so dd and
+        # everything upstream of it) to bf16 rounding (pw_bwd.hip regroups the BN-backward apply), the forward equal
+        assert abs(l1 - l0) / l0 < 1e-12 and rel(g1, g0) < 1e-2, (l0, l1, rel(g1, g0))
     else:
         assert abs(l1 - l0) / l0 < 1e-3, (l0, l1)
         assert rel(g1, g0) < 1e-2, rel(g1, g0)
@@ -2584,3 +2589,93 @@ def test_pw_streaming_1x1_matches_igemm_and_reference(B, H, Cin, N, use_stats, u
         assert torch.allclose(sts[0].double()[0], o.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
         assert torch.allclose(sts[0].double()[1], (o * o).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
         assert torch.allclose(sts[0], sts[1], rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("K,N,B,H,blocks,det", [
+    (64, 32, 2, 32, 0, 0), (64, 64, 2, 32, 0, 0),
+    (64, 64, 4, 128, 0, 0),          # 1024 tiles over the 256-block grid: four tiles per block, the prefetch path
+    (64, 32, 2, 32, 3, 0),           # 3 blocks: many tiles per block, the clamped refill past the last tile
+    (64, 32, 2, 32, 0, 1), (64, 64, 2, 16, 5, 1),
+])
+def test_pw_bwd_fused_matches_two_pass(K, N, B, H, blocks, det):
+    """The fused encoder pointwise backward (pw_bwd.hip: BN backward apply + dgrad + wgrad in one streaming pass)
+    vs the two-pass form it replaces - pw.hip's dgrad with the BN backward folded in (it stores dy) and conv_wgrad's
+    replica-row weight gradient of (d, dy). The fused kernel applies the BN backward as A g + (Bc y + Cc) (the same
+    value regrouped, two packed FMAs) so dy - and through it dd and dW - match to bf16 rounding: dd and dW vs the
+    two-pass form and vs fp32 references of the fp32 dy; dgamma / dbeta (the shared bnb_prologue) bit-identical; in
+    the deterministic mode two runs give the same dW bits."""
+    torch.manual_seed(43)
+    C_ = hip()
+    reps = 16
+    M = B * H * H
+    gb, g32 = bf(torch.randn(B, H, H, K))
+    yb, y32 = bf(torch.randn(B, H, H, K) * 0.7 + 0.2)
+    db, d32 = bf(torch.randn(B, H, H, N))
+    ab, a, _ = ab_for(K, 13)
+    mean, rstd = torch.randn(K) * 0.1 + 0.2, torch.rand(K) + 0.6
+    ab[2 * K:3 * K], ab[3 * K:] = mean, rstd
+    ab = ab.to(DEV)
+    sums = (torch.randn(reps, 2, K) * (M / reps) ** 0.5).reshape(-1)
+    s32 = sums.view(reps, 2, K).sum(0)
+    if det:             # the deterministic mode's node sums are int64 fixed point (red_add at CFL_FX_G = 2^40)
+        sums = (sums.double() * 2.0 ** 40).round().long().view(torch.float32)
+    sums = sums.to(DEV)
+    wk = torch.randn(1, 1, N, K) * 0.05
+    wpk = pack(PK_PW_DGRAD, wk, 1, N, K)
+    dy32 = (a * (g32 - s32[0] / M - (y32 - mean) * rstd * s32[1] / M)).reshape(M, K)
+    dd32 = dy32 @ wk.reshape(N, K).to(torch.bfloat16).float().t()
+    dw32 = (d32.reshape(M, N).t() @ dy32).reshape(-1)
+    rows = C_.conv_wgrad_slabs(B, H, H, N, 0, H, H, K, 1, 1, 0, 0)[0]
+    assert C_.pw_bwd_supported(B, H, H, K, N)
+    C_.set_tune(C_.TUNE_PWB_BLOCKS, blocks)
+    C_.set_det(det)
+    try:
+        def finish(slab):
+            dst = torch.zeros(N * K, device=DEV)
+            table, work = C_.make_grad_finish_table([(slab, dst, N * K, rows, C_.GF_REDUCE)])
+            C_.grad_finish(table, 1, work)
+            return dst
+
+        def fused():
+            dd = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+            slab = torch.zeros(rows * N * K * (2 if det else 1), device=DEV)
+            dgam, dbet = torch.zeros(K, device=DEV), torch.zeros(K, device=DEV)
+            C_.pw_bwd(gb, yb, ab, sums, reps, wpk, db, dd, slab, rows, dgam, dbet, B, H, H, K, N)
+            torch.cuda.synchronize()
+            return dd, finish(slab), dgam, dbet
+
+        dd_r = torch.zeros(B, H, H, N, dtype=torch.int16, device=DEV)
+        dy = torch.zeros_like(gb)
+        dgam_r, dbet_r = torch.zeros(K, device=DEV), torch.zeros(K, device=DEV)
+        C_.conv_igemm(gb, wpk, None, dd_r, None, None, 0, B, H, H, K, 0, H, H, N, 1, 1, 0, 0, None, bwd_y=yb,
+                      bwd_ab=ab, bwd_sums=sums, bwd_reps=reps, bwd_dx=dy, bwd_dgamma=dgam_r, bwd_dbeta=dbet_r)
+        slab_r = torch.zeros(rows * N * K * (2 if det else 1), device=DEV)
+        C_.conv_wgrad(db, dy, slab_r, None, 0, B, H, H, N, 0, H, H, K, 1, 1, 0, 0, 0, 0, 0, rows)
+        torch.cuda.synchronize()
+        dw_r = finish(slab_r)
+        dd, dw, dgam, dbet = fused()
+        assert torch.equal(dgam, dgam_r) and torch.equal(dbet, dbet_r)
+        assert rel(from_bits(dd).reshape(M, N), dd32) < 5e-3, rel(from_bits(dd).reshape(M, N), dd32)
+        assert rel(from_bits(dd), from_bits(dd_r)) < 5e-3
+        assert rel(dw.cpu(), dw32) < 5e-3, rel(dw.cpu(), dw32)
+        assert rel(dw.cpu(), dw_r.cpu()) < 5e-3
+        if det:
+            assert torch.equal(fused()[1], dw)
+    finally:
+        C_.set_tune(C_.TUNE_PWB_BLOCKS, 0)
+        C_.set_det(0)
+
+
+def test_pw_bwd_refuses_unsupported_shapes():
+    """pw_bwd covers the encoder's 128^2-level pointwise shapes (K 64: N 32, 64; M % 64 == 0); anything else is
+    refused (the engine then takes the two-pass path)."""
+    C_ = hip()
+    assert C_.pw_bwd_supported(2, 16, 16, 64, 32) and C_.pw_bwd_supported(2, 16, 16, 64, 64)
+    assert not C_.pw_bwd_supported(1, 4, 4, 64, 32)        # M = 16
+    assert not C_.pw_bwd_supported(2, 16, 16, 128, 64) and not C_.pw_bwd_supported(2, 16, 16, 128, 128)
+    assert not C_.pw_bwd_supported(2, 16, 16, 256, 128)
+    assert not C_.pw_bwd_supported(2, 16, 16, 64, 128)
+    t = torch.zeros(16 * 64, dtype=torch.int16, device=DEV)
+    with pytest.raises(RuntimeError):
+        C_.pw_bwd(t, t, torch.zeros(256, device=DEV), torch.zeros(128, device=DEV), 1, t, t[:512], t[:512],
+                  torch.zeros(2048, device=DEV), 1, None, None, 1, 4, 4, 64, 32)
