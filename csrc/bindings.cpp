@@ -1020,6 +1020,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("TUNE_OPT_SCALAR") = (int)TUNE_OPT_SCALAR;
   m.attr("TUNE_PWB") = (int)TUNE_PWB;
   m.attr("TUNE_PWB_BLOCKS") = (int)TUNE_PWB_BLOCKS;
+  m.attr("TUNE_WGRAD_REPS") = (int)TUNE_WGRAD_REPS;
   m.attr("TUNE_CONV3_F8") = (int)TUNE_CONV3_F8;
   m.attr("TUNE_DW_BWD_DMA") = (int)TUNE_DW_BWD_DMA;
   m.attr("TUNE_WGRAD3_WIDE") = (int)TUNE_WGRAD3_WIDE;

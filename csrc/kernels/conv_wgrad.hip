@@ -449,7 +449,7 @@ int conv3x3_wgrad_splits(const WgradParams& p);
 
 int conv_wgrad_slabs(const WgradParams& p) {
   if (p.algo != 1 && conv3x3_wgrad_supported(p)) return conv3x3_wgrad_splits(p);
-  return WGRAD_REPLICAS;
+  return cfl_tune(TUNE_WGRAD_REPS) > 0 ? cfl_tune(TUNE_WGRAD_REPS) : WGRAD_REPLICAS;
 }
 
 bool conv_wgrad_plain_slabs(const WgradParams& p) { return p.algo != 1 && conv3x3_wgrad_supported(p); }

@@ -551,7 +551,8 @@ enum TuneKey {
   TUNE_PWB_BLOCKS = 55,        // fused pointwise backward (pw_bwd.hip): grid (default 384 at N = 32, 256 at N = 64)
   TUNE_PWB = 56,               // encoder pointwise backward: 0 = fused dgrad + wgrad (pw_bwd.hip), 1 = pw.hip dgrad +
                                //   deferred wgrad (round 5)
-  TUNE_N = 57
+  TUNE_WGRAD_REPS = 57,         // generic weight-gradient replica rows (conv_wgrad_slabs; default WGRAD_REPLICAS)
+  TUNE_N = 58
 };
 int cfl_tune(int key);
 void cfl_set_tune(int key, int value);
