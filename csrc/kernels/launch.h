@@ -213,7 +213,7 @@ int conv_wgrad(const WgradParams& p, hipStream_t st);
 int conv_wgrad_batch(const WgradParams* ps, int n, hipStream_t st);
 int conv_wgrad_slabs(const WgradParams& p);
 bool conv_wgrad_plain_slabs(const WgradParams& p);   // slab rows are plain-stored (else atomic replica rows)
-#define WGRAD_REPLICAS 16
+#define WGRAD_REPLICAS 8     // 16 -> 8 in round 6: grad_finish -3 us, bench +0.3 % (profiles/r6_misc)
 
 // ---------------------------------------------------------------- fused pointwise backward (pw_bwd.hip)
 // dgrad + wgrad of a pointwise conv whose output feeds a BatchNorm, the BN backward folded in:
