@@ -18,6 +18,8 @@ Layouts: activations NHWC bf16; master weights, grads, Adam moments fp32 in one 
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import math
 import os
 from dataclasses import dataclass
@@ -32,6 +34,22 @@ from .spec import DEC_FILTERS, ENC_FILTERS, ENTRY_FILTERS, ParamTable
 
 PK_CONV, PK_CONV_DGRAD1x1, PK_CONVT, PK_CONVT_DGRAD, PK_PW, PK_PW_DGRAD = range(6)
 GM_NONE, GM_SAME, GM_SCATTER2, GM_SUM2X2, GM_MAXPOOL = range(5)
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """Collect garbage now and keep the collector off for the block: a hipGraph capture (global capture mode) must not
+    run a destructor of an unreachable object from an earlier engine - a CUDAGraph's private pool release or a
+    pinned-block event query is a prohibited call during capture and aborts the process (seen in the GPU test suite
+    after the FL tests: an engine cycle collected mid-capture)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 @dataclass
@@ -857,14 +875,14 @@ class UNetEngine:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _no_gc(), torch.cuda.graph(g):
             self.train_step_eager()
         self.graph = g
         # the same launch sequence split after the encoder forward into two graphs sharing the step's buffers (the
         # engine allocates nothing during capture): replayed only for the first step after a FedAvg
         pre, post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.dev)
-        with torch.cuda.stream(s):
+        with _no_gc(), torch.cuda.stream(s):
             pre.capture_begin()
 
             def split():
@@ -934,7 +952,7 @@ class UNetEngine:
             torch.cuda.current_stream(self.dev).wait_stream(s)
             torch.cuda.synchronize(self.dev)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _no_gc(), torch.cuda.graph(g):
                 self.forward(False)
             self.eval_graph = g
         self.eval_graph.replay()
