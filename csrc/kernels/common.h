@@ -449,6 +449,49 @@ CFL_DEVICE void bnb_prologue(const BnBwdIn& q, int C, float* co, float* part, bo
 // dx of 8 channels c0..c0+7 from 8 g and 8 y values (coefficients from bnb_prologue's LDS block)
 // (co 16-byte aligned, C and c0 multiples of 8: the five coefficient rows are read as 16-byte vectors - 10 LDS reads
 // per call instead of 40 scalar ones)
+// Global -> LDS copy of NP 16-byte pieces (piece e: src(e) -> dst(e), pointers) by an NTH-thread block, the loads of
+// up to G pieces per thread issued before their stores. A strided `for (e = tid; e < NP; e += NTH)` copy compiled
+// to one full memory round trip per iteration - measured as most of the 3-6 us per-block prologues of the streaming
+// kernels (tools/block_timeline.py phases, profiles/r6_misc).
+template <int NTH, int NP, int G = 8, typename Src, typename Dst>
+CFL_DEVICE void stage16(const Src& src, const Dst& dst) {
+  constexpr int PT = (NP + NTH - 1) / NTH;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i0 = 0; i0 < PT; i0 += G) {
+    u4v r[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+      if (i0 + i < PT) r[i] = *reinterpret_cast<const u4v*>(src(imin(tid + (i0 + i) * NTH, NP - 1)));
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int e = tid + (i0 + i) * NTH;
+      if (i0 + i < PT && e < NP) *reinterpret_cast<u4v*>(dst(e)) = r[i];
+    }
+  }
+}
+
+// The same copy split in two: load() issues every piece (kept in registers), store() writes them - so the loads can
+// be issued together with other prologue loads ahead of an unrelated wait
+template <int NTH, int NP>
+struct Stage16 {
+  static constexpr int PT = (NP + NTH - 1) / NTH;
+  u4v r[PT];
+  template <typename Src>
+  CFL_DEVICE void load(const Src& src) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) r[i] = *reinterpret_cast<const u4v*>(src(imin((int)threadIdx.x + i * NTH, NP - 1)));
+  }
+  template <typename Dst>
+  CFL_DEVICE void store(const Dst& dst) const {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = threadIdx.x + i * NTH;
+      if (e < NP) *reinterpret_cast<u4v*>(dst(e)) = r[i];
+    }
+  }
+};
+
 // The five coefficient vectors of channels c0..c0+7 in registers, for callers that apply them to many pixels
 // (pw_bwd.hip: a thread's channel group is fixed for the whole launch)
 struct BnbCo8 {

@@ -477,12 +477,22 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
   const bool has_ab = p.xf.ab != nullptr;
   const int relu = p.xf.relu;
 
-  // ---- all weights of this column block: piece e -> (row = (ch*9 + tap)*BN_ + n, quarter q) ----
-  for (int e = tid; e < CH * 9 * BN_ * 4; e += NT) {
+  // ---- all weights of this column block: piece e -> (row = (ch*9 + tap)*BN_ + n, quarter q). Every piece's load
+  //      is issued (index clamped) before the first LDS store: the strided copy loop waited one full memory round
+  //      trip per iteration (5 / 9 of them per block, most of a block's time at 2-3 tiles per block).
+  constexpr int WP = CH * 9 * BN_ * 4, WPT = (WP + NT - 1) / NT;
+  u4v wr[WPT];
+#pragma unroll
+  for (int i = 0; i < WPT; ++i) {
+    const int e = imin(tid + i * NT, WP - 1);
     const int row = e >> 2, q = e & 3;
     const int n = row % BN_, ct = row / BN_, ch = ct / 9, tap = ct - ch * 9;
-    *reinterpret_cast<uint4*>(sB + swz_off(row, q)) = *reinterpret_cast<const uint4*>(
-        p.wt + (size_t)(nBlock + n) * p.K + (size_t)tap * p.Cin + ch * BK + q * 8);
+    wr[i] = *reinterpret_cast<const u4v*>(p.wt + (size_t)(nBlock + n) * p.K + (size_t)tap * p.Cin + ch * BK + q * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < WPT; ++i) {
+    const int e = tid + i * NT;
+    if (e < WP) *reinterpret_cast<u4v*>(sB + swz_off(e >> 2, e & 3)) = wr[i];
   }
   // producer BN coefficients of this thread's channel quarter, per chunk (constant over the block's tiles); XFIN:
   // computed here from the producer's replica sums (consumer-side finalize, first block writes the ab rows)
@@ -594,6 +604,7 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
   if (item < n_items) load_halo(item);
   if (item < n_items) store_halo();
   __syncthreads();
+  cfl_ts_phase(0);
   for (; item < n_items; item += gridDim.x) {
     const int next = item + gridDim.x;
     if (next < n_items) load_halo(next);               // in flight during this tile's MFMAs
@@ -681,6 +692,7 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
     }
     __syncthreads();                                    // next halo visible, C tile consumed
   }
+  cfl_ts_phase(1);
   if (p.stats || node || (pj && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)

@@ -601,6 +601,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
   uint2 rg[SR + 1], rx[SR + 1];
   uint32_t okg = 0, okx = 0;
   const bf16_t* hsrc = p.add_half ? p.add_half : p.dy;
+  cfl_ts_phase(0);
   for (int s = 0; s < nsteps; ++s) {
     const int a = ybeg + s * SR;
     const bool more = s + 1 < nsteps;
@@ -726,6 +727,7 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
     }
     __syncthreads();
   }
+  cfl_ts_phase(1);
 
   // block reduction of the 9 tap sums (+ the 2 node sums), one atomic per (row, channel) into replica rows
   const int lane = tid & 63, wid = tid >> 6;

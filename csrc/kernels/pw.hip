@@ -133,14 +133,15 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
   for (int d = 0; d < D; ++d)
     if (t + d * wstride < tiles) load(d, t + d * wstride);
 
-  for (int c = tid; c < NB * K / 8; c += NT) {
-    const int n = c / (K / 8), kc = c - n * (K / 8);
-    *reinterpret_cast<uint4*>(sW + (kc >> 2) * NB * 32 + wswz(n, kc & 3)) =
-        *reinterpret_cast<const uint4*>(p.wt + (size_t)(n0 + n) * K + kc * 8);
-  }
-  if (tid < NB) sBias[tid] = p.bias ? p.bias[n0 + tid] : 0.f;
+  // the weight slice, bias and (BWD) the BN-backward replica rows are issued together with the first tiles: the
+  // prologue waits one memory round trip (a strided weight-copy loop waited one per iteration: ~6 us per block)
+  Stage16<NT, NB * K / 8> wst;
+  wst.load([&](int c) { const int n = c / (K / 8), kc = c - n * (K / 8); return p.wt + (size_t)(n0 + n) * K + kc * 8; });
+  const float bias_v = p.bias ? p.bias[n0 + imin(tid, NB - 1)] : 0.f;
   if constexpr (BWD) bnb_prologue<NT>(p.bwd, K, sco, sco + 5 * K, bid == 0);   // ends with a barrier
-  else __syncthreads();
+  wst.store([&](int c) { const int n = c / (K / 8), kc = c - n * (K / 8); return sW + (kc >> 2) * NB * 32 + wswz(n, kc & 3); });
+  if (tid < NB) sBias[tid] = bias_v;
+  __syncthreads();
 
   const bool stats = p.stats != nullptr;
   float s1[NF][4], s2[NF][4];
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
 #pragma unroll
     for (int r = 0; r < 4; ++r) s1[nf][r] = s2[nf][r] = 0.f;
 
+  cfl_ts_phase(0);
   for (; t < tiles; t += D * wstride) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -250,6 +252,7 @@ __global__ __launch_bounds__(NT, 2) void pw_kernel(const ConvParams p, int nslic
     }
   }
 
+  cfl_ts_phase(1);
   if (!stats) return;
   // lanes of one q group hold the same 4 channels per fragment column: reduce over r16, then over the 4 waves
 #pragma unroll

@@ -117,6 +117,15 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
   uint4 v0[PPT0];
   uint32_t ok0;
   sep_fetch<K, N, TW, RS + 2>(p, img, x0, ybeg - 1, true, v0, ok0);
+  // the block's weights, depthwise taps and bias issued with the first rows: the prologue waits one round trip
+  // (a strided weight-copy loop after the ring fill waited one per iteration: 4-5 us per block before the loop)
+  Stage16<NT, N * K / 8> wst;
+  wst.load([&](int c) { const int n = c / (K / 8), kc = c - n * (K / 8); return p.wpw + (size_t)n * K + kc * 8; });
+  const float bias_v = p.bias ? p.bias[imin(tid, N - 1)] : 0.f;
+  constexpr int WDT = (9 * K + NT - 1) / NT;
+  float wd[WDT];
+#pragma unroll
+  for (int i = 0; i < WDT; ++i) wd[i] = p.wdw[imin(tid + i * NT, 9 * K - 1)];
 
   // this thread's channel group (fixed: NT % CQ == 0) and its transform coefficients
   const int cq = tid % S::CQ;
@@ -145,13 +154,11 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
   }
   const int relu = p.xf.relu;
   sep_put<K, N, TW, RS + 2>(ring, v0, ok0, ybeg - 1, has_ab || relu, a8, b8, relu);
-  for (int c = tid; c < N * K / 8; c += NT) {
-    const int n = c / (K / 8), kc = c - n * (K / 8);
-    *reinterpret_cast<uint4*>(sW + (kc >> 2) * N * 32 + wswz(n, kc & 3)) =
-        *reinterpret_cast<const uint4*>(p.wpw + (size_t)n * K + kc * 8);
-  }
-  for (int e = tid; e < 9 * K; e += NT) sWd[e] = p.wdw[e];
-  if (tid < N) sBias[tid] = p.bias ? p.bias[tid] : 0.f;
+  wst.store([&](int c) { const int n = c / (K / 8), kc = c - n * (K / 8); return sW + (kc >> 2) * N * 32 + wswz(n, kc & 3); });
+#pragma unroll
+  for (int i = 0; i < WDT; ++i)
+    if (tid + i * NT < 9 * K) sWd[tid + i * NT] = wd[i];
+  if (tid < N) sBias[tid] = bias_v;
   __syncthreads();
 
   const bool stats = p.stats != nullptr;
@@ -164,6 +171,7 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
   const int px0 = (wid % S::WT) * 16;                        // this wave's tile column
   uint4 vn[PPT];
   uint32_t okn = 0;
+  cfl_ts_phase(0);
   for (int s = 0; s < nsteps; ++s) {
     const int a = ybeg + s * RS;
     const bool more = s + 1 < nsteps;
@@ -244,6 +252,7 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
     __syncthreads();
   }
 
+  cfl_ts_phase(1);
   if (!stats) return;
   float (*sred)[NT / 64][N] = reinterpret_cast<float (*)[NT / 64][N]>(ring);   // the loop ended on a barrier
   static_assert(2 * (NT / 64) * N * 4 <= S::RING * 2, "statistics staging fits the ring");

@@ -87,16 +87,23 @@ def main():
         f(*args, **kw)
         torch.cuda.synchronize()
         C.set_ts(None)
-        t = buf.cpu().numpy()[:CAP // 2]          # the upper half holds in-kernel phase stamps (cfl_ts_phase)
-        t = t[t[:, 0] != 0]
+        full = buf.cpu().numpy()
+        t, ph = full[:CAP // 2], full[CAP // 2:]   # the upper half holds in-kernel phase stamps (cfl_ts_phase)
+        keep = t[:, 0] != 0
+        t, ph = t[keep], ph[keep]
         if len(t) == 0:
             continue
         s, e = t[:, 0].astype(np.float64) / 100.0, t[:, 1].astype(np.float64) / 100.0   # us
         d = e - s
         span = e.max() - s.min()
         tot += span
+        extra = ""
+        if len(ph) and (ph[:, 0] != 0).all() and (ph[:, 1] != 0).all():   # phases: prologue | loop | epilogue
+            p0, p1 = ph[:, 0] / 100.0, ph[:, 1] / 100.0
+            extra = (f"   [phases: prologue {np.median(p0 - s):.1f}, loop {np.median(p1 - p0):.1f}, "
+                     f"epilogue {np.median(e - p1):.1f}]")
         print(f"{span:7.1f} {s.max() - s.min():6.1f} {np.median(d):6.1f} {d.max():6.1f} "
-              f"{e.max() - np.percentile(e, 90):6.1f} {len(t):6d}  {shape_key(name, args, kw)}", flush=True)
+              f"{e.max() - np.percentile(e, 90):6.1f} {len(t):6d}  {shape_key(name, args, kw)}{extra}", flush=True)
     print(f"{tot:7.1f} total span (us)")
 
 
