@@ -572,20 +572,30 @@ __global__ __launch_bounds__(NT, 2) void dw_bwd_stream_kernel(DwParams p, int re
   const size_t img = (size_t)b * p.H * p.W * p.C + c0;
   const bf16_t* g_b = p.dy + img;
   const bf16_t* x_b = p.x + img;
-  float a4[4], b4[4];
-  load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
-  load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
-  for (int e = tid; e < 9 * CT; e += NT) {
-    const int t = e / CT, c = e - t * CT;
-    sW[e] = p.w[(8 - t) * p.C + cbase + c];
-  }
   constexpr bool node = NODE;
-  if (node && tid < 4 * CT) sNode[tid] = p.node.ab[(tid / CT) * p.C + cbase + tid % CT];
+  float a4[4], b4[4];
   {
+    // the first rows, the flipped taps, the node coefficients and the producer coefficients all issued before the
+    // first wait (the strided tap copy waited one memory round trip per iteration)
     uint2 v[SR + 3], u[SR + 3];
     uint32_t okv, oku;
     fetch<SR + 2>(g_b, p, x0, ybeg - 1, true, v, okv);
     fetch<SR + 2>(x_b, p, x0, ybeg - 1, true, u, oku);
+    constexpr int WT = (9 * CT + NT - 1) / NT;
+    float wv[WT];
+#pragma unroll
+    for (int i = 0; i < WT; ++i) {
+      const int e = imin(tid + i * NT, 9 * CT - 1), t = e / CT, c = e - t * CT;
+      wv[i] = p.w[(8 - t) * p.C + cbase + c];
+    }
+    const int ne = imin(tid, 4 * CT - 1);
+    const float nv = node ? p.node.ab[(ne / CT) * p.C + cbase + ne % CT] : 0.f;
+    load_f4_or(p.xf.ab + c0, has_ab, 1.f, a4);
+    load_f4_or(p.xf.ab + p.xf.C + c0, has_ab, 0.f, b4);
+#pragma unroll
+    for (int i = 0; i < WT; ++i)
+      if (tid + i * NT < 9 * CT) sW[tid + i * NT] = wv[i];
+    if (node && tid < 4 * CT) sNode[tid] = nv;
     put<SR + 2, false>(sG, v, okv, ybeg - 1, false, a4, b4, 0);
     put<SR + 2, false>(sX, u, oku, ybeg - 1, has_ab || relu, a4, b4, relu);   // transformed x (padding stays zero)
   }
