@@ -138,6 +138,7 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) ns0[k] = ns1[k] = 0.f;
   const int stride = gridDim.x * NT;
+  cfl_ts_phase(0);
   for (int t0 = blockIdx.x * NT + threadIdx.x; (t0 >> 2) < npix; t0 += HPT * stride) {
     float f[HPT][8], hv[HPT], tt[HPT], yn[NODE ? HPT : 1][8];
     int pix[HPT];
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
       }
     }
   }
+  cfl_ts_phase(1);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if constexpr (FWD) {
     double v[7] = {bce, cor, mI, mP, mT, TP, PP};
