@@ -506,7 +506,7 @@ enum TuneKey {
   TUNE_WGRAD1_MINPIX = 19,     // generic (1x1) wgrad: min pixels per block (default 512)
   TUNE_NODE_BWD_IPT = 20,      // node_bwd: items in flight per thread (2 or 4; default 2)
   TUNE_DW_BWD_BLOCKS = 21,     // fused depthwise backward: target grid size (default 512)
-  TUNE_BBA_BLOCKS = 22,        // bn_bwd_apply grid cap (default 1024)
+  TUNE_BBA_BLOCKS = 22,        // bn_bwd_apply grid cap (default 256)
   TUNE_NODE_POOL_BLOCKS = 23,  // max-pool node gradient grid cap (default: TUNE_NODE_BWD_BLOCKS / 512)
   TUNE_WGRAD1_RM = 24,         // generic wgrad 64x64 tiles: pixels per pipeline stage (0 = 64, 128)
   TUNE_PW = 25,                // plain 1x1 convs: 0 = streaming kernel (pw.hip), 1 = conv_igemm tiles
