@@ -20,14 +20,20 @@ CFL_DEVICE s4v tr_read(const bf16_t* p) {
 }
 
 // halo rows: CBT input channels + 16 bf16 of padding (96 / 160 bytes, see the layout note in conv3x3_wgrad.hip)
+#ifndef WG3_HPAD
+#define WG3_HPAD 16
+#endif
+#ifndef WG3_DPAD
+#define WG3_DPAD 16
+#endif
 template <int CBT>
-constexpr int ldh() { return CBT + 16; }
+constexpr int ldh() { return CBT + WG3_HPAD; }
 
 // LDS bytes of one block of the (BNO, CBT) config: two halo images + two dy tiles, SB (single buffer): one of each
 // (the caller owns the allocation, so a grouped launch of several wgrad kinds can share one buffer: conv_wgrad.hip
 // wgrad_mix_kernel)
 template <int BNO, int CBT = CB, bool SB = false>
-constexpr int wgrad3_lds_bytes() { return (SB ? 1 : 2) * (HP * ldh<CBT>() * 2 + TP * (BNO + 16) * 2); }
+constexpr int wgrad3_lds_bytes() { return (SB ? 1 : 2) * (HP * ldh<CBT>() * 2 + TP * (BNO + WG3_DPAD) * 2); }
 
 // TR: accumulate D[n][c] instead of D[c][n] so that the 16 contiguous accumulator columns land on contiguous
 // addresses of the destination layout (c for the Conv2DTranspose (kh,kw,out,in) layout, n for HWIO): each atomic
@@ -43,7 +49,7 @@ CFL_DEVICE void wgrad3_body(const WgradParams& p, int tiles_total, int splits, i
   constexpr int COMBOS = (CBT / 16) * NF;   // (c fragment, n fragment) pairs per tap
   constexpr int CPW = COMBOS / 4;           // combos per wave
   constexpr int LDH = ldh<CBT>();
-  constexpr int LDD = BNO + 16;    // 96 / 160-byte dy rows
+  constexpr int LDD = BNO + WG3_DPAD;    // 96 / 160-byte dy rows
   constexpr int QP = CBT / 8;               // 16-byte pieces per halo pixel
   constexpr int HALO_CH = HP * QP, H_PER_T = (HALO_CH + NT - 1) / NT;
   constexpr int D_CH = TP * (BNO / 8), D_PER_T = (D_CH + NT - 1) / NT;
