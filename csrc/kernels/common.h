@@ -131,9 +131,41 @@ CFL_DEVICE int xcd_block_linear() {
   return xcd_swizzle(lin, gridDim.x * gridDim.y * gridDim.z);
 }
 
+// v + (v of lane ^ o) for o in {1, 2, 4, 8, 16, 32} without the LDS crossbar: DPP lane moves within a 16-lane row
+// (quad_perm, row_mirror, row_half_mirror; xor 4 / 8 as two of them) and gfx950's v_permlane16 / 32_swap across rows
+// (swap(v, v) leaves v_i and v_(i^16) in the two results: their sum is v_i + v_(i^16) in every lane). The value in
+// every lane is bit-identical to `v + __shfl_xor(v, o, 64)` (the partners are the same, fp add commutes); o must
+// fold to a constant (unrolled loops). __shfl_xor was one ds_bpermute - an LDS round trip - per step: the BN
+// statistics / wgrad reductions of the kernel epilogues ran hundreds of them per block.
+template <int CTRL>
+CFL_DEVICE float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+CFL_DEVICE float xor_add(float v, int o) {
+  constexpr int QP_1032 = 0xB1, QP_2301 = 0x4E, QP_3210 = 0x1B, ROW_MIRROR = 0x140, ROW_HALF_MIRROR = 0x141;
+  if (o == 1) return v + dppf<QP_1032>(v);
+  if (o == 2) return v + dppf<QP_2301>(v);
+  if (o == 4) return v + dppf<ROW_HALF_MIRROR>(dppf<QP_3210>(v));
+  if (o == 8) return v + dppf<ROW_HALF_MIRROR>(dppf<ROW_MIRROR>(v));
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  if (o == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+// the value of lane ^ 16 (an exchange, not a sum): v_permlane16_swap leaves the partner in the first result on
+// odd rows (lanes 16-31, 48-63) and in the second on even rows
+CFL_DEVICE unsigned xor16_get(unsigned v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (threadIdx.x & 16) ? (unsigned)r[0] : (unsigned)r[1];
+}
+
 CFL_DEVICE float wave_sum(float v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o > 0; o >>= 1) v = xor_add(v, o);
   return v;
 }
 
@@ -273,7 +305,8 @@ CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* bu
   for (int k = 0; k < NS; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      for (int o = G; o < 64; o <<= 1) s[k][j] += __shfl_xor(s[k][j], o, 64);
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) s[k][j] = xor_add(s[k][j], o);
   if (lane < G) {
 #pragma unroll
     for (int k = 0; k < NS; ++k)

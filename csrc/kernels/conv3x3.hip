@@ -415,9 +415,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_kernel(ConvParams p, int chunks
   if (p.stats || node || (pj && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
+#pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
-        s[0][q] += __shfl_xor(s[0][q], o, 64);
-        s[1][q] += __shfl_xor(s[1][q], o, 64);
+        s[0][q] = xor_add(s[0][q], o);
+        s[1][q] = xor_add(s[1][q], o);
       }
     if (lane < CG) {
 #pragma unroll
@@ -696,9 +697,10 @@ __global__ __launch_bounds__(NT, CH == 1 && !PJ ? 3 : 2) void conv3x3_ws_kernel(
   if (p.stats || node || (pj && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
+#pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
-        s[0][q] += __shfl_xor(s[0][q], o, 64);
-        s[1][q] += __shfl_xor(s[1][q], o, 64);
+        s[0][q] = xor_add(s[0][q], o);
+        s[1][q] = xor_add(s[1][q], o);
       }
     if (lane < CG) {
 #pragma unroll

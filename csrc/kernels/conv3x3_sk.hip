@@ -402,9 +402,10 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_sk_kernel(ConvParams p) {
   if (p.stats || node || (PJ && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
+#pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
-        s[0][q] += __shfl_xor(s[0][q], o, 64);
-        s[1][q] += __shfl_xor(s[1][q], o, 64);
+        s[0][q] = xor_add(s[0][q], o);
+        s[1][q] = xor_add(s[1][q], o);
       }
     if (lane < CG) {
 #pragma unroll

@@ -345,9 +345,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvParams p, int kt_
   if (p.stats || node) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
+#pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
-        s[q] += __shfl_xor(s[q], o, 64);
-        s2[q] += __shfl_xor(s2[q], o, 64);
+        s[q] = xor_add(s[q], o);
+        s2[q] = xor_add(s2[q], o);
       }
     if (lane < CG) {
 #pragma unroll
@@ -411,9 +412,10 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
   if (!p.stats && !node) return;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
+#pragma unroll
     for (int o = G; o < 64; o <<= 1) {
-      s[q] += __shfl_xor(s[q], o, 64);
-      s2[q] += __shfl_xor(s2[q], o, 64);
+      s[q] = xor_add(s[q], o);
+      s2[q] = xor_add(s2[q], o);
     }
   if (lane < G) {
 #pragma unroll

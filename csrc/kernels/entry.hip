@@ -128,7 +128,8 @@ __global__ __launch_bounds__(NT) void entry_wgrad_kernel(EntryParams p, int repl
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = acc[a][j];
-      for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) v = xor_add(v, o);
       acc[a][j] = v;
     }
   if (lane < G) {

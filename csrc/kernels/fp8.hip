@@ -452,9 +452,10 @@ __global__ __launch_bounds__(F8_NT, 2) void conv3x3_f8_kernel(ConvParams p) {
   if (p.stats || node || (PJ && p.pj.sums)) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
+#pragma unroll
       for (int o = CG; o < 64; o <<= 1) {
-        s2[0][q] += __shfl_xor(s2[0][q], o, 64);
-        s2[1][q] += __shfl_xor(s2[1][q], o, 64);
+        s2[0][q] = xor_add(s2[0][q], o);
+        s2[1][q] = xor_add(s2[1][q], o);
       }
     if (lane < CG) {
 #pragma unroll

@@ -66,8 +66,8 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
       float h = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) h = fmaf(f[u][k], w[k], h);
-      h += __shfl_xor(h, 1, 64);        // commutative pairings: all 4 lanes end with the same bits
-      h += __shfl_xor(h, 2, 64);
+      h = xor_add(h, 1);        // commutative pairings: all 4 lanes end with the same bits
+      h = xor_add(h, 2);
       h += bias;
       if (pix[u] < 0) continue;
       if (q == 0) p.h[pix[u]] = h;
@@ -158,8 +158,8 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
         float h = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) h = fmaf(f[u][k], w[k], h);
-        h += __shfl_xor(h, 1, 64);
-        h += __shfl_xor(h, 2, 64);
+        h = xor_add(h, 1);
+        h = xor_add(h, 2);
         h += bias;
         hv[u] = h;
         if (pix[u] < 0) continue;
@@ -180,8 +180,8 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
       const float sg = 1.f / (1.f + expf(-hv[u]));
       float dh = (sg - tt[u]) * inv_n;
       if (p.dice) dh += (dI * tt[u] + dP) * sg * (1.f - sg);
-      dh += __shfl_xor(dh, 1, 64);      // the pixel's gradient: sum over its 2x2 target block
-      dh += __shfl_xor(dh, 2, 64);
+      dh = xor_add(dh, 1);      // the pixel's gradient: sum over its 2x2 target block
+      dh = xor_add(dh, 2);
       if (pix[u] < 0) continue;
       if (q == 0) gb += dh;
       float o[8];
@@ -216,7 +216,8 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k)
-    for (int o = 4; o < 64; o <<= 1) gw[k] += __shfl_xor(gw[k], o, 64);   // lanes of one q hold the same channels
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) gw[k] = xor_add(gw[k], o);   // lanes of one q hold the same channels
   gb = wave_sum(gb);
   if (lane < 4) {
 #pragma unroll
@@ -226,9 +227,10 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
   if constexpr (NODE) {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
+#pragma unroll
       for (int o = 4; o < 64; o <<= 1) {
-        ns0[k] += __shfl_xor(ns0[k], o, 64);
-        ns1[k] += __shfl_xor(ns1[k], o, 64);
+        ns0[k] = xor_add(ns0[k], o);
+        ns1[k] = xor_add(ns1[k], o);
       }
     if (lane < 4) {
 #pragma unroll

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(NT, 2) void pw_bwd_kernel(const PwBwdParams p) {
         const uint2 u0 = make_uint2(pack2bf(x0[0], x0[1]), pack2bf(x0[2], x0[3]));
         const uint2 u1 = make_uint2(pack2bf(x1[0], x1[1]), pack2bf(x1[2], x1[3]));
         const uint2 give = odd ? u0 : u1;
-        const uint2 got = make_uint2(__shfl_xor(give.x, 16, 64), __shfl_xor(give.y, 16, 64));
+        const uint2 got = make_uint2(xor16_get(give.x), xor16_get(give.y));
         const uint4 v = odd ? make_uint4(got.x, got.y, u1.x, u1.y) : make_uint4(u0.x, u0.y, got.x, got.y);
         *reinterpret_cast<uint4*>(p.dd + m * N + (2 * cg + odd) * 16 + (q >> 1) * 8) = v;
       }

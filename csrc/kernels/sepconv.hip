@@ -230,7 +230,7 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
         const uint2 u0 = make_uint2(pack2bf(c0[0] + b0.x, c0[1] + b0.y), pack2bf(c0[2] + b0.z, c0[3] + b0.w));
         const uint2 u1 = make_uint2(pack2bf(c1[0] + b1.x, c1[1] + b1.y), pack2bf(c1[2] + b1.z, c1[3] + b1.w));
         const uint2 give = odd ? u0 : u1;
-        const uint2 got = make_uint2(__shfl_xor(give.x, 16, 64), __shfl_xor(give.y, 16, 64));
+        const uint2 got = make_uint2(xor16_get(give.x), xor16_get(give.y));
         const uint4 v = odd ? make_uint4(got.x, got.y, u1.x, u1.y) : make_uint4(u0.x, u0.y, got.x, got.y);
         *reinterpret_cast<uint4*>(p.y + m * N + (2 * h + odd) * 16 + (q >> 1) * 8) = v;
         if (stats) {
@@ -262,8 +262,8 @@ __global__ __launch_bounds__(NT, 2) void sep_fwd_kernel(const SepParams p, int s
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        s1[nf][r] += __shfl_xor(s1[nf][r], o, 64);
-        s2[nf][r] += __shfl_xor(s2[nf][r], o, 64);
+        s1[nf][r] = xor_add(s1[nf][r], o);
+        s2[nf][r] = xor_add(s2[nf][r], o);
       }
   if (r16 == 0) {
 #pragma unroll
