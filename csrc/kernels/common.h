@@ -305,8 +305,8 @@ CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* bu
   for (int k = 0; k < NS; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int o = G; o < 64; o <<= 1) s[k][j] = xor_add(s[k][j], o);
+      for (int o = G; o < 64; o <<= 1) s[k][j] += __shfl_xor(s[k][j], o, 64);   // G is a runtime value here: xor_add
+                                                                                  // needs a constant o (measured slower)
   if (lane < G) {
 #pragma unroll
     for (int k = 0; k < NS; ++k)

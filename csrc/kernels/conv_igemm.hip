@@ -412,10 +412,9 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
   if (!p.stats && !node) return;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
-#pragma unroll
-    for (int o = G; o < 64; o <<= 1) {
-      s[q] = xor_add(s[q], o);
-      s2[q] = xor_add(s2[q], o);
+    for (int o = G; o < 64; o <<= 1) {         // runtime G: the LDS-crossbar shuffle (xor_add needs a constant o)
+      s[q] += __shfl_xor(s[q], o, 64);
+      s2[q] += __shfl_xor(s2[q], o, 64);
     }
   if (lane < G) {
 #pragma unroll
