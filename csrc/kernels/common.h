@@ -301,12 +301,29 @@ template <int NS>
 CFL_DEVICE void block_channel_atomics(float (&s)[NS][8], int G, int C, float* buf, size_t off, bool stats,
                                       float (*red)[4][256]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c0 = (threadIdx.x % G) * 8;
+  // the lane stride is a runtime value: dispatched to a constant-stride DPP / permlane reduction per G (xor_add with
+  // a runtime o measured slower than the LDS shuffle it replaces; other strides keep the shuffle)
+  auto reduce = [&](auto g_c) __attribute__((always_inline)) {
+    constexpr int GC = decltype(g_c)::value;
 #pragma unroll
-  for (int k = 0; k < NS; ++k)
+    for (int k = 0; k < NS; ++k)
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      for (int o = G; o < 64; o <<= 1) s[k][j] += __shfl_xor(s[k][j], o, 64);   // G is a runtime value here: xor_add
-                                                                                  // needs a constant o (measured slower)
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int o = GC; o < 64; o <<= 1) s[k][j] = xor_add(s[k][j], o);
+  };
+  switch (G) {
+    case 4: reduce(std::integral_constant<int, 4>{}); break;
+    case 8: reduce(std::integral_constant<int, 8>{}); break;
+    case 16: reduce(std::integral_constant<int, 16>{}); break;
+    case 32: reduce(std::integral_constant<int, 32>{}); break;
+    default:
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          for (int o = G; o < 64; o <<= 1) s[k][j] += __shfl_xor(s[k][j], o, 64);
+  }
   if (lane < G) {
 #pragma unroll
     for (int k = 0; k < NS; ++k)
