@@ -293,6 +293,29 @@ __host__ __device__ inline int ilog2(int x) {
   return l;
 }
 
+// v[i] + the v[i] of every lane congruent to this one mod G (G a runtime power of two): strides 4..32 on the
+// constant-stride DPP / permlane reductions (xor_add), anything else on the LDS shuffle
+template <int N>
+CFL_DEVICE void reduce_stride(float (&v)[N], int G) {
+  auto red = [&](auto g_c) __attribute__((always_inline)) {
+    constexpr int GC = decltype(g_c)::value;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int o = GC; o < 64; o <<= 1) v[i] = xor_add(v[i], o);
+  };
+  switch (G) {
+    case 4: red(std::integral_constant<int, 4>{}); break;
+    case 8: red(std::integral_constant<int, 8>{}); break;
+    case 16: red(std::integral_constant<int, 16>{}); break;
+    case 32: red(std::integral_constant<int, 32>{}); break;
+    default:
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        for (int o = G; o < 64; o <<= 1) v[i] += __shfl_xor(v[i], o, 64);
+  }
+}
+
 // Per-channel sums of 8-channel vectors held by a 256-thread block where thread t owns channel group t % G:
 // reduce the wave's lanes that share the group (stride G), then the 4 waves through LDS, then one atomic per
 // channel into buf[off + 0..C) and (if NS == 2) buf[off + C..2C) (red_add: float, or int64 fixed point in the

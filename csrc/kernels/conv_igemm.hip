@@ -410,12 +410,8 @@ __global__ __launch_bounds__(NT) void splitk_epilogue_kernel(ConvParams p, const
     *reinterpret_cast<uint4*>(p.y + (size_t)m * p.N + c0) = o;
   }
   if (!p.stats && !node) return;
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-    for (int o = G; o < 64; o <<= 1) {         // runtime G: the LDS-crossbar shuffle (xor_add needs a constant o)
-      s[q] += __shfl_xor(s[q], o, 64);
-      s2[q] += __shfl_xor(s2[q], o, 64);
-    }
+  reduce_stride(s, G);                         // runtime lane stride G (common.h)
+  reduce_stride(s2, G);
   if (lane < G) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
