@@ -156,6 +156,32 @@ CFL_DEVICE float xor_add(float v, int o) {
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+// the double form of xor_add: both 32-bit halves moved by the same lane permutation (bit-identical to
+// v + __shfl_xor(v, o, 64) on a double)
+template <int CTRL>
+CFL_DEVICE double dppd(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+CFL_DEVICE double xor_add(double v, int o) {
+  constexpr int QP_1032 = 0xB1, QP_2301 = 0x4E, QP_3210 = 0x1B, ROW_MIRROR = 0x140, ROW_HALF_MIRROR = 0x141;
+  if (o == 1) return v + dppd<QP_1032>(v);
+  if (o == 2) return v + dppd<QP_2301>(v);
+  if (o == 4) return v + dppd<ROW_HALF_MIRROR>(dppd<QP_3210>(v));
+  if (o == 8) return v + dppd<ROW_HALF_MIRROR>(dppd<ROW_MIRROR>(v));
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto l = o == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                         : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = o == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                         : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const double d0 = __builtin_bit_cast(double, ((unsigned long long)(unsigned)h[0] << 32) | (unsigned)l[0]);
+  const double d1 = __builtin_bit_cast(double, ((unsigned long long)(unsigned)h[1] << 32) | (unsigned)l[1]);
+  return d0 + d1;
+}
+
 // the value of lane ^ 16 (an exchange, not a sum): v_permlane16_swap leaves the partner in the first result on
 // odd rows (lanes 16-31, 48-63) and in the second on even rows
 CFL_DEVICE unsigned xor16_get(unsigned v) {

@@ -87,7 +87,8 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadParams p) {
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     double x = v[k];
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = xor_add(x, o);
     if (lane == 0) red[k][wid] = x;
   }
   __syncthreads();
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadParams p) {
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       double x = v[k];
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x = xor_add(x, o);
       if (lane == 0) mred[k][wid] = x;
     }
   }
