@@ -62,7 +62,7 @@ for (H, K, N) in [(128, 64, 32), (128, 64, 64)]:
     sums = torch.randn(16 * 2 * K, device=DEV)
     dd = torch.zeros(M, N, dtype=torch.int16, device=DEV)
     dy = torch.zeros(M, K, dtype=torch.int16, device=DEV)
-    rows = 16
+    rows = C.conv_wgrad_slabs(B, H, H, N, 0, H, H, K, 1, 1, 0, 0)[0]
     slab = torch.zeros(rows * N * K, device=DEV)
     dg, db = torch.zeros(K, device=DEV), torch.zeros(K, device=DEV)
     print(f"== H {H} K {K} N {N} M {M}: HBM floor g+y+d+dd {M * (2 * K + 2 * N) * 2 / 8e6:.1f} us at 8 TB/s", flush=True)
